@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident GF(2^8) encode of 10+4 x 16 MiB stripes.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): "device-resident encode MB/s (data+parity)" -- bytes of
+data + parity shards per second, MB = 2^20 (the reference's unit,
+CHANGELOG.md:59-63), over the whole job.  A *step* encodes one batch of
+`--stripes` independent 10+4 x 16 MiB stripes per GPU (default 512, so N = 8
+is BASELINE config 4's 4096 stripes) with ONE launch of the fused kernel
+(rse_encode_flat).  Every stripe occupies its own HBM (no re-use of cached
+bytes); stripes are split across ranks with no data-path collective
+("scaling": "weak").  Inputs are resident in HBM before the timed region.
+
+Also reported (not `value`): the kernel's HBM roofline fraction (HIP events on
+the launch stream), the reference's own SIMD CPU path on this host (rank 0,
+N = 1, bounded sample), reconstruct of 2 erased data shards, and the
+pinned-host end-to-end rate (PCIe-inclusive).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-erasure_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident encode MB/s (data+parity), 10+4 × 16 MiB shards, 1/2/4/8 GPU"
+MiB = 1 << 20
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SEED = 0x5EED
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--data-shards", type=int, default=10)
+    ap.add_argument("--parity-shards", type=int, default=4)
+    ap.add_argument("--shard-mib", type=int, default=16)
+    ap.add_argument("--stripes", type=int, default=512, help="stripes per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip reconstruct / e2e legs")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------- distribution
+def stripes_for_rank(total: int, rank: int, world: int) -> range:
+    """Contiguous block of global stripe ids for `rank` (weak scaling: every
+    rank gets the same count when world divides total)."""
+    per, extra = divmod(total, world)
+    start = rank * per + min(rank, extra)
+    return range(start, start + per + (1 if rank < extra else 0))
+
+
+def shard_id(global_stripe: int, i: int) -> int:
+    """PRNG stream of shard i of a stripe; stripe 0 uses ids 0..k-1, which is
+    what tests/golden's full-size digests were made from."""
+    return (global_stripe << 8) | i
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+# ------------------------------------------------------------ CPU baseline
+def cpu_baseline(k, p, shard_bytes, seconds):
+    """The reference's simd-accel path (simd_c/reedsolomon.c compiled from the
+    reference sources into oracle/_ref, driven in core.rs:481-509 loop order),
+    1 thread, on a bounded sample: one k+p stripe re-encoded for ~`seconds`."""
+    import numpy as np
+    from oracle import oracle as O
+    data = [O.splitmix_bytes(SEED, i, shard_bytes) for i in range(k)]
+    par = [np.zeros(shard_bytes, np.uint8) for _ in range(p)]
+    rows = np.ascontiguousarray(O.Codec(8, k, p).matrix()[k:])
+    if O.ref_available():
+        kind = "reference"
+        ref = O.ref()
+
+        def run():
+            ref.ref_gf8_code_some_slices(rows.ctypes.data_as(O._u8p), p, k, O._ptrs(data),
+                                         O._ptrs(par), shard_bytes)
+    else:
+        kind = "port"
+
+        def run():
+            O.code_some_slices(8, rows, data, par)
+    run()  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    mbps = n * (k + p) * shard_bytes / dt / MiB
+    return {"value": round(mbps, 1), "unit": "MB/s", "cores": 1, "kind": kind,
+            "sample": f"{n} encodes of one {k}+{p} x {shard_bytes // MiB} MiB stripe "
+                      f"({dt:.1f} s, 1 thread, reference simd_c kernel -O3 -march=haswell)"}
+
+
+def load_traffic(workload):
+    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary for
+    this workload (profiles/*pmc_traffic*.json, written by
+    tools/pmc_traffic.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("workload") == workload:
+            best = d
+    return best
+
+
+# ----------------------------------------------------------------- main
+def main(argv=None):
+    args = parse(argv)
+    world, rank, local = init_dist(args)
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix
+
+    k, p = args.data_shards, args.parity_shards
+    L = args.shard_mib * MiB
+    stripe_bytes = (k + p) * L
+    total_stripes = args.stripes * world
+    mine = stripes_for_rank(total_stripes, rank, world)
+    n_local = len(mine)
+    free, _ = torch.cuda.mem_get_info()
+    # one HBM region per stripe when it fits (it does on 288 GB); otherwise a
+    # pool far larger than the 256 MiB Infinity Cache, cycled.
+    pool = min(n_local, max(8, int(0.8 * free) // stripe_bytes))
+    buf = torch.empty(pool * stripe_bytes, dtype=torch.uint8, device="cuda")
+    v = buf.view(pool, k + p, L)
+    for s in range(pool):
+        for i in range(k):
+            fill_splitmix(v[s, i], SEED, shard_id(mine.start + s, i))
+    torch.cuda.synchronize()
+    r = R.galois_8.ReedSolomon(k, p)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        done = 0
+        while done < n_local:
+            cnt = min(pool, n_local - done)
+            r.encode_flat(buf, L, cnt)
+            done += cnt
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate: global stripe 0's parity equals the reference's digest
+    check = None
+    if rank == 0 and (k, p, L) == (10, 4, 16 * MiB):
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+        want = g["generated"]["full_size"][f"gf8_10_4_{16 * MiB}"]["parity_sha256"]
+        got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
+        check = got == want
+        if not check:
+            print("PARITY MISMATCH vs reference digests", file=sys.stderr)
+            sys.exit(3)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    bytes_all = args.steps * total_stripes * stripe_bytes
+    value = bytes_all / elapsed / MiB
+
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        extras = extra_legs(r, v, k, p, L, min(pool, 64), stream)
+
+    if rank == 0:
+        launches = -(-n_local // pool)
+        per_launch_bytes = n_local * stripe_bytes / launches
+        mean_ms = sum(kern_ms) / len(kern_ms) / launches
+        achieved = per_launch_bytes / (mean_ms * 1e-3) / 1e9
+        workload = f"gf8 {k}+{p} x {args.shard_mib} MiB encode, {pool} stripes/launch"
+        tr = load_traffic(workload)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
+                "kernel_ms_per_launch": round(mean_ms, 4),
+                "algorithmic_bytes_per_launch": int(per_launch_bytes)}
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(k, p, L, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 shards generated in HBM)",
+            "config": {"workload": workload, "field": "GF(2^8)", "data_shards": k,
+                       "parity_shards": p, "shard_bytes": L,
+                       "stripes_per_gpu_per_step": n_local, "global_stripes_per_step":
+                       total_stripes, "parallelism": f"stripes split over {world} GPU(s), no collective",
+                       "parity_check_vs_reference": check},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        line.update(extras)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def extra_legs(r, v, k, p, L, n_stripes, stream):
+    """Reconstruct (data shards 0 and 1 erased, BASELINE config 3) and the
+    pinned-host end-to-end encode (PCIe-inclusive; never `value`)."""
+    import torch
+    out = {}
+    present = [i not in (0, 1) for i in range(k + p)]
+    flat = v[:n_stripes].reshape(-1)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    r.reconstruct_data_flat(flat, L, n_stripes, present)
+    torch.cuda.synchronize()
+    reps = 5
+    a.record(stream)
+    for _ in range(reps):
+        r.reconstruct_data_flat(flat, L, n_stripes, present)
+    b.record(stream)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    rb = n_stripes * (k + 2) * L
+    out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased",
+                          "stripes": n_stripes, "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
+                          "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
+    # end to end from pinned host memory: one stripe, H2D data, D2H parity
+    hs = [v[0, i].cpu().pin_memory() for i in range(k)] + \
+         [torch.empty(L, dtype=torch.uint8).pin_memory() for _ in range(p)]
+    r.encode_host(hs)
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        r.encode_host(hs)
+    dt = (time.perf_counter() - t0) / reps
+    ok = all(torch.equal(hs[k + i], v[0, k + i].cpu()) for i in range(p))
+    out["end_to_end_pinned_host"] = {
+        "what": "rse_encode_host, 1 stripe from pinned host memory (H2D data + kernel + D2H parity)",
+        "MB_per_s": round((k + p) * L / dt / MiB, 1), "parity_matches_device": ok}
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+/*
+ * rse_hip.h -- C ABI of the MI355X-native Reed-Solomon erasure-coding library
+ * (librse_hip.so).  Drop-in for the hot path of rust-rse/reed-solomon-erasure
+ * v6.0.0: the codec API of core.rs (ReedSolomon<F>::new / encode / encode_sep /
+ * encode_single / encode_single_sep / verify / verify_with_buffer / reconstruct /
+ * reconstruct_data) over the galois_8 and galois_16 fields, plus the fused
+ * shard x matrix kernel that replaces code_some_slices (core.rs:481-509) and the
+ * native FFI kernel reedsolomon_gal_mul(_xor) (simd_c/reedsolomon.h:30-42).
+ *
+ * Conventions (mirroring the reference; see INTEGRATION.md for the Rust binding):
+ *  - Shards are DEVICE pointers (HBM) unless the function name ends in _host.
+ *  - Lengths are in field ELEMENTS, like Rust slice lengths: bytes for GF(2^8),
+ *    2-byte [u8;2] elements ({coefficient of x, constant}, galois_16.rs:49-51)
+ *    for GF(2^16).
+ *  - Return value: RSE_OK (0), one of the 13 reference errors (errors.rs:4-18,
+ *    numbered as wasm/src/lib.rs:11-24), or an RSE_ERR_* library status >= 100.
+ *  - On any error nothing is written (core.rs:673-676).
+ *  - Work is enqueued on `stream` (a hipStream_t; NULL = the legacy default
+ *    stream) and runs asynchronously, except verify*, whose boolean result
+ *    requires a stream synchronisation before returning.
+ *  - A codec is immutable after rse_codec_new except for its mutex-guarded
+ *    decode-matrix LRU cache (capacity 254, core.rs:24), so concurrent calls on
+ *    different streams are allowed (core.rs:349).
+ *  - The caller owns all shard memory; the library never frees caller buffers.
+ */
+#ifndef RSE_HIP_H
+#define RSE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define RSE_OK 0
+/* errors.rs:4-18, in declaration order */
+#define RSE_TOO_FEW_SHARDS 1
+#define RSE_TOO_MANY_SHARDS 2
+#define RSE_TOO_FEW_DATA_SHARDS 3
+#define RSE_TOO_MANY_DATA_SHARDS 4
+#define RSE_TOO_FEW_PARITY_SHARDS 5
+#define RSE_TOO_MANY_PARITY_SHARDS 6
+#define RSE_TOO_FEW_BUFFER_SHARDS 7
+#define RSE_TOO_MANY_BUFFER_SHARDS 8
+#define RSE_INCORRECT_SHARD_SIZE 9
+#define RSE_TOO_FEW_SHARDS_PRESENT 10
+#define RSE_EMPTY_SHARD 11
+#define RSE_INVALID_SHARD_FLAGS 12
+#define RSE_INVALID_INDEX 13
+/* library statuses (no reference counterpart: the reference panics or cannot fail) */
+#define RSE_ERR_INVALID_ARGUMENT 100 /* NULL pointer, unknown field, bad size */
+#define RSE_ERR_DEVICE 101           /* HIP runtime error; see rse_last_device_error */
+#define RSE_ERR_NO_MEMORY 102
+#define RSE_ERR_SINGULAR_MATRIX 103  /* matrix.rs:11-13 Error::SingularMatrix */
+
+#define RSE_FIELD_GF8 8   /* galois_8::Field,  ORDER 256   */
+#define RSE_FIELD_GF16 16 /* galois_16::Field, ORDER 65536 */
+
+typedef struct rse_codec rse_codec;
+typedef void *rse_stream_t; /* hipStream_t */
+
+/* Human-readable message; reference errors use errors.rs:20-38 verbatim. */
+const char *rse_strerror(int status);
+/* hipError_t of the last RSE_ERR_DEVICE on this thread (0 if none). */
+int rse_last_device_error(void);
+/* Library version string. */
+const char *rse_version(void);
+
+/* ---- codec: core.rs:343-923 ------------------------------------------ */
+/* ReedSolomon::new (core.rs:445-467): TooFewDataShards / TooFewParityShards /
+ * TooManyShards (data + parity > ORDER).  Builds the systematic matrix
+ * V * (V[0..k])^-1 (core.rs:430-436) on the host; touches no device. */
+int rse_codec_new(int field, size_t data_shards, size_t parity_shards, rse_codec **out);
+void rse_codec_free(rse_codec *codec);
+int rse_codec_field(const rse_codec *codec);
+size_t rse_codec_data_shard_count(const rse_codec *codec);   /* core.rs:469 */
+size_t rse_codec_parity_shard_count(const rse_codec *codec); /* core.rs:473 */
+size_t rse_codec_total_shard_count(const rse_codec *codec);  /* core.rs:477 */
+/* Copy the (k+p) x k encoding matrix, row-major, elem bytes per element. */
+int rse_codec_matrix(const rse_codec *codec, uint8_t *out, size_t out_bytes);
+
+/* encode (core.rs:597-611): shards[0..k] data, shards[k..k+p] parity (overwritten). */
+int rse_encode(const rse_codec *codec, void *const *shards, const size_t *lens,
+               size_t n_shards, rse_stream_t stream);
+/* encode_sep (core.rs:617-632) */
+int rse_encode_sep(const rse_codec *codec, const void *const *data, const size_t *data_lens,
+                   size_t n_data, void *const *parity, const size_t *parity_lens,
+                   size_t n_parity, rse_stream_t stream);
+/* encode_single (core.rs:545-562): i_data == 0 overwrites parity, later indices
+ * accumulate (core.rs:503-507).  Used by ShardByShard (core.rs:101-231). */
+int rse_encode_single(const rse_codec *codec, size_t i_data, void *const *shards,
+                      const size_t *lens, size_t n_shards, rse_stream_t stream);
+/* encode_single_sep (core.rs:576-592) */
+int rse_encode_single_sep(const rse_codec *codec, size_t i_data, const void *single,
+                          size_t single_len, void *const *parity, const size_t *parity_lens,
+                          size_t n_parity, rse_stream_t stream);
+/* verify (core.rs:637-651): *ok = 1 iff the parity matches.  Reads k+p shards
+ * once, writes nothing.  Synchronises `stream`. */
+int rse_verify(const rse_codec *codec, const void *const *shards, const size_t *lens,
+               size_t n_shards, int *ok, rse_stream_t stream);
+/* verify_with_buffer (core.rs:654-669): on RSE_OK the buffer holds the correct
+ * parity whether or not verification passed (core.rs:328-331). */
+int rse_verify_with_buffer(const rse_codec *codec, const void *const *shards,
+                           const size_t *lens, size_t n_shards, void *const *buffer,
+                           const size_t *buffer_lens, size_t n_buffer, int *ok,
+                           rse_stream_t stream);
+/* reconstruct / reconstruct_data (core.rs:680-695, 733-923) with the
+ * ReconstructShard semantics of (T, bool) (lib.rs:168-200): present[i] != 0
+ * marks shard i present; a missing shard's buffer must still have the common
+ * length (else IncorrectShardSize) and is overwritten.  In data-only mode
+ * missing parity buffers are neither checked nor touched (core.rs:805-806). */
+int rse_reconstruct(const rse_codec *codec, void *const *shards, const size_t *lens,
+                    const uint8_t *present, size_t n_shards, rse_stream_t stream);
+int rse_reconstruct_data(const rse_codec *codec, void *const *shards, const size_t *lens,
+                         const uint8_t *present, size_t n_shards, rse_stream_t stream);
+
+/* ---- flat contiguous stripes (wasm/src/lib.rs:45-73 ABI, many stripes) --- */
+/* `stripes` holds n_stripes consecutive stripes; each stripe is k+p shards of
+ * shard_len elements laid end to end (the wasm encode() layout).  One launch. */
+int rse_encode_flat(const rse_codec *codec, void *stripes, size_t shard_len,
+                    size_t n_stripes, rse_stream_t stream);
+/* Same layout; every stripe has the same erasure pattern `present[k+p]`
+ * (wasm reconstruct(): reconstruct_data semantics). */
+int rse_reconstruct_data_flat(const rse_codec *codec, void *stripes, size_t shard_len,
+                              size_t n_stripes, const uint8_t *present, rse_stream_t stream);
+
+/* ---- low level: the fused kernel itself ------------------------------ */
+/* outputs[r] (+)= sum_i rows[r*n_in + i] * inputs[i] over len elements.
+ * rows is HOST memory, n_out x n_in elements (GF(2^16): [u8;2] each).
+ * accumulate = 0 reproduces code_some_slices (core.rs:481-490, first input
+ * overwrites); accumulate = 1 XORs into the outputs (mul_slice_add). */
+int rse_code_shards(int field, const uint8_t *rows, size_t n_out, size_t n_in,
+                    const void *const *inputs, void *const *outputs, size_t len,
+                    int accumulate, rse_stream_t stream);
+/* The reference FFI kernel's contract (reedsolomon_gal_mul(_xor),
+ * simd_c/reedsolomon.h:30-42) on device memory: out = c*in (or out ^= c*in)
+ * over GF(2^8).  Returns RSE_OK; the whole length is processed (no tail). */
+int rse_gf8_mul_slice(uint8_t c, const void *in, void *out, size_t len, int xor_into,
+                      rse_stream_t stream);
+
+/* ---- device matrix inversion (matrix.rs:249-261 semantics) ----------- */
+/* Invert `batch` n x n GF(2^8) matrices (device memory, row-major, n <= 255),
+ * one workgroup per matrix.  singular[b] = 1 for a singular matrix. */
+int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, size_t n,
+                         size_t batch, rse_stream_t stream);
+
+/* ---- host-memory (end-to-end) path ----------------------------------- */
+/* encode with host shards: data staged H2D through pinned buffers, parity
+ * staged D2H, chunked and double-buffered on `stream`.  Synchronous. */
+int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *lens,
+                    size_t n_shards, rse_stream_t stream);
+
+/* ---- utilities (benchmarks and tests) -------------------------------- */
+/* Fill device memory with the splitmix64 byte stream of (seed, shard_id):
+ * 64-bit word w = mix(seed + shard_id * 2^40 + w), little endian. */
+int rse_fill_splitmix(void *dst, size_t nbytes, uint64_t seed, uint64_t shard_id,
+                      rse_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSE_HIP_H */

@@ -1,0 +1,758 @@
+// rse_codec.cpp -- host side of the drop-in: the ReedSolomon<F> codec of
+// core.rs:343-923 (validation, matrix construction, decode-matrix LRU cache,
+// reconstruct planning) above the fused HIP kernel, exported as the C ABI of
+// include/rse_hip.h.
+//
+// Differences from the reference are in HOW, never in WHAT:
+//  * code_some_slices (core.rs:481-509) makes k*p passes over memory; here one
+//    kernel launch reads each input once and writes each output once.
+//  * verify (core.rs:637-651) encodes into a scratch buffer and compares; here
+//    the compare is fused into the same pass and no buffer is written.
+//  * reconstruct (core.rs:733-923) regenerates missing data, then missing parity
+//    from all data; here the missing parity rows are composed with the decode
+//    rows on the host (exact GF algebra) so both come out of ONE pass over the k
+//    surviving shards.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <list>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rse_hip.h"
+#include "rse_field.hpp"
+#include "rse_kernels.hpp"
+
+namespace {
+
+using rse::CodeArgs;
+using rse::kMaxIn;
+using rse::kMaxOut;
+
+thread_local int g_last_hip_error = 0;
+
+int dev_fail(hipError_t e) {
+  g_last_hip_error = (int)e;
+  return e == hipErrorOutOfMemory ? RSE_ERR_NO_MEMORY : RSE_ERR_DEVICE;
+}
+#define RSE_HIP(call)                              \
+  do {                                             \
+    hipError_t e_ = (call);                        \
+    if (e_ != hipSuccess) return dev_fail(e_);     \
+  } while (0)
+
+constexpr size_t kCacheCapacity = 254;  // core.rs:24 DATA_DECODE_MATRIX_CACHE_CAPACITY
+
+// Row-major coefficient block handed to the kernel (uint16 elements).
+struct Rows {
+  size_t n_out = 0, n_in = 0;
+  std::vector<uint16_t> c;
+  uint16_t at(size_t r, size_t i) const { return c[r * n_in + i]; }
+};
+
+}  // namespace
+
+struct rse_codec {
+  int field;
+  size_t k, p, total;
+  rse::Matrix<rse::Gf8Field> m8;   // field == 8
+  rse::Matrix<rse::Gf16Field> m16;  // field == 16
+  // decode-matrix LRU keyed by invalid indices (core.rs:697-731)
+  mutable std::mutex mu;
+  mutable std::list<std::pair<std::vector<size_t>, std::vector<uint16_t>>> lru;
+  mutable std::map<std::vector<size_t>, decltype(lru)::iterator> index;
+
+  size_t esize() const { return field == 16 ? 2 : 1; }
+  uint16_t mat(size_t r, size_t c) const { return field == 16 ? m16.at(r, c) : m8.at(r, c); }
+  uint16_t mul(uint16_t a, uint16_t b) const {
+    return field == 16 ? rse::Gf16Field::mul(a, b) : rse::Gf8Field::mul(a, b);
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------- validation
+// macros.rs:204-245 check_piece_count!
+int check_count(size_t got, size_t want, int too_few, int too_many) {
+  if (got < want) return too_few;
+  if (got > want) return too_many;
+  return RSE_OK;
+}
+// macros.rs:144-155 check_slices!(multi => ...)
+int check_multi(const size_t* lens, size_t n) {
+  const size_t size = lens[0];
+  if (size == 0) return RSE_EMPTY_SHARD;
+  for (size_t i = 0; i < n; ++i)
+    if (lens[i] != size) return RSE_INCORRECT_SHARD_SIZE;
+  return RSE_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ------------------------------------------------------------- launching
+// One fused pass: outputs (+)= rows x inputs over len_bytes, chunked so every
+// launch fits the kernel-argument block (<= kMaxIn inputs, <= kMaxOut outputs).
+struct Job {
+  int field;
+  const Rows* rows;
+  const uint8_t* const* in;  // n_in pointers
+  uint8_t* const* out;       // n_out pointers (may be null entries in kCheck mode)
+  const uint8_t* const* cmp; // n_out pointers (check modes) or null
+  size_t len_bytes;
+  uint32_t mode;
+  bool accumulate;
+  uint32_t* mismatch;
+  uint64_t stripe_stride;
+  size_t n_stripes;
+};
+
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mismatch,
+                          hipStream_t s);
+
+hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, uint32_t mode,
+                     bool acc, hipStream_t s) {
+  CodeArgs a;
+  std::memset(&a, 0, sizeof a);
+  bool al = (j.stripe_stride % 16u) == 0;
+  for (size_t i = 0; i < ni; ++i) {
+    a.in[i] = j.in[i0 + i];
+    al = al && aligned16(a.in[i]);
+  }
+  for (size_t r = 0; r < no; ++r) {
+    a.out[r] = j.out ? j.out[o0 + r] : nullptr;
+    a.cmp[r] = j.cmp ? j.cmp[o0 + r] : nullptr;
+    if (mode != rse::kCheck) al = al && aligned16(a.out[r]);
+    if (mode != rse::kStore) al = al && aligned16(a.cmp[r]);
+    for (size_t i = 0; i < ni; ++i) a.coef[r][i] = j.rows->at(o0 + r, i0 + i);
+  }
+  a.stripe_stride = j.stripe_stride;
+  a.len = j.len_bytes;
+  a.n_vec = al ? j.len_bytes / 16u : 0;
+  a.mismatch = j.mismatch;
+  a.n_in = (uint32_t)ni;
+  a.n_out = (uint32_t)no;
+  a.mode = mode;
+  a.accumulate = acc ? 1u : 0u;
+  size_t done = 0;
+  while (done < j.n_stripes) {
+    const size_t batch = std::min<size_t>(j.n_stripes - done, 65535);
+    if (done) {  // advance every pointer to stripe `done`
+      const uint64_t adv = (uint64_t)65535 * j.stripe_stride;
+      for (size_t i = 0; i < ni; ++i) a.in[i] += adv;
+      for (size_t r = 0; r < no; ++r) {
+        if (a.out[r]) a.out[r] += adv;
+        if (a.cmp[r]) a.cmp[r] += adv;
+      }
+    }
+    hipError_t e = rse::launch_code(j.field, a, (uint32_t)batch, s);
+    if (e != hipSuccess) return e;
+    done += batch;
+  }
+  return hipSuccess;
+}
+
+// Executes a Job; `scratch` provides per-output buffers when a CHECK job must
+// be split over several input chunks (full sums are needed before comparing).
+int run_job(const Job& j, hipStream_t s) {
+  const size_t n_out = j.rows->n_out, n_in = j.rows->n_in;
+  if (n_out == 0 || j.len_bytes == 0) return RSE_OK;
+  const bool single_in = n_in <= (size_t)kMaxIn;
+  if (j.mode == rse::kStore || single_in) {
+    for (size_t o0 = 0; o0 < n_out; o0 += kMaxOut) {
+      const size_t no = std::min<size_t>(kMaxOut, n_out - o0);
+      for (size_t i0 = 0; i0 < n_in; i0 += kMaxIn) {
+        const size_t ni = std::min<size_t>(kMaxIn, n_in - i0);
+        RSE_HIP(run_chunk(j, o0, no, i0, ni, j.mode, j.accumulate || i0 > 0, s));
+      }
+    }
+    return RSE_OK;
+  }
+  // CHECK modes with > kMaxIn inputs: materialise the sums, then compare.
+  std::vector<uint8_t*> dst(n_out, nullptr);
+  std::vector<void*> owned;
+  const size_t span = (j.n_stripes - 1) * j.stripe_stride + j.len_bytes;
+  for (size_t r = 0; r < n_out; ++r) {
+    if (j.mode == rse::kCheckStore) {
+      dst[r] = j.out[r];
+    } else {
+      void* p = nullptr;
+      hipError_t e = hipMallocAsync(&p, span, s);
+      if (e != hipSuccess) {
+        for (void* q : owned) (void)hipFreeAsync(q, s);
+        return dev_fail(e);
+      }
+      owned.push_back(p);
+      dst[r] = static_cast<uint8_t*>(p);
+    }
+  }
+  Job st = j;
+  st.out = dst.data();
+  st.cmp = nullptr;
+  st.mode = rse::kStore;
+  int rc = run_job(st, s);
+  for (size_t r = 0; rc == RSE_OK && r < n_out; ++r)
+    for (size_t sidx = 0; sidx < j.n_stripes && rc == RSE_OK; ++sidx) {
+      const size_t off = sidx * j.stripe_stride;
+      hipError_t e = launch_compare(dst[r] + off, j.cmp[r] + off, j.len_bytes, j.mismatch, s);
+      if (e != hipSuccess) rc = dev_fail(e);
+    }
+  for (void* q : owned) (void)hipFreeAsync(q, s);
+  return rc;
+}
+
+__global__ void compare_kernel(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mm) {
+  bool diff = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+       i += (size_t)gridDim.x * blockDim.x)
+    diff |= a[i] != b[i];
+  if (diff) atomicOr(mm, 1u);
+}
+
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mismatch,
+                          hipStream_t s) {
+  size_t blocks = std::min<size_t>((len + 255) / 256, 4096);
+  hipLaunchKernelGGL(compare_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, len, mismatch);
+  return hipGetLastError();
+}
+
+// Runs `j` in a check mode and returns the verdict (synchronises the stream).
+int run_check(Job j, hipStream_t s, int* ok) {
+  uint32_t* flag = nullptr;
+  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(uint32_t), s));
+  hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) {
+    (void)hipFreeAsync(flag, s);
+    return dev_fail(e);
+  }
+  j.mismatch = flag;
+  int rc = run_job(j, s);
+  uint32_t h = 0;
+  if (rc == RSE_OK) {
+    e = hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = dev_fail(e);
+  }
+  (void)hipFreeAsync(flag, s);
+  if (rc == RSE_OK) *ok = h == 0 ? 1 : 0;
+  return rc;
+}
+
+Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
+  Rows r;
+  r.n_out = c->p;
+  r.n_in = c->k;
+  r.c.resize(c->p * c->k);
+  for (size_t i = 0; i < c->p; ++i)
+    for (size_t j = 0; j < c->k; ++j) r.c[i * c->k + j] = c->mat(c->k + i, j);
+  return r;
+}
+
+Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, core.rs:492-509
+  Rows r;
+  r.n_out = c->p;
+  r.n_in = 1;
+  r.c.resize(c->p);
+  for (size_t i = 0; i < c->p; ++i) r.c[i] = c->mat(c->k + i, i_data);
+  return r;
+}
+
+// core.rs:697-731: k x k inverse of the valid rows, cached by invalid indices.
+int decode_matrix(const rse_codec* c, const std::vector<size_t>& valid,
+                  const std::vector<size_t>& invalid, std::vector<uint16_t>& out) {
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->index.find(invalid);
+    if (it != c->index.end()) {
+      c->lru.splice(c->lru.begin(), c->lru, it->second);
+      out = it->second->second;
+      return RSE_OK;
+    }
+  }
+  const size_t k = c->k;
+  bool ok;
+  if (c->field == 16) {
+    rse::Matrix<rse::Gf16Field> sub(k, k), inv;
+    for (size_t r = 0; r < k; ++r)
+      for (size_t j = 0; j < k; ++j) sub.at(r, j) = c->m16.at(valid[r], j);
+    ok = sub.invert(inv);
+    out = inv.d;
+  } else {
+    rse::Matrix<rse::Gf8Field> sub(k, k), inv;
+    for (size_t r = 0; r < k; ++r)
+      for (size_t j = 0; j < k; ++j) sub.at(r, j) = c->m8.at(valid[r], j);
+    ok = sub.invert(inv);
+    out = inv.d;
+  }
+  if (!ok) return RSE_ERR_SINGULAR_MATRIX;  // unreachable for an MDS code
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->index.find(invalid) == c->index.end()) {
+    c->lru.emplace_front(invalid, out);
+    c->index[invalid] = c->lru.begin();
+    if (c->lru.size() > kCacheCapacity) {
+      c->index.erase(c->lru.back().first);
+      c->lru.pop_back();
+    }
+  }
+  return RSE_OK;
+}
+
+// Plan of a reconstruct: the k surviving inputs and the combined rows that
+// produce every missing output in one pass (core.rs:733-923).
+struct ReconPlan {
+  std::vector<const uint8_t*> in;  // sub_shards (core.rs:792)
+  std::vector<uint8_t*> out;       // missing data shards, then missing parity shards
+  Rows rows;
+  size_t len = 0;  // elements
+  bool nothing_to_do = false;
+};
+
+int plan_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens,
+                     const uint8_t* present, size_t n, bool data_only, ReconPlan& plan) {
+  int rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS);
+  if (rc) return rc;
+  if (!lens || !present) return RSE_ERR_INVALID_ARGUMENT;
+  const size_t k = c->k;
+  size_t number_present = 0, shard_len = 0;
+  bool have = false;
+  for (size_t i = 0; i < n; ++i) {  // core.rs:747-761
+    if (!present[i]) continue;
+    if (lens[i] == 0) return RSE_EMPTY_SHARD;
+    ++number_present;
+    if (have && lens[i] != shard_len) return RSE_INCORRECT_SHARD_SIZE;
+    shard_len = lens[i];
+    have = true;
+  }
+  if (number_present == c->total) {  // core.rs:763-767
+    plan.nothing_to_do = true;
+    return RSE_OK;
+  }
+  if (number_present < k) return RSE_TOO_FEW_SHARDS_PRESENT;  // core.rs:770-772
+  if (!shards) return RSE_ERR_INVALID_ARGUMENT;
+
+  std::vector<size_t> valid, invalid, miss_data, miss_parity;
+  for (size_t row = 0; row < n; ++row) {  // core.rs:801-841
+    if (row >= k && data_only) {
+      if (present[row]) {
+        if (valid.size() < k) valid.push_back(row);
+      } else {
+        invalid.push_back(row);
+      }
+      continue;
+    }
+    if (lens[row] != shard_len) return RSE_INCORRECT_SHARD_SIZE;  // lib.rs:185-199
+    if (present[row]) {
+      if (valid.size() < k) valid.push_back(row);
+    } else {
+      if (!shards[row]) return RSE_ERR_INVALID_ARGUMENT;
+      (row < k ? miss_data : miss_parity).push_back(row);
+      invalid.push_back(row);
+    }
+  }
+  for (size_t v : valid)
+    if (!shards[v]) return RSE_ERR_INVALID_ARGUMENT;
+
+  std::vector<uint16_t> dec;
+  rc = decode_matrix(c, valid, invalid, dec);
+  if (rc) return rc;
+
+  // Coefficients that rebuild data shard j from the k valid inputs:
+  //   present data j  -> unit vector at its position among the valid inputs
+  //   missing data j  -> row j of the decode matrix (core.rs:853-861)
+  auto data_row = [&](size_t j, std::vector<uint16_t>& row) {
+    row.assign(k, 0);
+    auto it = std::find(valid.begin(), valid.end(), j);
+    if (it != valid.end()) row[it - valid.begin()] = 1;
+    else
+      for (size_t i = 0; i < k; ++i) row[i] = dec[j * k + i];
+  };
+  plan.rows.n_in = k;
+  plan.rows.n_out = miss_data.size() + (data_only ? 0 : miss_parity.size());
+  plan.rows.c.assign(plan.rows.n_out * k, 0);
+  std::vector<uint16_t> row;
+  size_t o = 0;
+  for (size_t j : miss_data) {
+    data_row(j, row);
+    std::copy(row.begin(), row.end(), plan.rows.c.begin() + o * k);
+    plan.out.push_back(static_cast<uint8_t*>(shards[j]));
+    ++o;
+  }
+  if (!data_only) {
+    // missing parity r = sum_j P[r][j] * data_j  (core.rs:872-918), with every
+    // data_j expanded over the valid inputs: one combined row per parity shard.
+    for (size_t pr : miss_parity) {
+      uint16_t* dst = &plan.rows.c[o * k];
+      for (size_t j = 0; j < k; ++j) {
+        const uint16_t pj = c->mat(pr, j);
+        if (!pj) continue;
+        data_row(j, row);
+        for (size_t i = 0; i < k; ++i) dst[i] ^= c->mul(pj, row[i]);
+      }
+      plan.out.push_back(static_cast<uint8_t*>(shards[pr]));
+      ++o;
+    }
+  }
+  for (size_t v : valid) plan.in.push_back(static_cast<const uint8_t*>(shards[v]));
+  plan.len = shard_len;
+  return RSE_OK;
+}
+
+int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens,
+                     const uint8_t* present, size_t n, bool data_only, hipStream_t s) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  ReconPlan plan;
+  int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
+  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  Job j{c->field, &plan.rows, plan.in.data(), plan.out.data(), nullptr, plan.len * c->esize(),
+        rse::kStore, false, nullptr, 0, 1};
+  return run_job(j, s);
+}
+
+int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* data_lens,
+                    size_t n_data, void* const* parity, const size_t* parity_lens,
+                    size_t n_parity, hipStream_t s) {
+  int rc;
+  if ((rc = check_count(n_data, c->k, RSE_TOO_FEW_DATA_SHARDS, RSE_TOO_MANY_DATA_SHARDS))) return rc;
+  if ((rc = check_count(n_parity, c->p, RSE_TOO_FEW_PARITY_SHARDS, RSE_TOO_MANY_PARITY_SHARDS)))
+    return rc;
+  if (!data_lens || !parity_lens || !data || !parity) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(data_lens, n_data))) return rc;
+  if ((rc = check_multi(parity_lens, n_parity))) return rc;
+  if (data_lens[0] != parity_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
+  const Rows rows = parity_rows(c);
+  Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(data),
+        reinterpret_cast<uint8_t* const*>(parity), nullptr, data_lens[0] * c->esize(),
+        rse::kStore, false, nullptr, 0, 1};
+  return run_job(j, s);
+}
+
+int encode_single_sep_impl(const rse_codec* c, size_t i_data, const void* single,
+                           size_t single_len, void* const* parity, const size_t* parity_lens,
+                           size_t n_parity, hipStream_t s) {
+  int rc;
+  if (i_data >= c->k) return RSE_INVALID_INDEX;
+  if ((rc = check_count(n_parity, c->p, RSE_TOO_FEW_PARITY_SHARDS, RSE_TOO_MANY_PARITY_SHARDS)))
+    return rc;
+  if (!parity_lens || !parity || !single) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(parity_lens, n_parity))) return rc;
+  if (parity_lens[0] != single_len) return RSE_INCORRECT_SHARD_SIZE;
+  const Rows rows = single_column(c, i_data);
+  const uint8_t* in[1] = {static_cast<const uint8_t*>(single)};
+  Job j{c->field, &rows, in, reinterpret_cast<uint8_t* const*>(parity), nullptr,
+        single_len * c->esize(), rse::kStore, i_data != 0, nullptr, 0, 1};
+  return run_job(j, s);
+}
+
+int verify_impl(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+                void* const* buffer, const size_t* buf_lens, size_t n_buf, bool with_buffer,
+                int* ok, hipStream_t s) {
+  int rc;
+  if (!c || !ok) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (with_buffer &&
+      (rc = check_count(n_buf, c->p, RSE_TOO_FEW_BUFFER_SHARDS, RSE_TOO_MANY_BUFFER_SHARDS)))
+    return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  if (with_buffer) {
+    if (!buf_lens || !buffer) return RSE_ERR_INVALID_ARGUMENT;
+    if ((rc = check_multi(buf_lens, n_buf))) return rc;
+    if (lens[0] != buf_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
+  }
+  const Rows rows = parity_rows(c);
+  Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(shards),
+        with_buffer ? reinterpret_cast<uint8_t* const*>(buffer) : nullptr,
+        reinterpret_cast<const uint8_t* const*>(shards) + c->k, lens[0] * c->esize(),
+        with_buffer ? rse::kCheckStore : rse::kCheck, false, nullptr, 0, 1};
+  return run_check(j, s, ok);
+}
+
+}  // namespace
+
+// =========================================================================
+// C ABI
+// =========================================================================
+extern "C" {
+
+const char* rse_strerror(int status) {
+  switch (status) {  // errors.rs:20-38
+    case RSE_OK: return "Ok";
+    case RSE_TOO_FEW_SHARDS: return "The number of provided shards is smaller than the one in codec";
+    case RSE_TOO_MANY_SHARDS: return "The number of provided shards is greater than the one in codec";
+    case RSE_TOO_FEW_DATA_SHARDS: return "The number of provided data shards is smaller than the one in codec";
+    case RSE_TOO_MANY_DATA_SHARDS: return "The number of provided data shards is greater than the one in codec";
+    case RSE_TOO_FEW_PARITY_SHARDS: return "The number of provided parity shards is smaller than the one in codec";
+    case RSE_TOO_MANY_PARITY_SHARDS: return "The number of provided parity shards is greater than the one in codec";
+    case RSE_TOO_FEW_BUFFER_SHARDS: return "The number of provided buffer shards is smaller than the number of parity shards in codec";
+    case RSE_TOO_MANY_BUFFER_SHARDS: return "The number of provided buffer shards is greater than the number of parity shards in codec";
+    case RSE_INCORRECT_SHARD_SIZE: return "At least one of the provided shards is not of the correct size";
+    case RSE_TOO_FEW_SHARDS_PRESENT: return "The number of shards present is smaller than number of parity shards, cannot reconstruct missing shards";
+    case RSE_EMPTY_SHARD: return "The first shard provided is of zero length";
+    case RSE_INVALID_SHARD_FLAGS: return "The number of flags does not match the total number of shards";
+    case RSE_INVALID_INDEX: return "The data shard index provided is greater or equal to the number of data shards in codec";
+    case RSE_ERR_INVALID_ARGUMENT: return "Invalid argument (null pointer, unknown field or size)";
+    case RSE_ERR_DEVICE: return "HIP runtime error";
+    case RSE_ERR_NO_MEMORY: return "Out of memory";
+    case RSE_ERR_SINGULAR_MATRIX: return "Singular matrix";
+    default: return "Unknown status";
+  }
+}
+
+int rse_last_device_error(void) { return g_last_hip_error; }
+const char* rse_version(void) { return "rse-mi355x 0.1.0 (gfx950)"; }
+
+int rse_codec_new(int field, size_t data_shards, size_t parity_shards, rse_codec** out) {
+  if (!out || (field != RSE_FIELD_GF8 && field != RSE_FIELD_GF16)) return RSE_ERR_INVALID_ARGUMENT;
+  const size_t order = field == RSE_FIELD_GF16 ? 65536 : 256;
+  if (data_shards == 0) return RSE_TOO_FEW_DATA_SHARDS;      // core.rs:446-448
+  if (parity_shards == 0) return RSE_TOO_FEW_PARITY_SHARDS;  // core.rs:449-451
+  if (data_shards + parity_shards > order) return RSE_TOO_MANY_SHARDS;  // core.rs:452-454
+  try {
+    std::unique_ptr<rse_codec> c(new rse_codec());
+    c->field = field;
+    c->k = data_shards;
+    c->p = parity_shards;
+    c->total = data_shards + parity_shards;
+    // core.rs:430-436: V * (V[0..k])^-1
+    if (field == RSE_FIELD_GF16) {
+      auto v = rse::Matrix<rse::Gf16Field>::vandermonde(c->total, c->k);
+      rse::Matrix<rse::Gf16Field> top(c->k, c->k), inv;
+      for (size_t r = 0; r < c->k; ++r)
+        for (size_t j = 0; j < c->k; ++j) top.at(r, j) = v.at(r, j);
+      if (!top.invert(inv)) return RSE_ERR_SINGULAR_MATRIX;
+      c->m16 = v.multiply(inv);
+    } else {
+      auto v = rse::Matrix<rse::Gf8Field>::vandermonde(c->total, c->k);
+      rse::Matrix<rse::Gf8Field> top(c->k, c->k), inv;
+      for (size_t r = 0; r < c->k; ++r)
+        for (size_t j = 0; j < c->k; ++j) top.at(r, j) = v.at(r, j);
+      if (!top.invert(inv)) return RSE_ERR_SINGULAR_MATRIX;
+      c->m8 = v.multiply(inv);
+    }
+    *out = c.release();
+    return RSE_OK;
+  } catch (const std::bad_alloc&) {
+    return RSE_ERR_NO_MEMORY;
+  }
+}
+
+void rse_codec_free(rse_codec* codec) { delete codec; }
+int rse_codec_field(const rse_codec* c) { return c ? c->field : 0; }
+size_t rse_codec_data_shard_count(const rse_codec* c) { return c ? c->k : 0; }
+size_t rse_codec_parity_shard_count(const rse_codec* c) { return c ? c->p : 0; }
+size_t rse_codec_total_shard_count(const rse_codec* c) { return c ? c->total : 0; }
+
+int rse_codec_matrix(const rse_codec* c, uint8_t* out, size_t out_bytes) {
+  if (!c || !out) return RSE_ERR_INVALID_ARGUMENT;
+  const size_t es = c->esize(), need = c->total * c->k * es;
+  if (out_bytes < need) return RSE_ERR_INVALID_ARGUMENT;
+  for (size_t r = 0; r < c->total; ++r)
+    for (size_t j = 0; j < c->k; ++j) {
+      const uint16_t v = c->mat(r, j);
+      if (es == 2) {
+        out[(r * c->k + j) * 2] = (uint8_t)(v >> 8);
+        out[(r * c->k + j) * 2 + 1] = (uint8_t)v;
+      } else {
+        out[r * c->k + j] = (uint8_t)v;
+      }
+    }
+  return RSE_OK;
+}
+
+int rse_encode(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
+               rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  int rc;
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  return encode_sep_impl(c, const_cast<const void* const*>(shards), lens, c->k, shards + c->k,
+                         lens + c->k, c->p, (hipStream_t)stream);
+}
+
+int rse_encode_sep(const rse_codec* c, const void* const* data, const size_t* data_lens,
+                   size_t n_data, void* const* parity, const size_t* parity_lens,
+                   size_t n_parity, rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  return encode_sep_impl(c, data, data_lens, n_data, parity, parity_lens, n_parity,
+                         (hipStream_t)stream);
+}
+
+int rse_encode_single(const rse_codec* c, size_t i_data, void* const* shards, const size_t* lens,
+                      size_t n, rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  int rc;
+  if (i_data >= c->k) return RSE_INVALID_INDEX;  // core.rs:552
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  return encode_single_sep_impl(c, i_data, shards[i_data], lens[i_data], shards + c->k,
+                                lens + c->k, c->p, (hipStream_t)stream);
+}
+
+int rse_encode_single_sep(const rse_codec* c, size_t i_data, const void* single,
+                          size_t single_len, void* const* parity, const size_t* parity_lens,
+                          size_t n_parity, rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  return encode_single_sep_impl(c, i_data, single, single_len, parity, parity_lens, n_parity,
+                                (hipStream_t)stream);
+}
+
+int rse_verify(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+               int* ok, rse_stream_t stream) {
+  return verify_impl(c, shards, lens, n, nullptr, nullptr, 0, false, ok, (hipStream_t)stream);
+}
+
+int rse_verify_with_buffer(const rse_codec* c, const void* const* shards, const size_t* lens,
+                           size_t n, void* const* buffer, const size_t* buf_lens, size_t n_buf,
+                           int* ok, rse_stream_t stream) {
+  return verify_impl(c, shards, lens, n, buffer, buf_lens, n_buf, true, ok, (hipStream_t)stream);
+}
+
+int rse_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens,
+                    const uint8_t* present, size_t n, rse_stream_t stream) {
+  return reconstruct_impl(c, shards, lens, present, n, false, (hipStream_t)stream);
+}
+
+int rse_reconstruct_data(const rse_codec* c, void* const* shards, const size_t* lens,
+                         const uint8_t* present, size_t n, rse_stream_t stream) {
+  return reconstruct_impl(c, shards, lens, present, n, true, (hipStream_t)stream);
+}
+
+int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
+                    rse_stream_t stream) {
+  if (!c || !stripes) return RSE_ERR_INVALID_ARGUMENT;
+  if (shard_len == 0) return RSE_EMPTY_SHARD;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t sb = shard_len * c->esize();
+  uint8_t* base = static_cast<uint8_t*>(stripes);
+  std::vector<const uint8_t*> in(c->k);
+  std::vector<uint8_t*> out(c->p);
+  for (size_t i = 0; i < c->k; ++i) in[i] = base + i * sb;
+  for (size_t r = 0; r < c->p; ++r) out[r] = base + (c->k + r) * sb;
+  const Rows rows = parity_rows(c);
+  Job j{c->field, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
+        (uint64_t)c->total * sb, n_stripes};
+  return run_job(j, (hipStream_t)stream);
+}
+
+int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_len,
+                              size_t n_stripes, const uint8_t* present, rse_stream_t stream) {
+  if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t sb = shard_len * c->esize();
+  uint8_t* base = static_cast<uint8_t*>(stripes);
+  std::vector<void*> ptrs(c->total);
+  std::vector<size_t> lens(c->total, shard_len);
+  for (size_t i = 0; i < c->total; ++i) ptrs[i] = base + i * sb;
+  ReconPlan plan;
+  int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, true, plan);
+  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  Job j{c->field, &plan.rows, plan.in.data(), plan.out.data(), nullptr, sb, rse::kStore, false,
+        nullptr, (uint64_t)c->total * sb, n_stripes};
+  return run_job(j, (hipStream_t)stream);
+}
+
+int rse_code_shards(int field, const uint8_t* rows, size_t n_out, size_t n_in,
+                    const void* const* inputs, void* const* outputs, size_t len, int accumulate,
+                    rse_stream_t stream) {
+  if ((field != RSE_FIELD_GF8 && field != RSE_FIELD_GF16) || !rows || !inputs || !outputs)
+    return RSE_ERR_INVALID_ARGUMENT;
+  if (n_out == 0 || n_in == 0 || len == 0) return RSE_OK;
+  const size_t es = field == RSE_FIELD_GF16 ? 2 : 1;
+  Rows r;
+  r.n_out = n_out;
+  r.n_in = n_in;
+  r.c.resize(n_out * n_in);
+  for (size_t i = 0; i < n_out * n_in; ++i)
+    r.c[i] = es == 2 ? (uint16_t)((rows[2 * i] << 8) | rows[2 * i + 1]) : rows[i];
+  Job j{field, &r, reinterpret_cast<const uint8_t* const*>(inputs),
+        reinterpret_cast<uint8_t* const*>(outputs), nullptr, len * es, rse::kStore,
+        accumulate != 0, nullptr, 0, 1};
+  return run_job(j, (hipStream_t)stream);
+}
+
+int rse_gf8_mul_slice(uint8_t c, const void* in, void* out, size_t len, int xor_into,
+                      rse_stream_t stream) {
+  const void* ins[1] = {in};
+  void* outs[1] = {out};
+  return rse_code_shards(RSE_FIELD_GF8, &c, 1, 1, ins, outs, len, xor_into, stream);
+}
+
+int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
+                         size_t batch, rse_stream_t stream) {
+  if (!d_in || !d_out || !d_singular || n == 0 || n > 255 || batch == 0 || batch > 0x7fffffff)
+    return RSE_ERR_INVALID_ARGUMENT;
+  RSE_HIP(rse::launch_gf8_invert(static_cast<const uint8_t*>(d_in), static_cast<uint8_t*>(d_out),
+                                 d_singular, (uint32_t)n, (uint32_t)batch, (hipStream_t)stream));
+  return RSE_OK;
+}
+
+// Host shards in, host parity out: chunks of every shard are staged H2D, coded
+// and staged D2H on two streams in turn, so chunk c+1's copies overlap chunk c's
+// kernel (and H2D overlaps D2H on the full-duplex link).  Pinned host memory
+// gives truly asynchronous DMA; pageable memory still works (the runtime
+// stages it) but serialises the copies.
+int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
+                    rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  int rc;
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
+  hipStream_t s0 = (hipStream_t)stream, s1 = nullptr;
+  const size_t bytes = lens[0] * c->esize();
+  const size_t chunk = std::min<size_t>(bytes, (size_t)8 << 20);
+  const size_t nchunks = (bytes + chunk - 1) / chunk;
+  uint8_t* dbuf = nullptr;
+  hipEvent_t ev = nullptr;
+  RSE_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), 2 * c->total * chunk, s0);
+  if (e == hipSuccess) e = hipEventRecord(ev, s0);  // s1 starts after s0's prior work
+  if (e == hipSuccess) e = hipStreamWaitEvent(s1, ev, 0);
+  const Rows rows = parity_rows(c);
+  std::vector<const uint8_t*> in(c->k);
+  std::vector<uint8_t*> out(c->p);
+  for (size_t ci = 0; e == hipSuccess && ci < nchunks; ++ci) {
+    const size_t off = ci * chunk, sz = std::min(chunk, bytes - off);
+    hipStream_t st = (ci & 1) ? s1 : s0;
+    uint8_t* set = dbuf + (ci & 1) * c->total * chunk;
+    for (size_t i = 0; e == hipSuccess && i < c->k; ++i) {
+      e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(shards[i]) + off, sz,
+                         hipMemcpyHostToDevice, st);
+      in[i] = set + i * chunk;
+    }
+    for (size_t r = 0; r < c->p; ++r) out[r] = set + (c->k + r) * chunk;
+    if (e != hipSuccess) break;
+    Job j{c->field, &rows, in.data(), out.data(), nullptr, sz, rse::kStore, false, nullptr, 0, 1};
+    rc = run_job(j, st);
+    if (rc) break;
+    for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
+      e = hipMemcpyAsync(static_cast<uint8_t*>(shards[c->k + r]) + off, out[r], sz,
+                         hipMemcpyDeviceToHost, st);
+  }
+  hipError_t e2 = hipEventRecord(ev, s1);
+  if (e2 == hipSuccess) e2 = hipStreamWaitEvent(s0, ev, 0);
+  if (dbuf) (void)hipFreeAsync(dbuf, s0);
+  if (e2 == hipSuccess) e2 = hipStreamSynchronize(s0);
+  if (ev) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(s1);
+  if (rc) return rc;
+  if (e != hipSuccess) return dev_fail(e);
+  if (e2 != hipSuccess) return dev_fail(e2);
+  return RSE_OK;
+}
+
+int rse_fill_splitmix(void* dst, size_t nbytes, uint64_t seed, uint64_t shard_id,
+                      rse_stream_t stream) {
+  if (!dst && nbytes) return RSE_ERR_INVALID_ARGUMENT;
+  RSE_HIP(rse::launch_fill_splitmix(dst, nbytes, seed, shard_id, (hipStream_t)stream));
+  return RSE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// rse_kernels.hpp -- internal launch interface between the host codec
+// (rse_codec.cpp) and the CDNA4 kernels (rse_kernels.hip).
+//
+// One fused kernel family replaces the reference's whole code_some_slices
+// (core.rs:481-509): every input shard byte is read once from HBM, every output
+// byte is written once, and the k x p' coefficient products are XOR-accumulated
+// in VGPRs.  The same launch also serves check_some_slices_with_buffer
+// (core.rs:511-532) through the CHECK modes, so verify never round-trips parity
+// through HBM twice.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace rse {
+
+// Shards per launch carried in the kernel-argument segment (no device-side
+// descriptor, hence no lifetime hazard across streams).  Bigger codecs are split
+// by the host into input/output chunks (see rse_codec.cpp: launch_code).
+constexpr int kMaxIn = 32;
+constexpr int kMaxOut = 16;
+
+enum CodeMode : uint32_t {
+  kStore = 0,       // out[r]  = sum_i coef[r][i] * in[i]            (encode)
+  kCheck = 1,       // mismatch |= (sum_i coef[r][i] * in[i]) != cmp[r]   (verify)
+  kCheckStore = 2,  // both: buffer written and compared (verify_with_buffer)
+};
+
+struct CodeArgs {
+  const uint8_t* in[kMaxIn];
+  uint8_t* out[kMaxOut];
+  const uint8_t* cmp[kMaxOut];
+  uint64_t stripe_stride;  // bytes between stripe s and s+1 for EVERY pointer
+  uint64_t n_vec;          // 16-byte vectors handled by the vector body
+  uint64_t len;            // bytes per shard
+  uint32_t* mismatch;      // device word, CHECK modes only
+  uint32_t n_in, n_out;
+  uint32_t mode;
+  uint32_t accumulate;     // 1: out[r] ^= ... (ShardByShard / chunked inputs)
+  // GF(2^8): coef[r][i] & 0xff.  GF(2^16): (coef_of_x << 8) | constant.
+  uint16_t coef[kMaxOut][kMaxIn];
+};
+
+// Launch the fused coding kernel over n_stripes stripes (grid.y) on `stream`.
+// field is 8 or 16.  Returns a hipError_t.
+hipError_t launch_code(int field, const CodeArgs& args, uint32_t n_stripes,
+                       hipStream_t stream);
+
+// Fill nbytes of device memory with the splitmix64 byte stream of
+// (seed, shard_id) -- identical to oracle/oracle.py: splitmix_bytes.
+hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed,
+                                uint64_t shard_id, hipStream_t stream);
+
+// Device Gauss-Jordan inversion of n x n matrices over GF(2^8) (batched: one
+// workgroup per matrix).  in/out are device pointers to batch*n*n bytes;
+// singular[b] receives 1 for a singular matrix.
+hipError_t launch_gf8_invert(const uint8_t* in, uint8_t* out, uint32_t* singular,
+                             uint32_t n, uint32_t batch, hipStream_t stream);
+
+}  // namespace rse

@@ -1,0 +1,85 @@
+"""ctypes binding of librse_hip.so (include/rse_hip.h).
+
+The HIP library is the product: there is no CPU fallback.  If the shared object
+is missing or fails to load, importing this package raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librse_hip.so")
+
+# Every entry point of include/rse_hip.h (checked by tests/test_capi.py).
+EXPORTS = (
+    "rse_strerror", "rse_last_device_error", "rse_version",
+    "rse_codec_new", "rse_codec_free", "rse_codec_field",
+    "rse_codec_data_shard_count", "rse_codec_parity_shard_count",
+    "rse_codec_total_shard_count", "rse_codec_matrix",
+    "rse_encode", "rse_encode_sep", "rse_encode_single", "rse_encode_single_sep",
+    "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
+    "rse_encode_flat", "rse_reconstruct_data_flat", "rse_code_shards",
+    "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_fill_splitmix",
+)
+
+_c = ctypes
+_vp = _c.c_void_p
+_sz = _c.c_size_t
+_szp = _c.POINTER(_c.c_size_t)
+_u8p = _c.POINTER(_c.c_uint8)
+_ip = _c.POINTER(_c.c_int)
+
+_SIGS = {
+    "rse_strerror": (_c.c_char_p, [_c.c_int]),
+    "rse_last_device_error": (_c.c_int, []),
+    "rse_version": (_c.c_char_p, []),
+    "rse_codec_new": (_c.c_int, [_c.c_int, _sz, _sz, _c.POINTER(_vp)]),
+    "rse_codec_free": (None, [_vp]),
+    "rse_codec_field": (_c.c_int, [_vp]),
+    "rse_codec_data_shard_count": (_sz, [_vp]),
+    "rse_codec_parity_shard_count": (_sz, [_vp]),
+    "rse_codec_total_shard_count": (_sz, [_vp]),
+    "rse_codec_matrix": (_c.c_int, [_vp, _u8p, _sz]),
+    "rse_encode": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
+    "rse_encode_sep": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _vp]),
+    "rse_encode_single": (_c.c_int, [_vp, _sz, _vp, _szp, _sz, _vp]),
+    "rse_encode_single_sep": (_c.c_int, [_vp, _sz, _vp, _sz, _vp, _szp, _sz, _vp]),
+    "rse_verify": (_c.c_int, [_vp, _vp, _szp, _sz, _ip, _vp]),
+    "rse_verify_with_buffer": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _ip, _vp]),
+    "rse_reconstruct": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
+    "rse_reconstruct_data": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
+    "rse_encode_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _vp]),
+    "rse_reconstruct_data_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
+    "rse_code_shards": (_c.c_int, [_c.c_int, _u8p, _sz, _sz, _vp, _vp, _sz, _c.c_int, _vp]),
+    "rse_gf8_mul_slice": (_c.c_int, [_c.c_uint8, _vp, _vp, _sz, _c.c_int, _vp]),
+    "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "rse_encode_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
+    "rse_fill_splitmix": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64, _vp]),
+}
+
+_LIB = None
+
+
+def load():
+    """Load librse_hip.so.  torch is imported first so that the HIP runtime torch
+    ships (SONAME libamdhip64.so.7) is the one the library binds to: one runtime,
+    shared streams and device pointers."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    try:
+        import torch  # noqa: F401  (must precede the dlopen, see docstring)
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C reed-solomon-erasure_amd` "
+            "(or __graft_entry__.build()).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib

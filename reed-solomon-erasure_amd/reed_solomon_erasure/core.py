@@ -1,0 +1,373 @@
+"""``ReedSolomon<F>`` and ``ShardByShard`` (core.rs:49-924) over librse_hip.so.
+
+Same method names, argument meaning and error behaviour as the reference, with
+Rust ``Result`` errors raised as :class:`RSError`.  Shards are torch tensors in
+HBM (``device='cuda'``); work is enqueued on torch's current stream, so results
+are ordered with surrounding torch work exactly like any torch op.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple, Union
+
+import torch
+
+from ._lib import load
+from .errors import DeviceError, Error, RSError, SBSError, SBSErrorKind
+
+_lib = load()
+
+ShardList = Sequence[torch.Tensor]
+
+
+def _raise(status: int):
+    if status == 0:
+        return
+    if 1 <= status <= 13:
+        raise RSError(Error(status))
+    msg = _lib.rse_strerror(status).decode()
+    raise DeviceError(status, msg, _lib.rse_last_device_error())
+
+
+def _stream(t: Optional[torch.Tensor] = None):
+    dev = t.device if t is not None else None
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _elems(t: torch.Tensor, field: int) -> int:
+    """Rust slice length of a shard: bytes (GF(2^8)) or [u8;2] elements."""
+    if t.dtype != torch.uint8:
+        raise TypeError(f"shards must be uint8 tensors, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("shards must be contiguous")
+    if field == 8:
+        return t.numel()
+    if t.dim() >= 2 and t.shape[-1] == 2:
+        return t.numel() // 2
+    if t.dim() == 1 and t.numel() % 2 == 0:
+        return t.numel() // 2
+    raise ValueError("GF(2^16) shards are uint8 tensors of shape (n, 2)")
+
+
+def _dev(t: torch.Tensor) -> int:
+    if not t.is_cuda:
+        raise ValueError("shards must be device (HBM) tensors; use encode_host() for host memory")
+    return t.data_ptr()
+
+
+def _arrays(shards, field):
+    n = len(shards)
+    ptrs = (ctypes.c_void_p * max(1, n))(*[_dev(s) for s in shards])
+    lens = (ctypes.c_size_t * max(1, n))(*[_elems(s, field) for s in shards])
+    return ptrs, lens
+
+
+class ReedSolomon:
+    """Reed-Solomon erasure code encoder/decoder (core.rs:343-350).
+
+    ``field`` is 8 (galois_8) or 16 (galois_16); prefer the aliases
+    ``galois_8.ReedSolomon`` / ``galois_16.ReedSolomon``.
+    """
+
+    def __init__(self, data_shards: int, parity_shards: int, field: int = 8):
+        if field not in (8, 16):
+            raise ValueError("field must be 8 or 16")
+        h = ctypes.c_void_p()
+        _raise(_lib.rse_codec_new(field, data_shards, parity_shards, ctypes.byref(h)))
+        self._h = h
+        self.field = field
+        self._k, self._p = data_shards, parity_shards
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.rse_codec_free(h)
+            self._h = None
+
+    # core.rs:352-364
+    def clone(self) -> "ReedSolomon":
+        other = ReedSolomon(self._k, self._p, self.field)
+        other.__class__ = type(self)
+        return other
+
+    def __eq__(self, rhs) -> bool:
+        return (isinstance(rhs, ReedSolomon) and self.field == rhs.field
+                and self._k == rhs._k and self._p == rhs._p)
+
+    def __repr__(self):
+        return f"ReedSolomon<GF(2^{self.field})>({self._k}, {self._p})"
+
+    # core.rs:469-479
+    def data_shard_count(self) -> int:
+        return self._k
+
+    def parity_shard_count(self) -> int:
+        return self._p
+
+    def total_shard_count(self) -> int:
+        return self._k + self._p
+
+    def matrix(self) -> "list":
+        """The (k+p) x k systematic encoding matrix (core.rs:430-436) as nested
+        lists of ints (GF(2^16): (coef_of_x << 8) | constant)."""
+        es = 2 if self.field == 16 else 1
+        n = (self._k + self._p) * self._k * es
+        buf = (ctypes.c_uint8 * n)()
+        _raise(_lib.rse_codec_matrix(self._h, buf, n))
+        b = bytes(buf)
+        rows = []
+        for r in range(self._k + self._p):
+            row = []
+            for c in range(self._k):
+                o = (r * self._k + c) * es
+                row.append(b[o] << 8 | b[o + 1] if es == 2 else b[o])
+            rows.append(row)
+        return rows
+
+    # ------------------------------------------------------------- encode
+    def encode(self, shards: ShardList) -> None:
+        """core.rs:597-611: overwrite shards[k:] with the parity of shards[:k]."""
+        ptrs, lens = _arrays(shards, self.field)
+        _raise(_lib.rse_encode(self._h, ptrs, lens, len(shards), _stream(_first(shards))))
+
+    def encode_sep(self, data: ShardList, parity: ShardList) -> None:
+        """core.rs:617-632."""
+        dp, dl = _arrays(data, self.field)
+        pp, pl = _arrays(parity, self.field)
+        _raise(_lib.rse_encode_sep(self._h, dp, dl, len(data), pp, pl, len(parity),
+                                   _stream(_first(data))))
+
+    def encode_single(self, i_data: int, shards: ShardList) -> None:
+        """core.rs:545-562 (i_data == 0 overwrites parity, later ones accumulate)."""
+        if i_data < 0:
+            raise RSError(Error.InvalidIndex)
+        ptrs, lens = _arrays(shards, self.field)
+        _raise(_lib.rse_encode_single(self._h, i_data, ptrs, lens, len(shards),
+                                      _stream(_first(shards))))
+
+    def encode_single_sep(self, i_data: int, single_data: torch.Tensor,
+                          parity: ShardList) -> None:
+        """core.rs:576-592."""
+        if i_data < 0:
+            raise RSError(Error.InvalidIndex)
+        pp, pl = _arrays(parity, self.field)
+        _raise(_lib.rse_encode_single_sep(self._h, i_data, _dev(single_data),
+                                          _elems(single_data, self.field), pp, pl, len(parity),
+                                          _stream(single_data)))
+
+    # ------------------------------------------------------------- verify
+    def verify(self, shards: ShardList) -> bool:
+        """core.rs:637-651."""
+        ptrs, lens = _arrays(shards, self.field)
+        ok = ctypes.c_int(0)
+        _raise(_lib.rse_verify(self._h, ptrs, lens, len(shards), ctypes.byref(ok),
+                               _stream(_first(shards))))
+        return bool(ok.value)
+
+    def verify_with_buffer(self, shards: ShardList, buffer: ShardList) -> bool:
+        """core.rs:654-669: on success `buffer` holds the correct parity."""
+        ptrs, lens = _arrays(shards, self.field)
+        bp, bl = _arrays(buffer, self.field)
+        ok = ctypes.c_int(0)
+        _raise(_lib.rse_verify_with_buffer(self._h, ptrs, lens, len(shards), bp, bl, len(buffer),
+                                           ctypes.byref(ok), _stream(_first(shards))))
+        return bool(ok.value)
+
+    # -------------------------------------------------------- reconstruct
+    def reconstruct(self, shards: list) -> None:
+        """core.rs:680-682.  `shards` is either a list of Optional[tensor]
+        (Option<T>, lib.rs:126-166: None = missing, filled in place with a new
+        tensor) or a list of (tensor, present) tuples ((T, bool), lib.rs:168-200:
+        missing buffers are overwritten)."""
+        self._reconstruct(shards, data_only=False)
+
+    def reconstruct_data(self, shards: list) -> None:
+        """core.rs:693-695: only the data shards are rebuilt."""
+        self._reconstruct(shards, data_only=True)
+
+    def _reconstruct(self, shards: list, data_only: bool) -> None:
+        if len(shards) < self.total_shard_count():
+            raise RSError(Error.TooFewShards)
+        if len(shards) > self.total_shard_count():
+            raise RSError(Error.TooManyShards)
+        flagged = len(shards) > 0 and all(isinstance(s, tuple) for s in shards)
+        if flagged:
+            bufs = [s[0] for s in shards]
+            present = [bool(s[1]) for s in shards]
+        else:
+            bufs = list(shards)
+            present = [s is not None for s in shards]
+            # Option<T> semantics: run the checks of core.rs:744-772 before
+            # allocating anything, then allocate zeroed missing shards
+            # (lib.rs:151-165; parity only when not data_only, core.rs:805-806).
+            shard_len, n_present, like = None, 0, None
+            for s in bufs:
+                if s is None:
+                    continue
+                n = _elems(s, self.field)
+                if n == 0:
+                    raise RSError(Error.EmptyShard)
+                n_present += 1
+                if shard_len is not None and n != shard_len:
+                    raise RSError(Error.IncorrectShardSize)
+                shard_len, like = n, s
+            if n_present == self.total_shard_count():
+                return
+            if n_present < self._k:
+                raise RSError(Error.TooFewShardsPresent)
+            for i, s in enumerate(bufs):
+                if s is None and (i < self._k or not data_only):
+                    shape = (shard_len,) if self.field == 8 else (shard_len, 2)
+                    bufs[i] = torch.zeros(shape, dtype=torch.uint8, device=like.device)
+        n = len(bufs)
+        ptrs = (ctypes.c_void_p * max(1, n))(
+            *[(_dev(b) if b is not None else None) for b in bufs])
+        lens = (ctypes.c_size_t * max(1, n))(
+            *[(_elems(b, self.field) if b is not None else 0) for b in bufs])
+        pres = (ctypes.c_uint8 * max(1, n))(*[1 if p else 0 for p in present])
+        like = next((b for b in bufs if b is not None), None)
+        fn = _lib.rse_reconstruct_data if data_only else _lib.rse_reconstruct
+        _raise(fn(self._h, ptrs, lens, pres, n, _stream(like)))
+        if not flagged:
+            for i in range(n):
+                shards[i] = bufs[i]
+
+    # ------------------------------------------------ beyond the reference
+    def encode_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int = 1) -> None:
+        """Encode `n_stripes` consecutive stripes of k+p shards of `shard_len`
+        elements each, laid out as wasm/src/lib.rs:45-55's flat buffer."""
+        _raise(_lib.rse_encode_flat(self._h, _dev(stripes), shard_len, n_stripes,
+                                    _stream(stripes)))
+
+    def reconstruct_data_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int,
+                              present: Sequence[bool]) -> None:
+        """wasm/src/lib.rs:57-73 over many stripes sharing one erasure pattern."""
+        pres = (ctypes.c_uint8 * len(present))(*[1 if p else 0 for p in present])
+        if len(present) != self.total_shard_count():
+            raise RSError(Error.InvalidShardFlags)
+        _raise(_lib.rse_reconstruct_data_flat(self._h, _dev(stripes), shard_len, n_stripes,
+                                              pres, _stream(stripes)))
+
+    def encode_host(self, shards: Sequence) -> None:
+        """encode() for shards in HOST memory (numpy arrays or CPU tensors;
+        pinned memory gives overlapped DMA).  Synchronous."""
+        ptrs, lens = [], []
+        for s in shards:
+            if isinstance(s, torch.Tensor):
+                if s.is_cuda:
+                    raise ValueError("encode_host takes host memory")
+                ptrs.append(s.data_ptr())
+                lens.append(_elems(s, self.field))
+            else:  # numpy
+                if s.dtype.itemsize != 1 or not s.flags["C_CONTIGUOUS"]:
+                    raise ValueError("host shards must be contiguous uint8 arrays")
+                ptrs.append(s.ctypes.data)
+                lens.append(s.size // (2 if self.field == 16 else 1))
+        n = len(shards)
+        pa = (ctypes.c_void_p * max(1, n))(*ptrs)
+        la = (ctypes.c_size_t * max(1, n))(*lens)
+        _raise(_lib.rse_encode_host(self._h, pa, la, n, _stream()))
+
+
+def _first(shards):
+    return shards[0] if len(shards) else None
+
+
+class ShardByShard:
+    """Bookkeeper for shard-by-shard encoding (core.rs:49-231)."""
+
+    def __init__(self, codec: ReedSolomon):
+        self.codec = codec
+        self.cur_input = 0
+
+    def parity_ready(self) -> bool:  # core.rs:117-119
+        return self.cur_input == self.codec.data_shard_count()
+
+    def reset(self) -> None:  # core.rs:128-136
+        if self.cur_input > 0 and not self.parity_ready():
+            raise SBSError(SBSErrorKind.LeftoverShards)
+        self.cur_input = 0
+
+    def reset_force(self) -> None:  # core.rs:139-141
+        self.cur_input = 0
+
+    def cur_input_index(self) -> int:  # core.rs:144-146
+        return self.cur_input
+
+    def _checks(self, fn):
+        if self.parity_ready():
+            raise SBSError(SBSErrorKind.TooManyCalls)
+        try:
+            fn()
+        except RSError as e:
+            raise SBSError(SBSErrorKind.RSError, e.error) from None
+
+    def encode(self, shards: ShardList) -> None:  # core.rs:201-212
+        c = self.codec
+
+        def checks():
+            n = len(shards)
+            if n < c.total_shard_count():
+                raise RSError(Error.TooFewShards)
+            if n > c.total_shard_count():
+                raise RSError(Error.TooManyShards)
+            _check_multi([_elems(s, c.field) for s in shards])
+
+        self._checks(checks)
+        c.encode_single(self.cur_input, shards)
+        self.cur_input += 1
+
+    def encode_sep(self, data: ShardList, parity: ShardList) -> None:  # core.rs:218-230
+        c = self.codec
+
+        def checks():
+            if len(data) < c.data_shard_count():
+                raise RSError(Error.TooFewDataShards)
+            if len(data) > c.data_shard_count():
+                raise RSError(Error.TooManyDataShards)
+            if len(parity) < c.parity_shard_count():
+                raise RSError(Error.TooFewParityShards)
+            if len(parity) > c.parity_shard_count():
+                raise RSError(Error.TooManyParityShards)
+            dl = [_elems(s, c.field) for s in data]
+            pl = [_elems(s, c.field) for s in parity]
+            _check_multi(dl)
+            _check_multi(pl)
+            if dl[0] != pl[0]:
+                raise RSError(Error.IncorrectShardSize)
+
+        self._checks(checks)
+        c.encode_single_sep(self.cur_input, data[self.cur_input], parity)
+        self.cur_input += 1
+
+
+def _check_multi(lens: List[int]) -> None:  # macros.rs:144-155
+    if lens[0] == 0:
+        raise RSError(Error.EmptyShard)
+    for n in lens:
+        if n != lens[0]:
+            raise RSError(Error.IncorrectShardSize)
+
+
+def code_shards(field: int, rows, inputs: ShardList, outputs: ShardList,
+                accumulate: bool = False) -> None:
+    """The fused kernel itself: outputs[r] (+)= sum_i rows[r][i] * inputs[i]
+    (core.rs:481-509 code_some_slices when accumulate is False)."""
+    n_out, n_in = len(outputs), len(inputs)
+    flat = []
+    for r in range(n_out):
+        for i in range(n_in):
+            v = int(rows[r][i])
+            flat += [v >> 8, v & 0xFF] if field == 16 else [v & 0xFF]
+    rb = (ctypes.c_uint8 * max(1, len(flat)))(*flat)
+    ip = (ctypes.c_void_p * max(1, n_in))(*[_dev(t) for t in inputs])
+    op = (ctypes.c_void_p * max(1, n_out))(*[_dev(t) for t in outputs])
+    n = _elems(inputs[0], field) if n_in else 0
+    _raise(_lib.rse_code_shards(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
+                                _stream(inputs[0] if n_in else None)))
+
+
+def fill_splitmix(t: torch.Tensor, seed: int, shard_id: int) -> None:
+    """Fill a device tensor with the synthetic byte stream of (seed, shard_id)."""
+    _raise(_lib.rse_fill_splitmix(_dev(t), t.numel() * t.element_size(), seed, shard_id,
+                                  _stream(t)))

@@ -1,0 +1,164 @@
+"""CPU-side checks of the C ABI (no device work): the library loads, exports
+every entry point include/rse_hip.h declares, builds the same matrices as the
+oracle, and reproduces the reference's validation errors before touching a GPU.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+import reed_solomon_erasure as R
+from reed_solomon_erasure import Error, RSError
+from reed_solomon_erasure._lib import EXPORTS, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+L = load()
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "rse_hip.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rse_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol():
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(L, name), name
+    assert sorted(declared) == sorted(EXPORTS)
+
+
+def test_error_strings_match_errors_rs():  # errors.rs:20-38
+    for e in Error:
+        assert L.rse_strerror(int(e)).decode() == str(e)
+    assert L.rse_strerror(0).decode() == "Ok"
+
+
+def test_codec_new_errors():  # core.rs:445-454, tests/mod.rs:97-116
+    for args, err in [((0, 1), Error.TooFewDataShards), ((1, 0), Error.TooFewParityShards),
+                      ((129, 128), Error.TooManyShards)]:
+        with pytest.raises(RSError) as ei:
+            R.galois_8.ReedSolomon(*args)
+        assert ei.value.error == err
+    R.galois_8.ReedSolomon(128, 128)
+    with pytest.raises(RSError):  # tests/galois_16.rs:24-34
+        R.galois_16.ReedSolomon(65536, 1)
+    with pytest.raises(RSError):
+        R.galois_16.ReedSolomon(1, 65536)
+
+
+def test_shard_counts_and_clone():  # tests/mod.rs:118-141
+    rng = np.random.default_rng(3)
+    for _ in range(10):
+        k, p = int(rng.integers(1, 128)), int(rng.integers(1, 128))
+        r = R.galois_8.ReedSolomon(k, p)
+        assert (r.data_shard_count(), r.parity_shard_count(), r.total_shard_count()) == (k, p, k + p)
+    r1 = R.galois_8.ReedSolomon(10, 3)
+    assert r1.clone() == r1
+
+
+@pytest.mark.parametrize("field,k,p", [(8, 1, 1), (8, 3, 2), (8, 10, 4), (8, 17, 3), (8, 128, 128),
+                                       (8, 200, 56), (16, 1, 1), (16, 20, 8), (16, 40, 24)])
+def test_matrix_matches_oracle(field, k, p):
+    r = R.core.ReedSolomon(k, p, field)
+    m = np.array(r.matrix(), dtype=np.int64)
+    om = O.Codec(field, k, p).matrix().astype(np.int64)
+    if field == 16:
+        om = om[..., 0] * 256 + om[..., 1]
+    assert (m == om).all()
+
+
+def test_matrix_matches_golden():
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
+    for name, hexstr in g["encoding_matrices"].items():
+        field, k, p = (int(x) for x in name[2:].split("_"))
+        r = R.core.ReedSolomon(k, p, field)
+        es = 2 if field == 16 else 1
+        buf = (ctypes.c_uint8 * ((k + p) * k * es))()
+        assert L.rse_codec_matrix(r._h, buf, len(buf)) == 0
+        assert bytes(buf).hex() == hexstr
+
+
+# ------- validation through the raw ABI with fake device pointers: every call
+# below fails its checks before any device access, exactly as the reference
+# returns Err before touching a slice.
+FAKE = 0x1000
+
+
+def ptrs(n):
+    return (ctypes.c_void_p * max(1, n))(*([FAKE] * n))
+
+
+def lens(xs):
+    return (ctypes.c_size_t * max(1, len(xs)))(*xs)
+
+
+def test_encode_verify_reconstruct_validation():  # tests/mod.rs:1058-1163
+    r = R.galois_8.ReedSolomon(3, 2)
+    ok = ctypes.c_int()
+    pres = (ctypes.c_uint8 * 6)(*([1] * 6))
+    for n, err in [(4, Error.TooFewShards), (6, Error.TooManyShards)]:
+        assert L.rse_encode(r._h, ptrs(n), lens([10] * n), n, None) == err
+        assert L.rse_verify(r._h, ptrs(n), lens([10] * n), n, ctypes.byref(ok), None) == err
+        assert L.rse_reconstruct(r._h, ptrs(n), lens([10] * n), pres, n, None) == err
+    r2 = R.galois_8.ReedSolomon(2, 2)
+    pres4 = (ctypes.c_uint8 * 4)(1, 1, 1, 1)
+    for ls, err in [([3, 2, 3, 3], Error.IncorrectShardSize), ([2, 2, 3, 3], Error.IncorrectShardSize),
+                    ([2, 3, 3, 3], Error.IncorrectShardSize), ([0, 3, 3, 3], Error.EmptyShard)]:
+        assert L.rse_encode(r2._h, ptrs(4), lens(ls), 4, None) == err
+        assert L.rse_verify(r2._h, ptrs(4), lens(ls), 4, ctypes.byref(ok), None) == err
+        assert L.rse_reconstruct(r2._h, ptrs(4), lens(ls), pres4, 4, None) == err
+    none = (ctypes.c_uint8 * 4)(0, 0, 0, 0)
+    assert L.rse_reconstruct(r2._h, ptrs(4), lens([3] * 4), none, 4, None) == Error.TooFewShardsPresent
+    # a missing shard's buffer must have the common size ((T,bool), lib.rs:185-199)
+    miss = (ctypes.c_uint8 * 4)(0, 1, 1, 1)
+    assert L.rse_reconstruct(r2._h, ptrs(4), lens([2, 3, 3, 3]), miss, 4, None) == \
+        Error.IncorrectShardSize
+    # all present: Ok with nothing to do (core.rs:763-767) -- no device access
+    assert L.rse_reconstruct(r2._h, ptrs(4), lens([3] * 4), pres4, 4, None) == 0
+
+
+def test_buffer_and_sep_validation():  # tests/mod.rs:905-964, 2304-2619
+    r = R.galois_8.ReedSolomon(3, 2)
+    ok = ctypes.c_int()
+    s5 = lens([100] * 5)
+    assert L.rse_verify_with_buffer(r._h, ptrs(5), s5, 5, ptrs(1), lens([100]), 1,
+                                    ctypes.byref(ok), None) == Error.TooFewBufferShards
+    assert L.rse_verify_with_buffer(r._h, ptrs(5), s5, 5, ptrs(3), lens([100] * 3), 3,
+                                    ctypes.byref(ok), None) == Error.TooManyBufferShards
+    assert L.rse_verify_with_buffer(r._h, ptrs(5), s5, 5, ptrs(2), lens([0, 100]), 2,
+                                    ctypes.byref(ok), None) == Error.EmptyShard
+    assert L.rse_verify_with_buffer(r._h, ptrs(5), s5, 5, ptrs(2), lens([100, 99]), 2,
+                                    ctypes.byref(ok), None) == Error.IncorrectShardSize
+    assert L.rse_verify_with_buffer(r._h, ptrs(5), s5, 5, ptrs(2), lens([99, 99]), 2,
+                                    ctypes.byref(ok), None) == Error.IncorrectShardSize
+    assert L.rse_encode_sep(r._h, ptrs(2), lens([9] * 2), 2, ptrs(2), lens([9] * 2), 2,
+                            None) == Error.TooFewDataShards
+    assert L.rse_encode_sep(r._h, ptrs(4), lens([9] * 4), 4, ptrs(2), lens([9] * 2), 2,
+                            None) == Error.TooManyDataShards
+    assert L.rse_encode_sep(r._h, ptrs(3), lens([9] * 3), 3, ptrs(1), lens([9]), 1,
+                            None) == Error.TooFewParityShards
+    assert L.rse_encode_sep(r._h, ptrs(3), lens([9] * 3), 3, ptrs(3), lens([9] * 3), 3,
+                            None) == Error.TooManyParityShards
+    assert L.rse_encode_sep(r._h, ptrs(3), lens([9] * 3), 3, ptrs(2), lens([8] * 2), 2,
+                            None) == Error.IncorrectShardSize
+    assert L.rse_encode_single(r._h, 3, ptrs(5), s5, 5, None) == Error.InvalidIndex
+    assert L.rse_encode_single(r._h, 0, ptrs(4), s5, 4, None) == Error.TooFewShards
+    assert L.rse_encode_single_sep(r._h, 3, FAKE, 100, ptrs(2), lens([100] * 2), 2,
+                                   None) == Error.InvalidIndex
+    assert L.rse_encode_single_sep(r._h, 0, FAKE, 100, ptrs(1), lens([100]), 1,
+                                   None) == Error.TooFewParityShards
+    assert L.rse_encode_single_sep(r._h, 0, FAKE, 99, ptrs(2), lens([100] * 2), 2,
+                                   None) == Error.IncorrectShardSize
+
+
+def test_null_arguments_are_rejected():
+    assert L.rse_codec_new(7, 1, 1, ctypes.byref(ctypes.c_void_p())) == 100
+    assert L.rse_encode(None, ptrs(2), lens([1, 1]), 2, None) == 100
+    assert L.rse_code_shards(8, None, 1, 1, ptrs(1), ptrs(1), 1, 0, None) == 100
+    assert L.rse_gf8_invert_batch(None, None, None, 3, 1, None) == 100

@@ -1,0 +1,489 @@
+"""Parity of the HIP library against the oracle and the reference's fixtures.
+
+Every test runs the product path (librse_hip.so through its C ABI, via the
+Python mirror of the reference API) on an MI355X and compares bit-for-bit with
+the CPU oracle (oracle/rse_oracle.c) or with golden vectors produced by the
+reference's own compiled kernel (tests/golden/).  Integer arithmetic: the bar
+is exact equality.
+"""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+KAT, GEN = GOLDEN["reference_kats"], GOLDEN["generated"]
+SEED = GEN["seed"]
+
+
+@pytest.fixture(scope="module")
+def R():
+    import reed_solomon_erasure as R
+    return R
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def rand_shards(rng, n_shards, n_bytes):
+    return [rng.integers(0, 256, n_bytes, dtype=np.uint8) for _ in range(n_shards)]
+
+
+def gf16_view(a):
+    return a.reshape(-1, 2)
+
+
+# ------------------------------------------------------------ kernels
+def test_native_library_is_loaded(R):
+    lib = R._lib.load()
+    assert lib.rse_version().decode().startswith("rse-mi355x")
+    assert torch.cuda.is_available()
+
+
+def test_mul_slice_kats(R):  # galois_8.rs:482-552 through rse_gf8_mul_slice
+    lib = R._lib.load()
+    inp = dev(KAT["mul_slice_input"])
+    out = torch.zeros_like(inp)
+    for c, xor, expect in KAT["mul_slice_steps"]:
+        assert lib.rse_gf8_mul_slice(c, inp.data_ptr(), out.data_ptr(), inp.numel(), int(xor),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+        assert host(out).tolist() == expect
+
+
+def test_mul_slice_every_coefficient_and_tail(R):
+    lib = R._lib.load()
+    rng = np.random.default_rng(7)
+    _, _, mul, _, _ = O.gf8_tables()
+    for n in [1, 5, 15, 16, 17, 33, 100, 4099]:
+        x = rng.integers(0, 256, n, dtype=np.uint8)
+        base = rng.integers(0, 256, n, dtype=np.uint8)
+        dx = dev(x)
+        for c in range(256):
+            for xor in (0, 1):
+                out = dev(base)
+                lib.rse_gf8_mul_slice(c, dx.data_ptr(), out.data_ptr(), n, xor,
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                want = mul[c][x] ^ (base if xor else 0)
+                assert (host(out) == want).all(), (n, c, xor)
+
+
+def test_fill_matches_host_prng(R):
+    from reed_solomon_erasure.core import fill_splitmix
+    for n in [1, 7, 8, 9, 1000, 1 << 20]:
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        fill_splitmix(t, SEED, 3)
+        assert (host(t) == O.splitmix_bytes(SEED, 3, n)).all()
+
+
+# ------------------------------------------------------------ codec KATs
+@pytest.mark.parametrize("name", ["one_encode", "readme", "reconstruct_2_2"])
+def test_encode_kats(R, name):
+    kat = KAT[name]
+    r = R.galois_8.ReedSolomon(kat["k"], kat["p"])
+    n = len(kat["data"][0])
+    shards = [dev(d) for d in kat["data"]] + [torch.full((n,), 77, dtype=torch.uint8,
+                                                         device="cuda") for _ in range(kat["p"])]
+    r.encode(shards)
+    assert [host(s).tolist() for s in shards[kat["k"]:]] == kat["parity"]
+    assert r.verify(shards)
+    shards[-1][0] += 1
+    assert not r.verify(shards)
+
+
+def test_reconstruct_kat_sequence(R):  # tests/mod.rs:249-353
+    r = R.galois_8.ReedSolomon(2, 2)
+    s = [dev([0, 1, 2]), dev([3, 4, 5]), dev([200, 201, 203]), dev([100, 101, 102])]
+    r.encode(s)
+    assert r.verify(s)
+    s[0].copy_(dev([101, 102, 103]))
+    r.reconstruct(list(zip(s, [False, True, True, True])))
+    assert r.verify(s)
+    assert [host(x).tolist() for x in s] == [[0, 1, 2], [3, 4, 5], [6, 11, 12], [5, 14, 11]]
+    s[0].copy_(dev([201, 202, 203]))
+    s[2].copy_(dev([101, 102, 103]))
+    r.reconstruct_data(list(zip(s, [False, True, False, True])))
+    assert not r.verify(s)
+    assert [host(x).tolist() for x in s] == [[0, 1, 2], [3, 4, 5], [101, 102, 103], [5, 14, 11]]
+    s[2].copy_(dev([101, 102, 103]))
+    s[3].copy_(dev([201, 202, 203]))
+    r.reconstruct_data(list(zip(s, [True, True, False, False])))
+    assert not r.verify(s)
+    assert [host(x).tolist() for x in s] == [[0, 1, 2], [3, 4, 5], [101, 102, 103], [201, 202, 203]]
+
+
+def test_reconstruct_error_handling(R):  # tests/mod.rs:810-848
+    r = R.galois_8.ReedSolomon(2, 2)
+    s = [dev([0, 1, 2]), dev([3, 4, 5]), dev([200, 201, 203]), dev([100, 101, 102])]
+    r.encode(s)
+    s[0].copy_(dev([101, 102, 103]))
+    flags = [[x, f] for x, f in zip(s, [True, False, False, False])]
+    with pytest.raises(R.RSError) as ei:
+        r.reconstruct([tuple(f) for f in flags])
+    assert ei.value.error == R.Error.TooFewShardsPresent
+    flags[3][1] = True
+    r.reconstruct([tuple(f) for f in flags])
+
+
+# ------------------------------------------------- golden vectors (reference SIMD)
+def test_encode_10_4_matches_reference_kernel_vectors(R):
+    r = R.galois_8.ReedSolomon(10, 4)
+    for n, want in GEN["gf8_10_4_encode"].items():
+        n = int(n)
+        s = [dev(O.splitmix_bytes(SEED + n, i, n)) for i in range(10)] + \
+            [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(4)]
+        r.encode(s)
+        got = [host(x) for x in s[10:]]
+        assert [sha(x) for x in got] == want["parity_sha256"], n
+        if want["parity_hex"]:
+            assert [x.tobytes().hex() for x in got] == want["parity_hex"]
+
+
+def test_full_size_digests(R):
+    """BASELINE configs at full size: 10+2 x 1 MiB, 10+4 x 16 MiB (GF(2^8),
+    reference SIMD digests) and 20+8 x 4 MiB (GF(2^16), oracle digests),
+    data generated on the device by the same PRNG."""
+    from reed_solomon_erasure.core import fill_splitmix
+    for key, want in GEN["full_size"].items():
+        f, k, p, n = key.split("_")
+        field, k, p, n = int(f[2:]), int(k), int(p), int(n)
+        r = R.core.ReedSolomon(k, p, field)
+        shape = (n,) if field == 8 else (n // 2, 2)
+        s = [torch.empty(shape, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
+        for i in range(k):
+            fill_splitmix(s[i], SEED, i)
+        r.encode(s)
+        assert [sha(host(x)) for x in s[:k]] == want["data_sha256"]
+        assert [sha(host(x)) for x in s[k:]] == want["parity_sha256"], key
+        assert r.verify(s)
+        # reconstruct with data shards 0 and 1 erased (BASELINE config 3)
+        orig = [x.clone() for x in s[:2]]
+        s[0].zero_()
+        s[1].fill_(0xA5)
+        r.reconstruct([(x, i not in (0, 1)) for i, x in enumerate(s)])
+        assert all(torch.equal(a, b) for a, b in zip(orig, s[:2]))
+        assert [sha(host(x)) for x in s[:2]] == want["data_sha256"][:2]
+
+
+# ------------------------------------------------------------ vs the oracle
+CONFIGS = [(8, 1, 1), (8, 3, 2), (8, 5, 5), (8, 10, 4), (8, 10, 2), (8, 7, 3), (8, 12, 4),
+           (8, 17, 9), (8, 33, 17), (8, 40, 20), (8, 100, 30),
+           (16, 1, 1), (16, 3, 2), (16, 10, 4), (16, 20, 8), (16, 35, 17), (16, 9, 5)]
+LENGTHS = [1, 2, 3, 15, 16, 17, 31, 63, 64, 65, 257, 4097]
+
+
+@pytest.mark.parametrize("field,k,p", CONFIGS)
+def test_encode_matches_oracle(R, field, k, p):
+    rng = np.random.default_rng(k * 131 + p + field)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    es = 2 if field == 16 else 1
+    for n in LENGTHS:
+        nb = n * es
+        data = rand_shards(rng, k, nb)
+        want = data + [np.zeros(nb, np.uint8) for _ in range(p)]
+        oc.encode(want)
+        shape = (n,) if field == 8 else (n, 2)
+        s = [dev(d).reshape(shape) for d in data] + \
+            [torch.full(shape, 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        r.encode(s)
+        for i in range(p):
+            assert (host(s[k + i]).reshape(-1) == want[k + i]).all(), (field, k, p, n, i)
+        assert r.verify(s)
+        # encode_sep gives the same bytes (tests/mod.rs:591-662)
+        par = [torch.zeros(shape, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        r.encode_sep(s[:k], par)
+        assert all(torch.equal(a, b) for a, b in zip(par, s[k:]))
+
+
+@pytest.mark.parametrize("field", [8, 16])
+def test_unaligned_views(R, field):
+    """Shards that are not 16-B aligned take the element path; same bytes."""
+    rng = np.random.default_rng(11)
+    k, p = 6, 3
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    es = 2 if field == 16 else 1
+    for off in [1, 2, 3, 4, 8, 15]:
+        off = off * es
+        n = 999
+        big = [dev(x) for x in rand_shards(rng, k + p, n * es + 64)]
+        views = [b[off:off + n * es] for b in big]
+        if field == 16:
+            views = [v.view(n, 2) for v in views]
+        r.encode(views)
+        arr = [host(b)[off:off + n * es].copy() for b in big]
+        want = [a.copy() for a in arr]
+        oc.encode(want)
+        assert all((a == b).all() for a, b in zip(arr, want))
+
+
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 8, 5), (8, 40, 20), (8, 3, 30),
+                                       (16, 20, 8), (16, 6, 3), (16, 36, 18)])
+def test_reconstruct_matches_oracle(R, field, k, p):
+    rng = np.random.default_rng(k * 7 + p + field)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    es = 2 if field == 16 else 1
+    n = 1037
+    shape = (n,) if field == 8 else (n, 2)
+    for trial in range(6):
+        full = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(full)
+        n_erase = int(rng.integers(1, p + 1))
+        erased = sorted(rng.choice(k + p, n_erase, replace=False).tolist())
+        present = [i not in erased for i in range(k + p)]
+        data_only = bool(trial % 2)
+        # oracle ((T, bool) semantics) on garbage-filled missing buffers
+        ob = [x.copy() for x in full]
+        for e in erased:
+            ob[e][:] = 0x33
+        oc.reconstruct(ob, present, data_only=data_only)
+        # product, (T, bool) form
+        tb = [dev(x).reshape(shape) for x in ob]
+        for e in erased:
+            tb[e].fill_(0x33)
+        (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+        for i in range(k + p):
+            assert (host(tb[i]).reshape(-1) == ob[i]).all(), (trial, erased, i, data_only)
+        for i in range(k):
+            assert (ob[i] == full[i]).all()
+        # product, Option form: missing = None, allocated and filled in place
+        opt = [dev(x).reshape(shape) if pr else None for x, pr in zip(full, present)]
+        (r.reconstruct_data if data_only else r.reconstruct)(opt)
+        for i in range(k + p):
+            if data_only and i >= k and not present[i]:
+                assert opt[i] is None
+            else:
+                assert (host(opt[i]).reshape(-1) == full[i]).all()
+
+
+def test_reconstruct_cache_hit_same_result(R):  # tests/mod.rs:167-247
+    rng = np.random.default_rng(5)
+    r = R.galois_8.ReedSolomon(8, 5)
+    master = [dev(x) for x in rand_shards(rng, 13, 100_000)]
+    r.encode(master)
+    for erase in [(0, 2), (0, 2), (0, 2, 12), (0, 1, 9, 10, 11)]:
+        s = [None if i in erase else m.clone() for i, m in enumerate(master)]
+        r.reconstruct(s)
+        assert all(torch.equal(a, b) for a, b in zip(s, master))
+        assert r.verify(s)
+    s = [None if i in (0, 1, 12) else m.clone() for i, m in enumerate(master)]
+    r.reconstruct_data(s)
+    assert torch.equal(s[0], master[0]) and torch.equal(s[1], master[1]) and s[12] is None
+
+
+def test_verify_with_buffer_gives_correct_parity(R):  # tests/mod.rs:966-1056
+    rng = np.random.default_rng(9)
+    r = R.galois_8.ReedSolomon(10, 3)
+    for _ in range(20):
+        raw = [dev(x) for x in rand_shards(rng, 13, 100)]
+        enc = [x.clone() for x in raw]
+        r.encode(enc)
+        buf = [dev(x) for x in rand_shards(rng, 3, 100)]
+        assert not r.verify_with_buffer(raw, buf)
+        assert all(torch.equal(a, b) for a, b in zip(enc[10:], buf))
+        buf = [dev(x) for x in rand_shards(rng, 3, 100)]
+        assert r.verify_with_buffer(enc, buf)
+        assert all(torch.equal(a, b) for a, b in zip(enc[10:], buf))
+
+
+def test_verify_detects_every_single_byte_corruption(R):  # tests/mod.rs:480-589
+    rng = np.random.default_rng(13)
+    for field, k, p, n in [(8, 10, 4, 4099), (16, 20, 8, 2051), (8, 40, 20, 777)]:
+        r = R.core.ReedSolomon(k, p, field)
+        shape = (n,) if field == 8 else (n, 2)
+        s = [dev(x).reshape(shape) for x in rand_shards(rng, k + p, n * (field // 8))]
+        r.encode(s)
+        assert r.verify(s)
+        for _ in range(8):
+            i = int(rng.integers(0, k + p))
+            j = int(rng.integers(0, s[i].numel()))
+            flat = s[i].view(-1)
+            old = flat[j].item()
+            flat[j] = old ^ int(rng.integers(1, 256))
+            assert not r.verify(s)
+            flat[j] = old
+        assert r.verify(s)
+
+
+# ------------------------------------------------------ shard by shard / single
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 5, 3), (16, 6, 2)])
+def test_shard_by_shard_same_as_encode(R, field, k, p):  # tests/mod.rs:1165-1317
+    rng = np.random.default_rng(17)
+    r = R.core.ReedSolomon(k, p, field)
+    n = 3001
+    shape = (n,) if field == 8 else (n, 2)
+    s = [dev(x).reshape(shape) for x in rand_shards(rng, k + p, n * (field // 8))]
+    expect = [x.clone() for x in s]
+    r.encode(expect)
+    sbs = R.ShardByShard(r)
+    for i in range(k):
+        assert not sbs.parity_ready()
+        assert sbs.cur_input_index() == i
+        sbs.encode(s)
+    assert sbs.parity_ready()
+    assert all(torch.equal(a, b) for a, b in zip(s, expect))
+    with pytest.raises(R.SBSError) as ei:
+        sbs.encode(s)
+    assert ei.value.kind == R.SBSErrorKind.TooManyCalls
+    sbs.reset()
+    # sep flavour
+    par = [torch.full(shape, 9, dtype=torch.uint8, device="cuda") for _ in range(p)]
+    for i in range(k):
+        sbs.encode_sep(s[:k], par)
+    assert all(torch.equal(a, b) for a, b in zip(par, expect[k:]))
+    sbs.reset()
+    sbs.encode(s)
+    with pytest.raises(R.SBSError) as ei:
+        sbs.reset()
+    assert ei.value.kind == R.SBSErrorKind.LeftoverShards
+    sbs.reset_force()
+    with pytest.raises(R.SBSError) as ei:
+        sbs.encode(s[:-1])
+    assert ei.value.kind == R.SBSErrorKind.RSError and ei.value.error == R.Error.TooFewShards
+
+
+def test_encode_single_sep_and_errors(R):  # tests/mod.rs:2205-2303
+    rng = np.random.default_rng(19)
+    r = R.galois_8.ReedSolomon(10, 3)
+    s = [dev(x) for x in rand_shards(rng, 13, 1000)]
+    expect = [x.clone() for x in s]
+    r.encode(expect)
+    for i in range(10):
+        r.encode_single_sep(i, s[i], s[10:])
+    assert all(torch.equal(a, b) for a, b in zip(s, expect))
+    with pytest.raises(R.RSError) as ei:
+        r.encode_single(10, s)
+    assert ei.value.error == R.Error.InvalidIndex
+    with pytest.raises(R.RSError) as ei:
+        r.encode_single_sep(0, s[0][:999], s[10:])
+    assert ei.value.error == R.Error.IncorrectShardSize
+
+
+# ------------------------------------------------------------ many stripes
+def test_encode_flat_many_stripes(R):
+    k, p, n, stripes = 10, 4, 65536 + 16, 7
+    r = R.galois_8.ReedSolomon(k, p)
+    buf = torch.empty(stripes * (k + p) * n, dtype=torch.uint8, device="cuda")
+    from reed_solomon_erasure.core import fill_splitmix
+    fill_splitmix(buf, SEED, 99)
+    ref = buf.clone().view(stripes, k + p, n)
+    r.encode_flat(buf, n, stripes)
+    for s in range(stripes):
+        shards = [ref[s, i] for i in range(k + p)]
+        r.encode(shards)
+    assert torch.equal(buf.view(stripes, k + p, n), ref)
+    # all stripes lose the same shards; reconstruct_data_flat restores data
+    erased = (1, 4, 11)
+    v = buf.view(stripes, k + p, n)
+    for e in erased:
+        v[:, e].fill_(0)
+    r.reconstruct_data_flat(buf, n, stripes, [i not in erased for i in range(k + p)])
+    assert torch.equal(v[:, :k], ref[:, :k])
+
+
+def test_encode_host_matches_device(R):
+    rng = np.random.default_rng(23)
+    k, p = 10, 4
+    r = R.galois_8.ReedSolomon(k, p)
+    for n in [100, (8 << 20) + 3, 20 << 20]:
+        data = rand_shards(rng, k, n)
+        hs = [torch.from_numpy(d).pin_memory() for d in data] + \
+             [torch.zeros(n, dtype=torch.uint8).pin_memory() for _ in range(p)]
+        r.encode_host(hs)
+        ds = [dev(d) for d in data] + [torch.empty(n, dtype=torch.uint8, device="cuda")
+                                        for _ in range(p)]
+        r.encode(ds)
+        for i in range(p):
+            assert (hs[k + i].numpy() == host(ds[k + i])).all()
+    # pageable numpy memory works too
+    data = rand_shards(rng, k, 5000)
+    hs = data + [np.zeros(5000, np.uint8) for _ in range(p)]
+    r.encode_host(hs)
+    want = data + [np.zeros(5000, np.uint8) for _ in range(p)]
+    O.Codec(8, k, p).encode(want)
+    assert all((a == b).all() for a, b in zip(hs, want))
+
+
+# ------------------------------------------------------ device inversion
+def test_device_inversion_matches_oracle(R):
+    lib = R._lib.load()
+    rng = np.random.default_rng(29)
+    oc = O.Codec(8, 10, 4)
+    m = oc.matrix()
+    mats, want = [], []
+    for _ in range(64):  # decode submatrices of random erasure patterns
+        erased = rng.choice(14, int(rng.integers(1, 5)), replace=False)
+        valid = [i for i in range(14) if i not in erased][:10]
+        mats.append(m[valid])
+        want.append(O.matrix_invert(8, m[valid]))
+    for n in [1, 3, 17, 64, 255]:  # random (mostly invertible) matrices
+        for _ in range(2):
+            a = rng.integers(0, 256, (n, n), dtype=np.uint8)
+            try:
+                want.append(O.matrix_invert(8, a))
+            except ValueError:
+                continue
+            mats.append(a)
+    by_n = {}
+    for a, w in zip(mats, want):
+        by_n.setdefault(a.shape[0], []).append((a, w))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for n, items in by_n.items():
+        src = dev(np.stack([a for a, _ in items]))
+        dst = torch.empty_like(src)
+        sing = torch.full((len(items),), 7, dtype=torch.int32, device="cuda")
+        assert lib.rse_gf8_invert_batch(src.data_ptr(), dst.data_ptr(), sing.data_ptr(), n,
+                                        len(items), stream) == 0
+        assert (host(sing) == 0).all()
+        assert (host(dst) == np.stack([w for _, w in items])).all(), n
+    # singular (matrix.rs:419-423)
+    src = dev(np.array(KAT["matrix_singular"], np.uint8)[None])
+    dst = torch.empty_like(src)
+    sing = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lib.rse_gf8_invert_batch(src.data_ptr(), dst.data_ptr(), sing.data_ptr(), 2, 1, stream)
+    assert host(sing)[0] == 1
+
+
+# ------------------------------------------------ quickcheck-style round trips
+def test_random_round_trips(R):  # tests/mod.rs:355-478, tests/galois_16.rs:36-140
+    rng = np.random.default_rng(31)
+    for trial in range(40):
+        field = 8 if trial % 3 else 16
+        k = int(rng.integers(1, 256))
+        p = int(rng.integers(1, 256))
+        if k + p > 256:
+            p -= k + p - 256
+        n = int(rng.integers(1, 3000))
+        r = R.core.ReedSolomon(k, p, field)
+        shape = (n,) if field == 8 else (n, 2)
+        expect = [dev(x).reshape(shape) for x in rand_shards(rng, k + p, n * (field // 8))]
+        r.encode(expect)
+        assert r.verify(expect)
+        corrupt = int(rng.integers(0, p + 1))
+        pos = rng.choice(k + p, corrupt, replace=False).tolist()
+        s = [x.clone() for x in expect]
+        for q in pos:
+            s[q].random_(0, 256)
+        r.reconstruct([(x, i not in pos) for i, x in enumerate(s)])
+        assert all(torch.equal(a, b) for a, b in zip(s, expect)), (field, k, p, n, pos)
+        assert r.verify(s)
