@@ -152,6 +152,16 @@ int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, si
 int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *lens,
                     size_t n_shards, rse_stream_t stream);
 
+/* ---- launch-shape options (performance only; results never change) ----- */
+#define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */
+#define RSE_OPT_GRID_X 2            /* workgroups per stripe row; 0 = automatic */
+#define RSE_OPT_STRIPES_IN_FLIGHT 3 /* stripes coded concurrently (grid.y); 0 = all */
+#define RSE_OPT_KERNEL_VARIANT 4    /* alternate compiled variant of a tuned shape; 0 = default */
+/* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
+int rse_set_option(int key, int64_t value);
+/* Current value, or -1 for an unknown key. */
+int64_t rse_get_option(int key);
+
 /* ---- utilities (benchmarks and tests) -------------------------------- */
 /* Fill device memory with the splitmix64 byte stream of (seed, shard_id):
  * 64-bit word w = mix(seed + shard_id * 2^40 + w), little endian. */

@@ -136,22 +136,21 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
   a.n_out = (uint32_t)no;
   a.mode = mode;
   a.accumulate = acc ? 1u : 0u;
-  size_t done = 0;
-  while (done < j.n_stripes) {
-    const size_t batch = std::min<size_t>(j.n_stripes - done, 65535);
-    if (done) {  // advance every pointer to stripe `done`
-      const uint64_t adv = (uint64_t)65535 * j.stripe_stride;
-      for (size_t i = 0; i < ni; ++i) a.in[i] += adv;
-      for (size_t r = 0; r < no; ++r) {
-        if (a.out[r]) a.out[r] += adv;
-        if (a.cmp[r]) a.cmp[r] += adv;
-      }
-    }
-    hipError_t e = rse::launch_code(j.field, a, (uint32_t)batch, s);
-    if (e != hipSuccess) return e;
+  a.n_stripes = 0;
+  hipError_t e = hipSuccess;
+  for (size_t done = 0; done < j.n_stripes && e == hipSuccess;) {
+    const size_t batch = std::min<size_t>(j.n_stripes - done, 0x7fffffffu);
+    a.n_stripes = (uint32_t)batch;
+    e = rse::launch_code(j.field, a, s);
     done += batch;
+    const uint64_t adv = (uint64_t)batch * j.stripe_stride;  // next batch's stripe 0
+    for (size_t i = 0; i < ni; ++i) a.in[i] += adv;
+    for (size_t r = 0; r < no; ++r) {
+      if (a.out[r]) a.out[r] += adv;
+      if (a.cmp[r]) a.cmp[r] += adv;
+    }
   }
-  return hipSuccess;
+  return e;
 }
 
 // Executes a Job; `scratch` provides per-output buffers when a CHECK job must
@@ -747,6 +746,12 @@ int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens,
   if (e2 != hipSuccess) return dev_fail(e2);
   return RSE_OK;
 }
+
+int rse_set_option(int key, int64_t value) {
+  return rse::set_option(key, value) == 0 ? RSE_OK : RSE_ERR_INVALID_ARGUMENT;
+}
+
+int64_t rse_get_option(int key) { return rse::get_option(key); }
 
 int rse_fill_splitmix(void* dst, size_t nbytes, uint64_t seed, uint64_t shard_id,
                       rse_stream_t stream) {

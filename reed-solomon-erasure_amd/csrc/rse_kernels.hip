@@ -109,11 +109,27 @@ __device__ __forceinline__ void write_tab(uint4* q, uint32_t* t2, int idx, const
   t2[idx] = t.t2;
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte global access.  NT = non-temporal (streaming) hint: every shard byte
+// is touched exactly once, so there is nothing to keep in L2/MALL.
+template <bool NT = false>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-  return *reinterpret_cast<const uint4*>(p);
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
 }
+template <bool NT = false>
 __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
-  *reinterpret_cast<uint4*>(p) = v;
+  if constexpr (NT) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
 }
 __device__ __forceinline__ bool ne4(uint4 a, uint4 b) {
   return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u;
@@ -130,7 +146,8 @@ __device__ __forceinline__ void flag_mismatch(bool diff, uint32_t* word) {
 //   KC : inputs loaded per chunk (compile time; all KC loads are issued before
 //        any arithmetic so a lane keeps KC x 16 B in flight per shard sweep)
 //   NO : output capacity (accumulators live in VGPRs)
-//   EXACT: n_in == KC and n_out == NO -- the chunk loop runs once, no guards.
+//   NOGUARD: n_out == NO and KC divides n_in -- no runtime guards.
+//   VPL: 16-byte vectors per lane per span (amortises each LDS table read).
 // grid = (blocks, stripes); each block grid-strides over 16-byte vectors.
 //
 // Table reads go through an opaque LDS offset (`lds_base`) re-materialised
@@ -150,14 +167,91 @@ __device__ __forceinline__ void pin(uint4& v) {
   pin(v.w);
 }
 
-template <int KC, int NO, bool EXACT>
-__global__ __launch_bounds__(kBlock, 4) void gf8_code_kernel(const CodeArgs a) {
-  // table (r, i) lives at index r * n_in + i
-  __shared__ uint4 tq[EXACT ? KC * NO : kMaxIn * NO];
-  __shared__ uint32_t tt2[EXACT ? KC * NO : kMaxIn * NO];
+// One span of the vector body: lane t codes the VPL vectors vfirst,
+// vfirst + kBlock, ... (each wave-instruction stays a coalesced 1 KiB; a wave
+// covers VPL KiB of every shard).  Every (input, output) table read from LDS
+// is applied to VPL*4 dwords.
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__device__ __forceinline__ void gf8_span(const CodeArgs& a, const uint4* tq, const uint32_t* tt2,
+                                         uint64_t soff, uint64_t vfirst, uint32_t n_in,
+                                         uint32_t n_out, uint32_t mode) {
+  const uint32_t lb = opaque_zero();
+  uint64_t off[VPL];
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) off[q] = soff + (vfirst + (uint64_t)q * kBlock) * 16u;
+  uint4 acc[NO][VPL];
+#pragma unroll
+  for (int r = 0; r < NO; ++r)
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) {
+      acc[r][q] = make_uint4(0u, 0u, 0u, 0u);
+      if (a.accumulate && (NOGUARD || (uint32_t)r < n_out)) acc[r][q] = ld16(a.out[r] + off[q]);
+    }
+  for (uint32_t i0 = 0; i0 < n_in; i0 += KC) {
+    uint4 x[KC][VPL];
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+      if (NOGUARD || i0 + j < n_in)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) x[j][q] = ld16<NT>(a.in[i0 + j] + off[q]);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      if (!(NOGUARD || i0 + j < n_in)) continue;
+      Sel sel[VPL][4];
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) {
+        sel[q][0] = make_sel(x[j][q].x);
+        sel[q][1] = make_sel(x[j][q].y);
+        sel[q][2] = make_sel(x[j][q].z);
+        sel[q][3] = make_sel(x[j][q].w);
+      }
+#pragma unroll
+      for (int r = 0; r < NO; ++r) {
+        if (!(NOGUARD || (uint32_t)r < n_out)) continue;
+        const Gf8Tab t = read_tab(tq, tt2, lb + r * n_in + i0 + j);
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+          acc[r][q].x ^= gf8_mul4(t, sel[q][0]);
+          acc[r][q].y ^= gf8_mul4(t, sel[q][1]);
+          acc[r][q].z ^= gf8_mul4(t, sel[q][2]);
+          acc[r][q].w ^= gf8_mul4(t, sel[q][3]);
+        }
+      }
+      // Pin the running sums after every input: without it the XOR chain is
+      // reassociated into a tree whose k*p partial products spill.
+#pragma unroll
+      for (int r = 0; r < NO; ++r)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) pin(acc[r][q]);
+    }
+  }
+  if (mode != kCheck) {
+#pragma unroll
+    for (int r = 0; r < NO; ++r)
+      if (NOGUARD || (uint32_t)r < n_out)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) st16<NT>(a.out[r] + off[q], acc[r][q]);
+  }
+  if (mode != kStore) {
+    bool diff = false;
+#pragma unroll
+    for (int r = 0; r < NO; ++r)
+      if (NOGUARD || (uint32_t)r < n_out)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) diff |= ne4(acc[r][q], ld16<NT>(a.cmp[r] + off[q]));
+    flag_mismatch(diff, a.mismatch);
+  }
+}
 
-  const uint32_t n_in = EXACT ? KC : a.n_in;
-  const uint32_t n_out = EXACT ? NO : a.n_out;
+// GF(2^8) fused coding kernel.  NOGUARD: n_out == NO and KC divides n_in.
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8_code_kernel(const CodeArgs a) {
+  // table (r, i) lives at index r * n_in + i
+  __shared__ uint4 tq[kMaxIn * NO];
+  __shared__ uint32_t tt2[kMaxIn * NO];
+
+  const uint32_t n_in = a.n_in;
+  const uint32_t n_out = NOGUARD ? NO : a.n_out;
 
   for (uint32_t t = threadIdx.x; t < n_out * n_in; t += kBlock) {
     const uint32_t r = t / n_in, i = t % n_in;
@@ -165,59 +259,24 @@ __global__ __launch_bounds__(kBlock, 4) void gf8_code_kernel(const CodeArgs a) {
   }
   __syncthreads();
 
-  const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
   const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
   const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint32_t mode = a.mode;
+  const uint64_t span = (uint64_t)kBlock * VPL;
+  const uint64_t n_full = a.n_vec / span;
 
-  for (uint64_t v = gtid; v < a.n_vec; v += gstride) {
-    const uint64_t off = soff + v * 16u;
-    const uint32_t lb = opaque_zero();
-    uint4 acc[NO];
-#pragma unroll
-    for (int r = 0; r < NO; ++r) {
-      acc[r] = make_uint4(0u, 0u, 0u, 0u);
-      if (a.accumulate && (EXACT || (uint32_t)r < n_out)) acc[r] = ld16(a.out[r] + off);
-    }
-    for (uint32_t i0 = 0; i0 < n_in; i0 += KC) {
-      uint4 x[KC];
-#pragma unroll
-      for (int j = 0; j < KC; ++j)
-        if (EXACT || i0 + j < n_in) x[j] = ld16(a.in[i0 + j] + off);
-#pragma unroll
-      for (int j = 0; j < KC; ++j) {
-        if (!(EXACT || i0 + j < n_in)) continue;
-        const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y);
-        const Sel sz = make_sel(x[j].z), sw = make_sel(x[j].w);
-#pragma unroll
-        for (int r = 0; r < NO; ++r) {
-          if (!(EXACT || (uint32_t)r < n_out)) continue;
-          const Gf8Tab t = read_tab(tq, tt2, lb + r * n_in + i0 + j);
-          acc[r].x ^= gf8_mul4(t, sx);
-          acc[r].y ^= gf8_mul4(t, sy);
-          acc[r].z ^= gf8_mul4(t, sz);
-          acc[r].w ^= gf8_mul4(t, sw);
-        }
-        // Pin the running sums after every input: without it the XOR chain is
-        // reassociated into a tree whose k*p partial products spill.
-#pragma unroll
-        for (int r = 0; r < NO; ++r) pin(acc[r]);
-      }
-    }
+  // Stripes in flight = gridDim.y: every block of row y sweeps stripes
+  // y, y + gridDim.y, ...  (gridDim.y == 1: the whole grid walks the stripes in
+  // order, keeping few DRAM regions open at a time).
+  for (uint32_t stripe = blockIdx.y; stripe < a.n_stripes; stripe += gridDim.y) {
+  const uint64_t soff = (uint64_t)stripe * a.stripe_stride;
 
-    if (mode != kCheck) {
-#pragma unroll
-      for (int r = 0; r < NO; ++r)
-        if (EXACT || (uint32_t)r < n_out) st16(a.out[r] + off, acc[r]);
-    }
-    if (mode != kStore) {
-      bool diff = false;
-#pragma unroll
-      for (int r = 0; r < NO; ++r)
-        if (EXACT || (uint32_t)r < n_out) diff |= ne4(acc[r], ld16(a.cmp[r] + off));
-      flag_mismatch(diff, a.mismatch);
-    }
-  }
+  for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
+    gf8_span<KC, NO, NOGUARD, NT, VPL>(a, tq, tt2, soff, sp * span + threadIdx.x, n_in, n_out,
+                                       mode);
+  if (VPL > 1)  // vectors after the last full span, one per lane
+    for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
+      gf8_span<KC, NO, NOGUARD, NT, 1>(a, tq, tt2, soff, v, n_in, n_out, mode);
 
   // Byte tail (len % 16), and the whole range when a pointer is not 16-B aligned.
   for (uint64_t b = a.n_vec * 16u + gtid; b < a.len; b += gstride) {
@@ -225,24 +284,25 @@ __global__ __launch_bounds__(kBlock, 4) void gf8_code_kernel(const CodeArgs a) {
     uint32_t acc[NO];
 #pragma unroll
     for (int r = 0; r < NO; ++r)
-      acc[r] = (a.accumulate && (EXACT || (uint32_t)r < n_out)) ? a.out[r][off] : 0u;
+      acc[r] = (a.accumulate && (NOGUARD || (uint32_t)r < n_out)) ? a.out[r][off] : 0u;
     const uint32_t lb = opaque_zero();
 #pragma unroll 1
     for (uint32_t i = 0; i < n_in; ++i) {
       const Sel s = make_sel(a.in[i][off]);
 #pragma unroll
       for (int r = 0; r < NO; ++r)
-        if (EXACT || (uint32_t)r < n_out) acc[r] ^= gf8_mul4(read_tab(tq, tt2, lb + r * n_in + i), s);
+        if (NOGUARD || (uint32_t)r < n_out) acc[r] ^= gf8_mul4(read_tab(tq, tt2, lb + r * n_in + i), s);
     }
     bool diff = false;
 #pragma unroll
     for (int r = 0; r < NO; ++r) {
-      if (!(EXACT || (uint32_t)r < n_out)) continue;
+      if (!(NOGUARD || (uint32_t)r < n_out)) continue;
       if (mode != kCheck) a.out[r][off] = (uint8_t)acc[r];
       if (mode != kStore) diff |= (uint8_t)acc[r] != a.cmp[r][off];
     }
     if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
   }
+  }  // stripe loop
 }
 
 // ---------------------------------------------------------------------------
@@ -278,13 +338,92 @@ __device__ __forceinline__ void gf16_sub_coefs(uint32_t c, uint32_t sub[4]) {
   sub[3] = c0;              // LL
 }
 
-template <int KC, int NO, bool EXACT>
-__global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) {
-  __shared__ uint4 tq[(EXACT ? KC * NO : kMaxIn * NO) * 4];
-  __shared__ uint32_t tt2[(EXACT ? KC * NO : kMaxIn * NO) * 4];
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__device__ __forceinline__ void gf16_span(const CodeArgs& a, const uint4* tq, const uint32_t* tt2,
+                                          uint64_t soff, uint64_t vfirst, uint32_t n_in,
+                                          uint32_t n_out, uint32_t mode) {
+  const uint32_t lb = opaque_zero();
+  uint64_t off[VPL];
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) off[q] = soff + (vfirst + (uint64_t)q * kBlock) * 16u;
+  // [r][q][0..3] = OH(elements 0-3), OL(0-3), OH(4-7), OL(4-7)
+  uint32_t o[NO][VPL][4];
+#pragma unroll
+  for (int r = 0; r < NO; ++r)
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) {
+      o[r][q][0] = o[r][q][1] = o[r][q][2] = o[r][q][3] = 0u;
+      if (a.accumulate && (NOGUARD || (uint32_t)r < n_out))
+        split_planes(ld16(a.out[r] + off[q]), o[r][q][0], o[r][q][1], o[r][q][2], o[r][q][3]);
+    }
+  for (uint32_t i0 = 0; i0 < n_in; i0 += KC) {
+    uint4 x[KC][VPL];
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+      if (NOGUARD || i0 + j < n_in)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) x[j][q] = ld16<NT>(a.in[i0 + j] + off[q]);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      if (!(NOGUARD || i0 + j < n_in)) continue;
+      Sel sel[VPL][4];  // H0, L0, H1, L1 planes
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) {
+        uint32_t h0, l0, h1, l1;
+        split_planes(x[j][q], h0, l0, h1, l1);
+        sel[q][0] = make_sel(h0);
+        sel[q][1] = make_sel(l0);
+        sel[q][2] = make_sel(h1);
+        sel[q][3] = make_sel(l1);
+      }
+#pragma unroll
+      for (int r = 0; r < NO; ++r) {
+        if (!(NOGUARD || (uint32_t)r < n_out)) continue;
+        const uint32_t base = lb + (r * n_in + i0 + j) * 4;
+        const Gf8Tab hh = read_tab(tq, tt2, base + 0);
+        const Gf8Tab lh = read_tab(tq, tt2, base + 1);
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+          o[r][q][0] ^= gf8_mul4(hh, sel[q][0]) ^ gf8_mul4(lh, sel[q][1]);
+          o[r][q][2] ^= gf8_mul4(hh, sel[q][2]) ^ gf8_mul4(lh, sel[q][3]);
+        }
+        const Gf8Tab hl = read_tab(tq, tt2, base + 2);
+        const Gf8Tab ll = read_tab(tq, tt2, base + 3);
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+          o[r][q][1] ^= gf8_mul4(hl, sel[q][0]) ^ gf8_mul4(ll, sel[q][1]);
+          o[r][q][3] ^= gf8_mul4(hl, sel[q][2]) ^ gf8_mul4(ll, sel[q][3]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NO; ++r)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) pin(o[r][q][w]);
+    }
+  }
+  bool diff = false;
+#pragma unroll
+  for (int r = 0; r < NO; ++r) {
+    if (!(NOGUARD || (uint32_t)r < n_out)) continue;
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) {
+      const uint4 ov = merge_planes(o[r][q][0], o[r][q][1], o[r][q][2], o[r][q][3]);
+      if (mode != kCheck) st16<NT>(a.out[r] + off[q], ov);
+      if (mode != kStore) diff |= ne4(ov, ld16<NT>(a.cmp[r] + off[q]));
+    }
+  }
+  if (mode != kStore) flag_mismatch(diff, a.mismatch);
+}
 
-  const uint32_t n_in = EXACT ? KC : a.n_in;
-  const uint32_t n_out = EXACT ? NO : a.n_out;
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(const CodeArgs a) {
+  __shared__ uint4 tq[kMaxIn * NO * 4];
+  __shared__ uint32_t tt2[kMaxIn * NO * 4];
+
+  const uint32_t n_in = a.n_in;
+  const uint32_t n_out = NOGUARD ? NO : a.n_out;
 
   for (uint32_t t = threadIdx.x; t < n_out * n_in; t += kBlock) {
     const uint32_t r = t / n_in, i = t % n_in;
@@ -295,65 +434,21 @@ __global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) 
   }
   __syncthreads();
 
-  const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
   const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
   const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint32_t mode = a.mode;
+  const uint64_t span = (uint64_t)kBlock * VPL;
+  const uint64_t n_full = a.n_vec / span;
 
-  for (uint64_t v = gtid; v < a.n_vec; v += gstride) {
-    const uint64_t off = soff + v * 16u;
-    const uint32_t lb = opaque_zero();
-    uint32_t oh0[NO], ol0[NO], oh1[NO], ol1[NO];
-#pragma unroll
-    for (int r = 0; r < NO; ++r) {
-      oh0[r] = ol0[r] = oh1[r] = ol1[r] = 0u;
-      if (a.accumulate && (EXACT || (uint32_t)r < n_out))
-        split_planes(ld16(a.out[r] + off), oh0[r], ol0[r], oh1[r], ol1[r]);
-    }
-    for (uint32_t i0 = 0; i0 < n_in; i0 += KC) {
-      uint4 x[KC];
-#pragma unroll
-      for (int j = 0; j < KC; ++j)
-        if (EXACT || i0 + j < n_in) x[j] = ld16(a.in[i0 + j] + off);
-#pragma unroll
-      for (int j = 0; j < KC; ++j) {
-        if (!(EXACT || i0 + j < n_in)) continue;
-        uint32_t h0, l0, h1, l1;
-        split_planes(x[j], h0, l0, h1, l1);
-        const Sel sh0 = make_sel(h0), sl0 = make_sel(l0), sh1 = make_sel(h1), sl1 = make_sel(l1);
-#pragma unroll
-        for (int r = 0; r < NO; ++r) {
-          if (!(EXACT || (uint32_t)r < n_out)) continue;
-          const uint32_t base = lb + (r * n_in + i0 + j) * 4;
-          const Gf8Tab hh = read_tab(tq, tt2, base + 0);
-          const Gf8Tab lh = read_tab(tq, tt2, base + 1);
-          oh0[r] ^= gf8_mul4(hh, sh0) ^ gf8_mul4(lh, sl0);
-          oh1[r] ^= gf8_mul4(hh, sh1) ^ gf8_mul4(lh, sl1);
-          const Gf8Tab hl = read_tab(tq, tt2, base + 2);
-          const Gf8Tab ll = read_tab(tq, tt2, base + 3);
-          ol0[r] ^= gf8_mul4(hl, sh0) ^ gf8_mul4(ll, sl0);
-          ol1[r] ^= gf8_mul4(hl, sh1) ^ gf8_mul4(ll, sl1);
-        }
-#pragma unroll
-        for (int r = 0; r < NO; ++r) {
-          pin(oh0[r]);
-          pin(ol0[r]);
-          pin(oh1[r]);
-          pin(ol1[r]);
-        }
-      }
-    }
+  for (uint32_t stripe = blockIdx.y; stripe < a.n_stripes; stripe += gridDim.y) {
+  const uint64_t soff = (uint64_t)stripe * a.stripe_stride;
 
-    bool diff = false;
-#pragma unroll
-    for (int r = 0; r < NO; ++r) {
-      if (!(EXACT || (uint32_t)r < n_out)) continue;
-      const uint4 o = merge_planes(oh0[r], ol0[r], oh1[r], ol1[r]);
-      if (mode != kCheck) st16(a.out[r] + off, o);
-      if (mode != kStore) diff |= ne4(o, ld16(a.cmp[r] + off));
-    }
-    if (mode != kStore) flag_mismatch(diff, a.mismatch);
-  }
+  for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
+    gf16_span<KC, NO, NOGUARD, NT, VPL>(a, tq, tt2, soff, sp * span + threadIdx.x, n_in, n_out,
+                                        mode);
+  if (VPL > 1)
+    for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
+      gf16_span<KC, NO, NOGUARD, NT, 1>(a, tq, tt2, soff, v, n_in, n_out, mode);
 
   // Element tail: 2 bytes per element, byte loads (any alignment).
   for (uint64_t e = a.n_vec * 8u + gtid; e * 2u < a.len; e += gstride) {
@@ -362,7 +457,7 @@ __global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) 
 #pragma unroll
     for (int r = 0; r < NO; ++r) {
       oh[r] = ol[r] = 0u;
-      if (a.accumulate && (EXACT || (uint32_t)r < n_out)) {
+      if (a.accumulate && (NOGUARD || (uint32_t)r < n_out)) {
         oh[r] = a.out[r][off];
         ol[r] = a.out[r][off + 1];
       }
@@ -373,7 +468,7 @@ __global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) 
       const Sel sh = make_sel(a.in[i][off]), sl = make_sel(a.in[i][off + 1]);
 #pragma unroll
       for (int r = 0; r < NO; ++r) {
-        if (!(EXACT || (uint32_t)r < n_out)) continue;
+        if (!(NOGUARD || (uint32_t)r < n_out)) continue;
         const uint32_t base = lb + (r * n_in + i) * 4;
         oh[r] ^= gf8_mul4(read_tab(tq, tt2, base + 0), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 1), sl);
         ol[r] ^= gf8_mul4(read_tab(tq, tt2, base + 2), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 3), sl);
@@ -382,7 +477,7 @@ __global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) 
     bool diff = false;
 #pragma unroll
     for (int r = 0; r < NO; ++r) {
-      if (!(EXACT || (uint32_t)r < n_out)) continue;
+      if (!(NOGUARD || (uint32_t)r < n_out)) continue;
       if (mode != kCheck) {
         a.out[r][off] = (uint8_t)oh[r];
         a.out[r][off + 1] = (uint8_t)ol[r];
@@ -392,42 +487,65 @@ __global__ __launch_bounds__(kBlock, 4) void gf16_code_kernel(const CodeArgs a) 
     }
     if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
   }
+  }  // stripe loop
 }
 
 // ---------------------------------------------------------------------------
 // Dispatch: exact instantiations for the configurations the reference's
 // README / benches / BASELINE configs use; capacity-bucketed generic kernels
-// (8-input chunks, 4/8/16 outputs) for everything else.
+// (8-input chunks, up to 2/4/8/16 outputs) for everything else.  Each in a
+// plain and a non-temporal flavour.
 using KernelFn = void (*)(const CodeArgs);
 
-struct Entry {
+struct Variant {
+  KernelFn fn[2];  // [nt]
+};
+struct Shape {
+  int field;
   uint32_t ni, no;
-  KernelFn fn;
+  int n;
+  Variant v[4];  // v[0] is the default (fastest measured); others for tools/tune.py
 };
 
-#define RSE_EXACT8(I, O) {I, O, gf8_code_kernel<I, O, true>}
-static const Entry kGf8Exact[] = {
-    RSE_EXACT8(10, 4), RSE_EXACT8(10, 2), RSE_EXACT8(3, 2),
-    RSE_EXACT8(5, 5),  RSE_EXACT8(2, 2),
+#define V8(KC, NO, NG, VPL) \
+  { {gf8_code_kernel<KC, NO, NG, false, VPL>, gf8_code_kernel<KC, NO, NG, true, VPL>} }
+#define V16(KC, NO, NG, VPL) \
+  { {gf16_code_kernel<KC, NO, NG, false, VPL>, gf16_code_kernel<KC, NO, NG, true, VPL>} }
+static const Shape kShapes[] = {
+    {8, 10, 4, 3, {V8(10, 4, true, 1), V8(10, 4, true, 2), V8(5, 4, true, 2)}},
+    {8, 10, 2, 2, {V8(10, 2, true, 1), V8(10, 2, true, 2)}},
+    {8, 3, 2, 1, {V8(3, 2, true, 1)}},
+    {8, 5, 5, 1, {V8(5, 5, true, 1)}},
+    {8, 2, 2, 1, {V8(2, 2, true, 1)}},
+    {16, 20, 8, 4, {V16(10, 8, true, 1), V16(4, 8, true, 2), V16(5, 8, true, 2), V16(10, 8, true, 2)}},
 };
-#undef RSE_EXACT8
+static const Variant kGf8Generic[4] = {V8(8, 2, false, 1), V8(8, 4, false, 1), V8(8, 8, false, 1),
+                                       V8(8, 16, false, 1)};
+static const Variant kGf16Generic[4] = {V16(4, 2, false, 1), V16(4, 4, false, 1),
+                                        V16(4, 8, false, 1), V16(4, 16, false, 1)};
+#undef V8
+#undef V16
 
-KernelFn pick_gf8(uint32_t ni, uint32_t no) {
-  for (const Entry& e : kGf8Exact)
-    if (e.ni == ni && e.no == no) return e.fn;
-  if (no <= 2) return gf8_code_kernel<8, 2, false>;
-  if (no <= 4) return gf8_code_kernel<8, 4, false>;
-  if (no <= 8) return gf8_code_kernel<8, 8, false>;
-  return gf8_code_kernel<8, 16, false>;
+KernelFn pick(int field, uint32_t ni, uint32_t no, int nt, int64_t variant) {
+  for (const Shape& sh : kShapes)
+    if (sh.field == field && sh.ni == ni && sh.no == no) {
+      const int v = (variant >= 0 && variant < sh.n) ? (int)variant : 0;
+      return sh.v[v].fn[nt];
+    }
+  const Variant* g = field == 8 ? kGf8Generic : kGf16Generic;
+  const int idx = no <= 2 ? 0 : no <= 4 ? 1 : no <= 8 ? 2 : 3;
+  return g[idx].fn[nt];
 }
 
-KernelFn pick_gf16(uint32_t ni, uint32_t no) {
-  if (ni == 20 && no == 8) return gf16_code_kernel<10, 8, false>;
-  if (no <= 2) return gf16_code_kernel<4, 2, false>;
-  if (no <= 4) return gf16_code_kernel<4, 4, false>;
-  if (no <= 8) return gf16_code_kernel<4, 8, false>;
-  return gf16_code_kernel<4, 16, false>;
-}
+// Launch-shape options (rse_set_option).  Defaults come from in-process A/B
+// sweeps on MI355X (tools/tune.py; DESIGN.md "Launch shape").
+struct Options {
+  int64_t nontemporal = 1;        // streaming hint on shard loads/stores
+  int64_t grid_x = 0;             // blocks per stripe row (0 = auto)
+  int64_t stripes_in_flight = 1;  // gridDim.y (0 = all stripes at once)
+  int64_t variant = 0;            // kernel variant of a tuned shape (0 = default)
+};
+Options g_opt;
 
 // ---------------------------------------------------------------------------
 // splitmix64 fill (synthetic shards; same byte stream as oracle/oracle.py).
@@ -538,20 +656,47 @@ __global__ __launch_bounds__(1024) void gf8_invert_kernel(const uint8_t* in, uin
 
 }  // namespace
 
-hipError_t launch_code(int field, const CodeArgs& args, uint32_t n_stripes,
-                       hipStream_t stream) {
+hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
   if (args.n_in == 0 || args.n_in > (uint32_t)kMaxIn || args.n_out == 0 ||
-      args.n_out > (uint32_t)kMaxOut || n_stripes == 0 || n_stripes > 65535u)
+      args.n_out > (uint32_t)kMaxOut || args.n_stripes == 0)
     return hipErrorInvalidValue;
-  KernelFn fn = field == 16 ? pick_gf16(args.n_in, args.n_out) : pick_gf8(args.n_in, args.n_out);
-  // ~8 workgroups per CU over 256 CUs in total, spread over the stripes.
+  KernelFn fn = pick(field, args.n_in, args.n_out, g_opt.nontemporal ? 1 : 0, g_opt.variant);
+  if (!fn) return hipErrorInvalidValue;
+  uint64_t gy = g_opt.stripes_in_flight > 0 ? (uint64_t)g_opt.stripes_in_flight : args.n_stripes;
+  if (gy > args.n_stripes) gy = args.n_stripes;
+  if (gy > 65535) gy = 65535;
   const uint64_t units = args.n_vec ? args.n_vec : (args.len + 1u);
-  uint64_t want = (units + kBlock - 1) / kBlock;
-  const uint64_t per_stripe_cap = (2048u + n_stripes - 1) / n_stripes;
-  uint64_t gx = want < per_stripe_cap ? want : per_stripe_cap;
+  const uint64_t want = (units + kBlock - 1) / kBlock;
+  uint64_t gx;
+  if (g_opt.grid_x > 0) {
+    gx = (uint64_t)g_opt.grid_x;
+  } else {  // ~2048 workgroups over the chip in total, see Options
+    gx = (2048u + gy - 1) / gy;
+  }
+  if (gx > want) gx = want;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(fn, dim3((uint32_t)gx, n_stripes, 1), dim3(kBlock, 1, 1), 0, stream, args);
+  hipLaunchKernelGGL(fn, dim3((uint32_t)gx, (uint32_t)gy, 1), dim3(kBlock, 1, 1), 0, stream, args);
   return hipGetLastError();
+}
+
+int set_option(int key, int64_t value) {
+  switch (key) {
+    case 1: g_opt.nontemporal = value ? 1 : 0; return 0;
+    case 2: g_opt.grid_x = value < 0 ? 0 : value; return 0;
+    case 3: g_opt.stripes_in_flight = value < 0 ? 0 : value; return 0;
+    case 4: g_opt.variant = value; return 0;
+    default: return -1;
+  }
+}
+
+int64_t get_option(int key) {
+  switch (key) {
+    case 1: return g_opt.nontemporal;
+    case 2: return g_opt.grid_x;
+    case 3: return g_opt.stripes_in_flight;
+    case 4: return g_opt.variant;
+    default: return -1;
+  }
 }
 
 hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed, uint64_t shard_id,

@@ -32,6 +32,7 @@ struct CodeArgs {
   uint8_t* out[kMaxOut];
   const uint8_t* cmp[kMaxOut];
   uint64_t stripe_stride;  // bytes between stripe s and s+1 for EVERY pointer
+  uint32_t n_stripes;      // stripes handled by this launch (>= 1)
   uint64_t n_vec;          // 16-byte vectors handled by the vector body
   uint64_t len;            // bytes per shard
   uint32_t* mismatch;      // device word, CHECK modes only
@@ -42,10 +43,13 @@ struct CodeArgs {
   uint16_t coef[kMaxOut][kMaxIn];
 };
 
-// Launch the fused coding kernel over n_stripes stripes (grid.y) on `stream`.
+// Launch the fused coding kernel over args.n_stripes stripes on `stream`.
 // field is 8 or 16.  Returns a hipError_t.
-hipError_t launch_code(int field, const CodeArgs& args, uint32_t n_stripes,
-                       hipStream_t stream);
+hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
+
+// Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
+int set_option(int key, int64_t value);
+int64_t get_option(int key);
 
 // Fill nbytes of device memory with the splitmix64 byte stream of
 // (seed, shard_id) -- identical to oracle/oracle.py: splitmix_bytes.

@@ -21,6 +21,7 @@ EXPORTS = (
     "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
     "rse_encode_flat", "rse_reconstruct_data_flat", "rse_code_shards",
     "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_fill_splitmix",
+    "rse_set_option", "rse_get_option",
 )
 
 _c = ctypes
@@ -56,6 +57,8 @@ _SIGS = {
     "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "rse_encode_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
     "rse_fill_splitmix": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64, _vp]),
+    "rse_set_option": (_c.c_int, [_c.c_int, _c.c_int64]),
+    "rse_get_option": (_c.c_int64, [_c.c_int]),
 }
 
 _LIB = None

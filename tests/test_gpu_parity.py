@@ -487,3 +487,44 @@ def test_random_round_trips(R):  # tests/mod.rs:355-478, tests/galois_16.rs:36-1
         r.reconstruct([(x, i not in pos) for i, x in enumerate(s)])
         assert all(torch.equal(a, b) for a, b in zip(s, expect)), (field, k, p, n, pos)
         assert r.verify(s)
+
+
+# ------------------------------------------------ every compiled variant
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 10, 2), (16, 20, 8), (8, 3, 2), (8, 12, 6)])
+def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
+    """Launch-shape options and alternate kernel variants (tools/tune.py) change
+    speed only: every combination must produce the oracle's bytes."""
+    lib = R._lib.load()
+    rng = np.random.default_rng(37)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    es = field // 8
+    stripes, n = 3, 512 * 16 * 3 + 16 * 7 + 5  # full VPL=2 spans, leftovers, byte tail
+    shape = (n,) if field == 8 else (n, 2)
+    saved = [lib.rse_get_option(i) for i in (1, 2, 3, 4)]
+    data = [rand_shards(rng, k, n * es) for _ in range(stripes)]
+    want = []
+    for s in range(stripes):
+        w = data[s] + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(w)
+        want.append(np.concatenate(w))
+    try:
+        for variant in range(4):
+            for nt in (0, 1):
+                for gx, gy in [(0, 1), (3, 1), (1, 0), (2, 2), (4096, 1)]:
+                    for key, val in ((1, nt), (2, gx), (3, gy), (4, variant)):
+                        lib.rse_set_option(key, val)
+                    buf = torch.empty(stripes * (k + p) * n * es, dtype=torch.uint8, device="cuda")
+                    v = buf.view(stripes, k + p, n * es)
+                    for s in range(stripes):
+                        for i in range(k):
+                            v[s, i].copy_(dev(data[s][i]))
+                    r.encode_flat(buf, n, stripes)
+                    got = host(buf).reshape(stripes, -1)
+                    for s in range(stripes):
+                        assert (got[s] == want[s]).all(), (variant, nt, gx, gy, s)
+                    shards = [v[0, i].view(*shape) for i in range(k + p)]
+                    assert r.verify(shards)
+    finally:
+        for key, val in zip((1, 2, 3, 4), saved):
+            lib.rse_set_option(key, val)

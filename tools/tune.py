@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""In-process A/B sweep of the fused encode kernel's launch shape on MI355X.
+
+Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
+every configuration is timed once per round, the median over rounds reported.
+
+    python tools/tune.py [--stripes 128] [--rounds 5] [--k 10 --p 4]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-erasure_amd"))
+
+import torch  # noqa: E402
+
+import reed_solomon_erasure as R  # noqa: E402
+from reed_solomon_erasure.core import fill_splitmix  # noqa: E402
+
+MiB = 1 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--p", type=int, default=4)
+    ap.add_argument("--field", type=int, default=8)
+    ap.add_argument("--shard-mib", type=int, default=16)
+    ap.add_argument("--op", default="encode", choices=["encode", "reconstruct"])
+    ap.add_argument("--variants", type=int, default=1)
+    args = ap.parse_args()
+    lib = R._lib.load()
+    k, p, L, S = args.k, args.p, args.shard_mib * MiB, args.stripes
+    buf = torch.empty(S * (k + p) * L, dtype=torch.uint8, device="cuda")
+    v = buf.view(S, k + p, L)
+    for s in range(S):
+        for i in range(k):
+            fill_splitmix(v[s, i], 1, (s << 8) | i)
+    r = R.core.ReedSolomon(k, p, args.field)
+    elems = L // (args.field // 8)
+    present = [i not in (0, 1) for i in range(k + p)]
+
+    def op():
+        if args.op == "encode":
+            r.encode_flat(buf, elems, S)
+        else:
+            r.reconstruct_data_flat(buf, elems, S, present)
+
+    nbytes = S * ((k + p) if args.op == "encode" else (k + 2)) * L
+    shapes = [(1024, 1), (2048, 1), (4096, 1), (4, 0), (8, 0), (16, 0)]
+    configs = [(nt, gx, gy, var) for var in range(args.variants) for nt in (0, 1)
+               for gx, gy in shapes]
+    res = {c: [] for c in configs}
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    op()
+    torch.cuda.synchronize()
+    for rnd in range(args.rounds):
+        for c in configs:
+            nt, gx, gy, var = c
+            lib.rse_set_option(1, nt)
+            lib.rse_set_option(2, gx)
+            lib.rse_set_option(3, gy)
+            lib.rse_set_option(4, var)
+            op()  # warm this shape
+            a.record()
+            op()
+            b.record()
+            torch.cuda.synchronize()
+            res[c].append(nbytes / (a.elapsed_time(b) * 1e-3) / 1e9)
+        print(f"round {rnd} done", flush=True)
+    rows = sorted(((statistics.median(x), min(x), max(x), c) for c, x in res.items()), reverse=True)
+    print(f"{args.op} GF(2^{args.field}) {k}+{p} x {args.shard_mib} MiB, {S} stripes; GB/s (1e9)")
+    for med, lo, hi, (nt, gx, gy, var) in rows:
+        print(f"  variant={var} nt={nt} grid_x={gx:<5} stripes_in_flight={gy:<3}  median "
+              f"{med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
+    b = rows[0][3]
+    print(json.dumps({"best": {"variant": b[3], "nt": b[0], "grid_x": b[1],
+                               "stripes_in_flight": b[2], "GBps": round(rows[0][0], 1)}}))
+
+
+if __name__ == "__main__":
+    main()
