@@ -156,7 +156,7 @@ int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *l
 #define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */
 #define RSE_OPT_GRID_X 2            /* workgroups per stripe row; 0 = automatic */
 #define RSE_OPT_STRIPES_IN_FLIGHT 3 /* stripes coded concurrently (grid.y); 0 = all */
-#define RSE_OPT_KERNEL_VARIANT 4    /* alternate compiled variant of a tuned shape; 0 = default */
+#define RSE_OPT_KERNEL_VARIANT 4    /* compiled variant of a tuned shape; -1 = tuned default */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

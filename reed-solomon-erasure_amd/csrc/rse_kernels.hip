@@ -274,8 +274,8 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
   for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
     gf8_span<KC, NO, NOGUARD, NT, VPL>(a, tq, tt2, soff, sp * span + threadIdx.x, n_in, n_out,
                                        mode);
-  if (VPL > 1)  // vectors after the last full span, one per lane
-    for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
+  // vectors after the last full span, one per lane
+  for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
       gf8_span<KC, NO, NOGUARD, NT, 1>(a, tq, tt2, soff, v, n_in, n_out, mode);
 
   // Byte tail (len % 16), and the whole range when a pointer is not 16-B aligned.
@@ -303,6 +303,114 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
     if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
   }
   }  // stripe loop
+}
+
+// ---------------------------------------------------------------------------
+// Software-pipelined GF(2^8) kernel for exact shapes (n_in == K, n_out == NO,
+// STORE mode, no accumulate): while a lane codes span s, the K loads of its
+// next span s + gridDim.x are already in flight, so a wave never idles on HBM
+// between spans and fewer waves (fewer open DRAM regions) keep the bus busy.
+// Spans are numbered across stripes (stripe-major), so the pipeline also runs
+// across stripe boundaries.  Partial spans and byte tails fall back to the
+// plain span code after the pipelined sweep.
+template <int K>
+__device__ __forceinline__ void load_k(uint4 (&x)[K], const CodeArgs& a, uint64_t off) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = ld16<true>(a.in[j] + off);
+}
+
+template <int K, int NO>
+__device__ __forceinline__ void code_k(const uint4 (&x)[K], const uint4* tq, const uint32_t* tt2,
+                                       const CodeArgs& a, uint64_t off) {
+  const uint32_t lb = opaque_zero();
+  uint4 acc[NO];
+#pragma unroll
+  for (int r = 0; r < NO; ++r) acc[r] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y);
+    const Sel sz = make_sel(x[j].z), sw = make_sel(x[j].w);
+#pragma unroll
+    for (int r = 0; r < NO; ++r) {
+      const Gf8Tab t = read_tab(tq, tt2, lb + r * K + j);
+      acc[r].x ^= gf8_mul4(t, sx);
+      acc[r].y ^= gf8_mul4(t, sy);
+      acc[r].z ^= gf8_mul4(t, sz);
+      acc[r].w ^= gf8_mul4(t, sw);
+    }
+#pragma unroll
+    for (int r = 0; r < NO; ++r) pin(acc[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < NO; ++r) st16<true>(a.out[r] + off, acc[r]);
+}
+
+template <int K, int NO>
+__global__ __launch_bounds__(kBlock, 2) void gf8_pipe_kernel(const CodeArgs a) {
+  __shared__ uint4 tq[K * NO];
+  __shared__ uint32_t tt2[K * NO];
+  for (uint32_t t = threadIdx.x; t < (uint32_t)(K * NO); t += kBlock)
+    write_tab(tq, tt2, t, make_gf8_tab(a.coef[t / K][t % K]));
+  __syncthreads();
+
+  const uint64_t sps = a.n_vec / kBlock;  // full spans per stripe
+  const uint64_t total = sps * a.n_stripes;
+  uint64_t sp = blockIdx.x;
+  if (sps && sp < total) {
+    uint64_t stripe = sp / sps, local = sp % sps;
+    uint64_t off = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
+    uint4 xa[K], xb[K];
+    load_k<K>(xa, a, off);
+    for (;;) {  // two spans per trip: xa/xb swap roles without register copies
+      uint64_t sp2 = sp + gridDim.x, off2 = 0;
+      const bool more = sp2 < total;
+      if (more) {
+        local += gridDim.x;
+        while (local >= sps) { local -= sps; ++stripe; }
+        off2 = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
+        load_k<K>(xb, a, off2);
+      }
+      code_k<K, NO>(xa, tq, tt2, a, off);
+      if (!more) break;
+      sp = sp2;
+      off = off2;
+      const uint64_t sp3 = sp + gridDim.x;
+      const bool more2 = sp3 < total;
+      if (more2) {
+        local += gridDim.x;
+        while (local >= sps) { local -= sps; ++stripe; }
+        off2 = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
+        load_k<K>(xa, a, off2);
+      }
+      code_k<K, NO>(xb, tq, tt2, a, off);
+      if (!more2) break;
+      sp = sp3;
+      off = off2;
+    }
+  }
+  // leftovers: vectors after the last full span of every stripe, byte tails
+  const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (uint32_t stripe = 0; stripe < a.n_stripes; ++stripe) {
+    const uint64_t soff = (uint64_t)stripe * a.stripe_stride;
+    for (uint64_t v = sps * kBlock + gtid; v < a.n_vec; v += gstride)
+      gf8_span<K, NO, true, true, 1>(a, tq, tt2, soff, v, K, NO, kStore);
+    for (uint64_t b = a.n_vec * 16u + gtid; b < a.len; b += gstride) {
+      const uint64_t off = soff + b;
+      uint32_t acc[NO];
+#pragma unroll
+      for (int r = 0; r < NO; ++r) acc[r] = 0u;
+      const uint32_t lb = opaque_zero();
+#pragma unroll 1
+      for (uint32_t i = 0; i < (uint32_t)K; ++i) {
+        const Sel s = make_sel(a.in[i][off]);
+#pragma unroll
+        for (int r = 0; r < NO; ++r) acc[r] ^= gf8_mul4(read_tab(tq, tt2, lb + r * K + i), s);
+      }
+#pragma unroll
+      for (int r = 0; r < NO; ++r) a.out[r][off] = (uint8_t)acc[r];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -446,8 +554,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
   for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
     gf16_span<KC, NO, NOGUARD, NT, VPL>(a, tq, tt2, soff, sp * span + threadIdx.x, n_in, n_out,
                                         mode);
-  if (VPL > 1)
-    for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
+  for (uint64_t v = n_full * span + gtid; v < a.n_vec; v += gstride)
       gf16_span<KC, NO, NOGUARD, NT, 1>(a, tq, tt2, soff, v, n_in, n_out, mode);
 
   // Element tail: 2 bytes per element, byte loads (any alignment).
@@ -499,25 +606,30 @@ using KernelFn = void (*)(const CodeArgs);
 
 struct Variant {
   KernelFn fn[2];  // [nt]
+  bool pipe;       // gf8_pipe_kernel: STORE mode only, no accumulate, gridDim.y == 1
 };
 struct Shape {
   int field;
   uint32_t ni, no;
-  int n;
-  Variant v[4];  // v[0] is the default (fastest measured); others for tools/tune.py
+  int n;        // variants compiled
+  int def;      // default variant (fastest in tools/tune.py sweeps)
+  Variant v[5];
 };
 
 #define V8(KC, NO, NG, VPL) \
-  { {gf8_code_kernel<KC, NO, NG, false, VPL>, gf8_code_kernel<KC, NO, NG, true, VPL>} }
+  { {gf8_code_kernel<KC, NO, NG, false, VPL>, gf8_code_kernel<KC, NO, NG, true, VPL>}, false }
 #define V16(KC, NO, NG, VPL) \
-  { {gf16_code_kernel<KC, NO, NG, false, VPL>, gf16_code_kernel<KC, NO, NG, true, VPL>} }
+  { {gf16_code_kernel<KC, NO, NG, false, VPL>, gf16_code_kernel<KC, NO, NG, true, VPL>}, false }
+#define VP8(K, NO) \
+  { {gf8_pipe_kernel<K, NO>, gf8_pipe_kernel<K, NO>}, true }
 static const Shape kShapes[] = {
-    {8, 10, 4, 3, {V8(10, 4, true, 1), V8(10, 4, true, 2), V8(5, 4, true, 2)}},
-    {8, 10, 2, 2, {V8(10, 2, true, 1), V8(10, 2, true, 2)}},
-    {8, 3, 2, 1, {V8(3, 2, true, 1)}},
-    {8, 5, 5, 1, {V8(5, 5, true, 1)}},
-    {8, 2, 2, 1, {V8(2, 2, true, 1)}},
-    {16, 20, 8, 4, {V16(10, 8, true, 1), V16(4, 8, true, 2), V16(5, 8, true, 2), V16(10, 8, true, 2)}},
+    {8, 10, 4, 4, 1, {V8(10, 4, true, 1), V8(10, 4, true, 2), V8(5, 4, true, 2), VP8(10, 4)}},
+    {8, 10, 2, 3, 0, {V8(10, 2, true, 1), V8(10, 2, true, 2), VP8(10, 2)}},
+    {8, 3, 2, 1, 0, {V8(3, 2, true, 1)}},
+    {8, 5, 5, 1, 0, {V8(5, 5, true, 1)}},
+    {8, 2, 2, 1, 0, {V8(2, 2, true, 1)}},
+    {16, 20, 8, 4, 3,
+     {V16(10, 8, true, 1), V16(4, 8, true, 2), V16(5, 8, true, 2), V16(10, 8, true, 2)}},
 };
 static const Variant kGf8Generic[4] = {V8(8, 2, false, 1), V8(8, 4, false, 1), V8(8, 8, false, 1),
                                        V8(8, 16, false, 1)};
@@ -525,16 +637,21 @@ static const Variant kGf16Generic[4] = {V16(4, 2, false, 1), V16(4, 4, false, 1)
                                         V16(4, 8, false, 1), V16(4, 16, false, 1)};
 #undef V8
 #undef V16
+#undef VP8
 
-KernelFn pick(int field, uint32_t ni, uint32_t no, int nt, int64_t variant) {
+// variant < 0 or out of range: the shape's default.  A pipelined variant is
+// only used where it applies (plain encode); otherwise the first plain one.
+const Variant* pick(int field, const CodeArgs& a, int64_t variant) {
   for (const Shape& sh : kShapes)
-    if (sh.field == field && sh.ni == ni && sh.no == no) {
-      const int v = (variant >= 0 && variant < sh.n) ? (int)variant : 0;
-      return sh.v[v].fn[nt];
+    if (sh.field == field && sh.ni == a.n_in && sh.no == a.n_out) {
+      int v = (variant > 0 && variant < sh.n) ? (int)variant : sh.def;
+      if (variant == 0) v = 0;
+      if (sh.v[v].pipe && (a.mode != kStore || a.accumulate)) v = 0;
+      return &sh.v[v];
     }
   const Variant* g = field == 8 ? kGf8Generic : kGf16Generic;
-  const int idx = no <= 2 ? 0 : no <= 4 ? 1 : no <= 8 ? 2 : 3;
-  return g[idx].fn[nt];
+  const uint32_t no = a.n_out;
+  return &g[no <= 2 ? 0 : no <= 4 ? 1 : no <= 8 ? 2 : 3];
 }
 
 // Launch-shape options (rse_set_option).  Defaults come from in-process A/B
@@ -543,7 +660,7 @@ struct Options {
   int64_t nontemporal = 1;        // streaming hint on shard loads/stores
   int64_t grid_x = 0;             // blocks per stripe row (0 = auto)
   int64_t stripes_in_flight = 1;  // gridDim.y (0 = all stripes at once)
-  int64_t variant = 0;            // kernel variant of a tuned shape (0 = default)
+  int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
 };
 Options g_opt;
 
@@ -660,11 +777,12 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
   if (args.n_in == 0 || args.n_in > (uint32_t)kMaxIn || args.n_out == 0 ||
       args.n_out > (uint32_t)kMaxOut || args.n_stripes == 0)
     return hipErrorInvalidValue;
-  KernelFn fn = pick(field, args.n_in, args.n_out, g_opt.nontemporal ? 1 : 0, g_opt.variant);
-  if (!fn) return hipErrorInvalidValue;
+  const Variant* var = pick(field, args, g_opt.variant);
+  KernelFn fn = var->fn[g_opt.nontemporal ? 1 : 0];
   uint64_t gy = g_opt.stripes_in_flight > 0 ? (uint64_t)g_opt.stripes_in_flight : args.n_stripes;
   if (gy > args.n_stripes) gy = args.n_stripes;
   if (gy > 65535) gy = 65535;
+  if (var->pipe) gy = 1;
   const uint64_t units = args.n_vec ? args.n_vec : (args.len + 1u);
   const uint64_t want = (units + kBlock - 1) / kBlock;
   uint64_t gx;

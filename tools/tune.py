@@ -52,7 +52,7 @@ def main():
             r.reconstruct_data_flat(buf, elems, S, present)
 
     nbytes = S * ((k + p) if args.op == "encode" else (k + 2)) * L
-    shapes = [(1024, 1), (2048, 1), (4096, 1), (4, 0), (8, 0), (16, 0)]
+    shapes = [(512, 1), (1024, 1), (2048, 1), (4096, 1), (8, 0), (16, 0)]
     configs = [(nt, gx, gy, var) for var in range(args.variants) for nt in (0, 1)
                for gx, gy in shapes]
     res = {c: [] for c in configs}
