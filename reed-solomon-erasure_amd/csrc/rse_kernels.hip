@@ -313,14 +313,64 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
 // Spans are numbered across stripes (stripe-major), so the pipeline also runs
 // across stripe boundaries.  Partial spans and byte tails fall back to the
 // plain span code after the pipelined sweep.
+// The K loads of a span are issued from inline asm and waited for by hand:
+// hipcc's own vmcnt accounting is conservative across the loop back-edge and
+// drains the next span's loads before the current span is coded (measured:
+// vmcnt(7)..vmcnt(0) inside the compute).  Invariant kept here: between a
+// span's loads and its coding, the only younger vector-memory operations of the
+// wave are the previous span's NO stores (older than the next loads) and, when
+// `more`, the next span's K loads; so input j is complete once at most
+// K - 1 - j (+ K when more) operations are outstanding.  Waiting with that
+// count ignores the NO stores, which only makes the wait stricter.
 template <int K>
-__device__ __forceinline__ void load_k(uint4 (&x)[K], const CodeArgs& a, uint64_t off) {
+__device__ __forceinline__ void load_k(u32x4 (&x)[K], const CodeArgs& a, uint64_t off) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) x[j] = ld16<true>(a.in[j] + off);
+  for (int j = 0; j < K; ++j)
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(x[j]) : "v"(a.in[j] + off) : "memory");
 }
 
-template <int K, int NO>
-__device__ __forceinline__ void code_k(const uint4 (&x)[K], const uint4* tq, const uint32_t* tt2,
+// s_waitcnt vmcnt(n) that also "produces" v, so v's consumers stay behind it.
+// n is a compile-time constant after unrolling; the switch folds away.
+__device__ __forceinline__ void wait_vm(int n, u32x4& v) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) :: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" : "+v"(v) :: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" : "+v"(v) :: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" : "+v"(v) :: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" : "+v"(v) :: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" : "+v"(v) :: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" : "+v"(v) :: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" : "+v"(v) :: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" : "+v"(v) :: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" : "+v"(v) :: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" : "+v"(v) :: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" : "+v"(v) :: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" : "+v"(v) :: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" : "+v"(v) :: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" : "+v"(v) :: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" : "+v"(v) :: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" : "+v"(v) :: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" : "+v"(v) :: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" : "+v"(v) :: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" : "+v"(v) :: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" : "+v"(v) :: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" : "+v"(v) :: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" : "+v"(v) :: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" : "+v"(v) :: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" : "+v"(v) :: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" : "+v"(v) :: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" : "+v"(v) :: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" : "+v"(v) :: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" : "+v"(v) :: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" : "+v"(v) :: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" : "+v"(v) :: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" : "+v"(v) :: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) :: "memory"); break;
+  }
+}
+
+template <int K, int NO, int NB>
+__device__ __forceinline__ void code_k(u32x4 (&x)[K], const uint4* tq, const uint32_t* tt2,
                                        const CodeArgs& a, uint64_t off) {
   const uint32_t lb = opaque_zero();
   uint4 acc[NO];
@@ -328,6 +378,7 @@ __device__ __forceinline__ void code_k(const uint4 (&x)[K], const uint4* tq, con
   for (int r = 0; r < NO; ++r) acc[r] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
   for (int j = 0; j < K; ++j) {
+    wait_vm(NB + K - 1 - j, x[j]);
     const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y);
     const Sel sz = make_sel(x[j].z), sw = make_sel(x[j].w);
 #pragma unroll
@@ -338,6 +389,7 @@ __device__ __forceinline__ void code_k(const uint4 (&x)[K], const uint4* tq, con
       acc[r].z ^= gf8_mul4(t, sz);
       acc[r].w ^= gf8_mul4(t, sw);
     }
+    // also orders input j's arithmetic before input j+1's wait (both volatile)
 #pragma unroll
     for (int r = 0; r < NO; ++r) pin(acc[r]);
   }
@@ -359,7 +411,7 @@ __global__ __launch_bounds__(kBlock, 2) void gf8_pipe_kernel(const CodeArgs a) {
   if (sps && sp < total) {
     uint64_t stripe = sp / sps, local = sp % sps;
     uint64_t off = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
-    uint4 xa[K], xb[K];
+    u32x4 xa[K], xb[K];
     load_k<K>(xa, a, off);
     for (;;) {  // two spans per trip: xa/xb swap roles without register copies
       uint64_t sp2 = sp + gridDim.x, off2 = 0;
@@ -369,21 +421,24 @@ __global__ __launch_bounds__(kBlock, 2) void gf8_pipe_kernel(const CodeArgs a) {
         while (local >= sps) { local -= sps; ++stripe; }
         off2 = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
         load_k<K>(xb, a, off2);
+        code_k<K, NO, K>(xa, tq, tt2, a, off);
+      } else {
+        code_k<K, NO, 0>(xa, tq, tt2, a, off);
+        break;
       }
-      code_k<K, NO>(xa, tq, tt2, a, off);
-      if (!more) break;
       sp = sp2;
       off = off2;
       const uint64_t sp3 = sp + gridDim.x;
-      const bool more2 = sp3 < total;
-      if (more2) {
+      if (sp3 < total) {
         local += gridDim.x;
         while (local >= sps) { local -= sps; ++stripe; }
         off2 = stripe * a.stripe_stride + (local * kBlock + threadIdx.x) * 16u;
         load_k<K>(xa, a, off2);
+        code_k<K, NO, K>(xb, tq, tt2, a, off);
+      } else {
+        code_k<K, NO, 0>(xb, tq, tt2, a, off);
+        break;
       }
-      code_k<K, NO>(xb, tq, tt2, a, off);
-      if (!more2) break;
       sp = sp3;
       off = off2;
     }
