@@ -76,6 +76,24 @@ def init_dist(args):
     return world, rank, local
 
 
+def reduce_timing(elapsed: float, world: int, device=None) -> float:
+    """Job time = the slowest rank's timed region (all_reduce MAX).  The only
+    collective in the benchmark; stripes never cross ranks."""
+    if world == 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(steps: int, stripes_per_rank: int, world: int, stripe_bytes: int,
+                   elapsed_max: float) -> float:
+    """Whole-job MB/s (MB = 2^20): every rank's stripes over the slowest rank's time."""
+    return steps * stripes_per_rank * world * stripe_bytes / elapsed_max / MiB
+
+
 # ------------------------------------------------------------ CPU baseline
 def cpu_baseline(k, p, shard_bytes, seconds):
     """The reference's simd-accel path (simd_c/reedsolomon.c compiled from the
@@ -196,12 +214,8 @@ def main(argv=None):
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    bytes_all = args.steps * total_stripes * stripe_bytes
-    value = bytes_all / elapsed / MiB
+    elapsed = reduce_timing(elapsed, world, device="cuda")
+    value = job_throughput(args.steps, n_local, world, stripe_bytes, elapsed)
 
     extras = {}
     if rank == 0 and not args.no_extras:

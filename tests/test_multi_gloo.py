@@ -1,0 +1,90 @@
+"""The multi-GPU path of bench.py, rehearsed on CPU with 2 gloo ranks.
+
+Each rank encodes its own block of global stripes (bench.stripes_for_rank) with
+the CPU checker standing in for the GPU kernel, the slowest rank's time is
+all-reduced (bench.reduce_timing) and the job throughput aggregated
+(bench.job_throughput).  Checks: the partition is disjoint and complete, the
+aggregate equals the single-process computation, and every stripe's parity is
+identical whichever rank encoded it (stripes are independent, so placement
+cannot change results).
+"""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+from oracle import oracle as O
+
+K, P, L, STRIPES_PER_RANK = 4, 2, 4096, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _stripe_digest(g):
+    c = O.Codec(8, K, P)
+    shards = [O.splitmix_bytes(bench.SEED, bench.shard_id(g, i), L) for i in range(K)]
+    shards += [np.zeros(L, np.uint8) for _ in range(P)]
+    c.encode(shards)
+    return hashlib.sha256(b"".join(x.tobytes() for x in shards[K:])).hexdigest()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = bench.stripes_for_rank(STRIPES_PER_RANK * world, rank, world)
+    digests = {g: _stripe_digest(g) for g in mine}
+    elapsed = 0.5 + rank  # deterministic stand-in for the timed region
+    t = bench.reduce_timing(elapsed, world)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, digests)
+    if rank == 0:
+        q.put((t, gathered, [list(bench.stripes_for_rank(STRIPES_PER_RANK * world, r, world))
+                             for r in range(world)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_stripe_split_and_reduction():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    t, gathered, parts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # partition: disjoint, complete, equal sizes (weak scaling)
+    flat = [g for part in parts for g in part]
+    assert sorted(flat) == list(range(STRIPES_PER_RANK * world))
+    assert all(len(part) == STRIPES_PER_RANK for part in parts)
+    # timing reduction is the max over ranks; throughput counts every rank's bytes
+    assert t == 1.5
+    stripe_bytes = (K + P) * L
+    v = bench.job_throughput(3, STRIPES_PER_RANK, world, stripe_bytes, t)
+    assert v == pytest.approx(3 * STRIPES_PER_RANK * world * stripe_bytes / 1.5 / (1 << 20))
+    # placement-independent results
+    merged = {}
+    for d in gathered:
+        merged.update(d)
+    for g in range(STRIPES_PER_RANK * world):
+        assert merged[g] == _stripe_digest(g)
+
+
+def test_uneven_partition():
+    parts = [bench.stripes_for_rank(10, r, 4) for r in range(4)]
+    assert [len(p) for p in parts] == [3, 3, 2, 2]
+    assert sorted(g for p in parts for g in p) == list(range(10))

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the headline kernel from rocprofv3 PMC counters.
+
+Runs bench.py twice under rocprofv3 (one counter per pass: FETCH_SIZE, then
+WRITE_SIZE -- they cannot share a pass), keeps the dispatches of the fused
+encode kernel with the bench's grid, and applies the gfx950 correction of
+MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide
+coalesced stream, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+Writes profiles/<tag>_pmc_traffic.json, which bench.py reports as
+roofline.traffic.
+
+    python tools/pmc_traffic.py --tag r01 [bench args...]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(counter, outdir, bench_args):
+    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "gf8_code|gf8_pipe",
+           "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
+           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-extras"] + bench_args
+    out = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
+    if out.returncode != 0:
+        sys.stderr.write(out.stdout[-3000:] + out.stderr[-3000:])
+        raise SystemExit(out.returncode)
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    rows = []
+    for path in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        rows += list(csv.DictReader(open(path)))
+    return json.loads(line), rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r01")
+    args, bench_args = ap.parse_known_args()
+    base = os.path.join(ROOT, "gpurun_out", "pmc")
+    bench, fetch = run("FETCH_SIZE", base + "_fetch", bench_args)
+    _, write = run("WRITE_SIZE", base + "_write", bench_args)
+    grid = max(int(r["Grid_Size"]) for r in fetch)  # the bench's launches
+    f = [float(r["Counter_Value"]) for r in fetch if int(r["Grid_Size"]) == grid]
+    w = [float(r["Counter_Value"]) for r in write if int(r["Grid_Size"]) == grid]
+    fetch_b = 2 * sum(f) / len(f) * 1024
+    write_b = sum(w) / len(w) * 1024
+    alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    res = {
+        "workload": bench["config"]["workload"],
+        "kernel": [r["Kernel_Name"] for r in fetch][0],
+        "dispatches": len(f),
+        "fetch_size_kb_raw_mean": sum(f) / len(f),
+        "write_size_kb_raw_mean": sum(w) / len(w),
+        "hbm_read_bytes_per_launch": int(fetch_b),
+        "hbm_write_bytes_per_launch": int(write_b),
+        "hbm_bytes_per_launch": int(fetch_b + write_b),
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": round((fetch_b + write_b) / alg, 4),
+        "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md §HBM); WRITE_SIZE as is; KB = 1024 B",
+    }
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    path = os.path.join(ROOT, "profiles", f"{args.tag}_pmc_traffic.json")
+    json.dump(res, open(path, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
