@@ -509,7 +509,7 @@ def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
         oc.encode(w)
         want.append(np.concatenate(w))
     try:
-        for variant in range(4):
+        for variant in range(5):
             for nt in (0, 1):
                 for gx, gy in [(0, 1), (3, 1), (1, 0), (2, 2), (4096, 1)]:
                     for key, val in ((1, nt), (2, gx), (3, gy), (4, variant)):
