@@ -78,12 +78,25 @@ __device__ __forceinline__ Sel make_sel(uint32_t x) {
   return s;
 }
 
-// c * x for the four bytes of x (tables of c), 3 v_perm_b32 + 2 v_xor_b32.
+// a ^ b ^ c in one instruction: gfx950's v_bitop3_b32 (truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// c * x for the four bytes of x (tables of c): 3 v_perm_b32 + 1 v_bitop3_b32.
 __device__ __forceinline__ uint32_t gf8_mul4(const Gf8Tab& t, const Sel& s) {
   const uint32_t a = __builtin_amdgcn_perm(t.t0hi, t.t0lo, s.s0);
   const uint32_t b = __builtin_amdgcn_perm(t.t1hi, t.t1lo, s.s1);
   const uint32_t c = __builtin_amdgcn_perm(t.t2, t.t2, s.s2);
-  return a ^ b ^ c;
+  return xor3(a, b, c);
+}
+
+// acc ^ c*x: 3 v_perm_b32 + 2 v_bitop3_b32-class ops (acc ^ a ^ b, then ^ c).
+__device__ __forceinline__ uint32_t gf8_mac4(uint32_t acc, const Gf8Tab& t, const Sel& s) {
+  const uint32_t a = __builtin_amdgcn_perm(t.t0hi, t.t0lo, s.s0);
+  const uint32_t b = __builtin_amdgcn_perm(t.t1hi, t.t1lo, s.s1);
+  const uint32_t c = __builtin_amdgcn_perm(t.t2, t.t2, s.s2);
+  return xor3(acc, a, b) ^ c;
 }
 
 // LDS image of one table: a 16-byte part and a 4-byte part so each is one
@@ -211,10 +224,10 @@ __device__ __forceinline__ void gf8_span(const CodeArgs& a, const uint4* tq, con
         const Gf8Tab t = read_tab(tq, tt2, lb + r * n_in + i0 + j);
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
-          acc[r][q].x ^= gf8_mul4(t, sel[q][0]);
-          acc[r][q].y ^= gf8_mul4(t, sel[q][1]);
-          acc[r][q].z ^= gf8_mul4(t, sel[q][2]);
-          acc[r][q].w ^= gf8_mul4(t, sel[q][3]);
+          acc[r][q].x = gf8_mac4(acc[r][q].x, t, sel[q][0]);
+          acc[r][q].y = gf8_mac4(acc[r][q].y, t, sel[q][1]);
+          acc[r][q].z = gf8_mac4(acc[r][q].z, t, sel[q][2]);
+          acc[r][q].w = gf8_mac4(acc[r][q].w, t, sel[q][3]);
         }
       }
       // Pin the running sums after every input: without it the XOR chain is
@@ -384,10 +397,10 @@ __device__ __forceinline__ void code_k(u32x4 (&x)[K], const uint4* tq, const uin
 #pragma unroll
     for (int r = 0; r < NO; ++r) {
       const Gf8Tab t = read_tab(tq, tt2, lb + r * K + j);
-      acc[r].x ^= gf8_mul4(t, sx);
-      acc[r].y ^= gf8_mul4(t, sy);
-      acc[r].z ^= gf8_mul4(t, sz);
-      acc[r].w ^= gf8_mul4(t, sw);
+      acc[r].x = gf8_mac4(acc[r].x, t, sx);
+      acc[r].y = gf8_mac4(acc[r].y, t, sy);
+      acc[r].z = gf8_mac4(acc[r].z, t, sz);
+      acc[r].w = gf8_mac4(acc[r].w, t, sw);
     }
     // also orders input j's arithmetic before input j+1's wait (both volatile)
 #pragma unroll
@@ -547,15 +560,15 @@ __device__ __forceinline__ void gf16_span(const CodeArgs& a, const uint4* tq, co
         const Gf8Tab lh = read_tab(tq, tt2, base + 1);
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
-          o[r][q][0] ^= gf8_mul4(hh, sel[q][0]) ^ gf8_mul4(lh, sel[q][1]);
-          o[r][q][2] ^= gf8_mul4(hh, sel[q][2]) ^ gf8_mul4(lh, sel[q][3]);
+          o[r][q][0] = xor3(o[r][q][0], gf8_mul4(hh, sel[q][0]), gf8_mul4(lh, sel[q][1]));
+          o[r][q][2] = xor3(o[r][q][2], gf8_mul4(hh, sel[q][2]), gf8_mul4(lh, sel[q][3]));
         }
         const Gf8Tab hl = read_tab(tq, tt2, base + 2);
         const Gf8Tab ll = read_tab(tq, tt2, base + 3);
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
-          o[r][q][1] ^= gf8_mul4(hl, sel[q][0]) ^ gf8_mul4(ll, sel[q][1]);
-          o[r][q][3] ^= gf8_mul4(hl, sel[q][2]) ^ gf8_mul4(ll, sel[q][3]);
+          o[r][q][1] = xor3(o[r][q][1], gf8_mul4(hl, sel[q][0]), gf8_mul4(ll, sel[q][1]));
+          o[r][q][3] = xor3(o[r][q][3], gf8_mul4(hl, sel[q][2]), gf8_mul4(ll, sel[q][3]));
         }
       }
 #pragma unroll
@@ -632,8 +645,8 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
       for (int r = 0; r < NO; ++r) {
         if (!(NOGUARD || (uint32_t)r < n_out)) continue;
         const uint32_t base = lb + (r * n_in + i) * 4;
-        oh[r] ^= gf8_mul4(read_tab(tq, tt2, base + 0), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 1), sl);
-        ol[r] ^= gf8_mul4(read_tab(tq, tt2, base + 2), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 3), sl);
+        oh[r] = xor3(oh[r], gf8_mul4(read_tab(tq, tt2, base + 0), sh), gf8_mul4(read_tab(tq, tt2, base + 1), sl));
+        ol[r] = xor3(ol[r], gf8_mul4(read_tab(tq, tt2, base + 2), sh), gf8_mul4(read_tab(tq, tt2, base + 3), sl));
       }
     }
     bool diff = false;
@@ -694,12 +707,12 @@ __device__ __forceinline__ void gf16_code_chunk(u32x4 (&x)[KC], uint32_t (&o)[NO
       const uint32_t base = lb + (r * K + i0 + j) * 4;
       const Gf8Tab hh = read_tab(tq, tt2, base + 0);
       const Gf8Tab lh = read_tab(tq, tt2, base + 1);
-      o[r][0] ^= gf8_mul4(hh, sh0) ^ gf8_mul4(lh, sl0);
-      o[r][2] ^= gf8_mul4(hh, sh1) ^ gf8_mul4(lh, sl1);
+      o[r][0] = xor3(o[r][0], gf8_mul4(hh, sh0), gf8_mul4(lh, sl0));
+      o[r][2] = xor3(o[r][2], gf8_mul4(hh, sh1), gf8_mul4(lh, sl1));
       const Gf8Tab hl = read_tab(tq, tt2, base + 2);
       const Gf8Tab ll = read_tab(tq, tt2, base + 3);
-      o[r][1] ^= gf8_mul4(hl, sh0) ^ gf8_mul4(ll, sl0);
-      o[r][3] ^= gf8_mul4(hl, sh1) ^ gf8_mul4(ll, sl1);
+      o[r][1] = xor3(o[r][1], gf8_mul4(hl, sh0), gf8_mul4(ll, sl0));
+      o[r][3] = xor3(o[r][3], gf8_mul4(hl, sh1), gf8_mul4(ll, sl1));
     }
 #pragma unroll
     for (int r = 0; r < NO; ++r)
@@ -805,8 +818,8 @@ __global__ __launch_bounds__(kBlock, 2) void gf16_pipe_kernel(const CodeArgs a) 
 #pragma unroll
         for (int r = 0; r < NO; ++r) {
           const uint32_t base = lb + (r * K + i) * 4;
-          oh[r] ^= gf8_mul4(read_tab(tq, tt2, base + 0), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 1), sl);
-          ol[r] ^= gf8_mul4(read_tab(tq, tt2, base + 2), sh) ^ gf8_mul4(read_tab(tq, tt2, base + 3), sl);
+          oh[r] = xor3(oh[r], gf8_mul4(read_tab(tq, tt2, base + 0), sh), gf8_mul4(read_tab(tq, tt2, base + 1), sl));
+          ol[r] = xor3(ol[r], gf8_mul4(read_tab(tq, tt2, base + 2), sh), gf8_mul4(read_tab(tq, tt2, base + 3), sl));
         }
       }
 #pragma unroll
