@@ -125,6 +125,19 @@ int rse_encode_flat(const rse_codec *codec, void *stripes, size_t shard_len,
  * (wasm reconstruct(): reconstruct_data semantics). */
 int rse_reconstruct_data_flat(const rse_codec *codec, void *stripes, size_t shard_len,
                               size_t n_stripes, const uint8_t *present, rse_stream_t stream);
+/* Same layout; EVERY stripe has its own erasure pattern: present is
+ * n_stripes x (k+p) flags, row s for stripe s.  reconstruct (data_only = 0,
+ * core.rs:680) or reconstruct_data (data_only = 1, core.rs:690) of each stripe,
+ * with the per-stripe planning of core.rs:733-923 (valid/invalid partition,
+ * decode-matrix inversion, composed parity rows) done by a HIP kernel: two
+ * launches for the whole batch.  Errors (TooFewShardsPresent / EmptyShard for
+ * the first offending stripe) are detected before any stripe is modified.
+ * GF(2^8) with k <= 32 and p <= 16 runs on the device planner; other codecs
+ * fall back to the host planner stripe by stripe (same results).  Returns after
+ * the work is queued and the host inputs have been consumed. */
+int rse_reconstruct_batch(const rse_codec *codec, void *stripes, size_t shard_len,
+                          size_t n_stripes, const uint8_t *present, int data_only,
+                          rse_stream_t stream);
 
 /* ---- low level: the fused kernel itself ------------------------------ */
 /* outputs[r] (+)= sum_i rows[r*n_in + i] * inputs[i] over len elements.

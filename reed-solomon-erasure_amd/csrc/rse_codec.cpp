@@ -654,6 +654,61 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
   return run_job(j, (hipStream_t)stream);
 }
 
+// Many stripes, each with its own erasure pattern, in two launches: the plan
+// (partition + k x k inverse + composed rows, core.rs:733-923) is computed per
+// stripe on the device, then every stripe is coded from its descriptor.  No
+// host round trip and no decode-matrix cache: a batch of distinct patterns
+// costs one inversion per stripe on the GPU instead of one per stripe on the
+// host.  Validation happens up front on the host, so an error leaves every
+// stripe untouched.
+int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
+                          const uint8_t* present, int data_only, rse_stream_t stream) {
+  if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t T = c->total, sb = shard_len * c->esize();
+  for (size_t s = 0; s < n_stripes; ++s) {  // core.rs:747-772, stripe by stripe
+    size_t np = 0;
+    for (size_t i = 0; i < T; ++i) np += present[s * T + i] ? 1 : 0;
+    if (np && shard_len == 0) return RSE_EMPTY_SHARD;
+    if (np < c->k) return RSE_TOO_FEW_SHARDS_PRESENT;
+  }
+  uint8_t* base = static_cast<uint8_t*>(stripes);
+  hipStream_t st = (hipStream_t)stream;
+  if (c->field != RSE_FIELD_GF8 || c->k > (size_t)kMaxIn || c->p > (size_t)kMaxOut ||
+      n_stripes > 0xffffffffu) {
+    std::vector<void*> ptrs(T);
+    std::vector<size_t> lens(T, shard_len);
+    for (size_t s = 0; s < n_stripes; ++s) {
+      for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb;
+      int rc = reconstruct_impl(c, ptrs.data(), lens.data(), present + s * T, T, data_only != 0, st);
+      if (rc) return rc;
+    }
+    return RSE_OK;
+  }
+  const size_t mat_bytes = T * c->k, pres_off = (mat_bytes + 255) & ~size_t(255);
+  const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
+  const size_t ws_bytes = desc_off + n_stripes * sizeof(CodeArgs);
+  std::vector<uint8_t> mat(mat_bytes);
+  for (size_t r = 0; r < T; ++r)
+    for (size_t j = 0; j < c->k; ++j) mat[r * c->k + j] = (uint8_t)c->mat(r, j);
+  uint8_t* ws = nullptr;
+  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), ws_bytes, st));
+  hipError_t e = hipMemcpyAsync(ws, mat.data(), mat_bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = rse::launch_recon_batch(ws, ws + pres_off, (uint32_t)c->k, (uint32_t)T,
+                                data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes,
+                                reinterpret_cast<CodeArgs*>(ws + desc_off), st);
+  hipError_t f = hipFreeAsync(ws, st);
+  if (e != hipSuccess) return dev_fail(e);
+  if (f != hipSuccess) return dev_fail(f);
+  // The pageable copies above were staged before returning, but `mat` dies
+  // here: make sure the runtime is done reading it.
+  RSE_HIP(hipStreamSynchronize(st));
+  return RSE_OK;
+}
+
 int rse_code_shards(int field, const uint8_t* rows, size_t n_out, size_t n_in,
                     const void* const* inputs, void* const* outputs, size_t len, int accumulate,
                     rse_stream_t stream) {

@@ -258,7 +258,8 @@ __device__ __forceinline__ void gf8_span(const CodeArgs& a, const uint4* tq, con
 
 // GF(2^8) fused coding kernel.  NOGUARD: n_out == NO and KC divides n_in.
 template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
-__global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8_code_kernel(const CodeArgs a) {
+__device__ __forceinline__ void gf8_code_impl(const CodeArgs& a, uint32_t stripe0,
+                                              uint32_t stripe_step) {
   // table (r, i) lives at index r * n_in + i
   __shared__ uint4 tq[kMaxIn * NO];
   __shared__ uint32_t tt2[kMaxIn * NO];
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
   // Stripes in flight = gridDim.y: every block of row y sweeps stripes
   // y, y + gridDim.y, ...  (gridDim.y == 1: the whole grid walks the stripes in
   // order, keeping few DRAM regions open at a time).
-  for (uint32_t stripe = blockIdx.y; stripe < a.n_stripes; stripe += gridDim.y) {
+  for (uint32_t stripe = stripe0; stripe < a.n_stripes; stripe += stripe_step) {
   const uint64_t soff = (uint64_t)stripe * a.stripe_stride;
 
   for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
@@ -316,6 +317,21 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
     if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
   }
   }  // stripe loop
+}
+
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8_code_kernel(
+    const CodeArgs a) {
+  gf8_code_impl<KC, NO, NOGUARD, NT, VPL>(a, blockIdx.y, gridDim.y);
+}
+
+// Per-stripe descriptors in HBM (written by gf8_recon_plan_kernel): row y of
+// the grid codes stripe y with its own shard pointers and coefficient rows.
+template <bool NT>
+__global__ __launch_bounds__(kBlock, 3) void gf8_code_desc_kernel(const CodeArgs* __restrict__ descs) {
+  const CodeArgs& a = descs[blockIdx.y];
+  if (a.n_out == 0) return;  // uniform: nothing missing in this stripe
+  gf8_code_impl<8, kMaxOut, false, NT, 1>(a, 0, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -860,7 +876,7 @@ struct Shape {
   { {gf16_pipe_kernel<KC, CPS, NO>, gf16_pipe_kernel<KC, CPS, NO>}, true }
 static const Shape kShapes[] = {
     {8, 10, 4, 4, 1, {V8(10, 4, true, 1), V8(10, 4, true, 2), V8(5, 4, true, 2), VP8(10, 4)}},
-    {8, 10, 2, 3, 0, {V8(10, 2, true, 1), V8(10, 2, true, 2), VP8(10, 2)}},
+    {8, 10, 2, 3, 1, {V8(10, 2, true, 1), V8(10, 2, true, 2), VP8(10, 2)}},
     {8, 3, 2, 1, 0, {V8(3, 2, true, 1)}},
     {8, 5, 5, 1, 0, {V8(5, 5, true, 1)}},
     {8, 2, 2, 1, 0, {V8(2, 2, true, 1)}},
@@ -1008,6 +1024,132 @@ __global__ __launch_bounds__(1024) void gf8_invert_kernel(const uint8_t* in, uin
   if (tid == 0) singular[blockIdx.x] = 0u;
 }
 
+// One workgroup per stripe: the reconstruct planning of core.rs:733-923 on the
+// device -- the valid/invalid partition (core.rs:801-841), the k x k inverse of
+// the valid rows (core.rs:711-722; Gauss-Jordan in LDS, the unique inverse of
+// matrix.rs:195-261), the rows that rebuild each missing data shard
+// (core.rs:850-861) and, unless data_only, each missing parity shard composed
+// over the valid inputs (core.rs:872-918, exact GF algebra) -- written as the
+// stripe's CodeArgs for gf8_code_desc_kernel.  k <= kMaxIn, p <= kMaxOut.
+__global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
+    const uint8_t* __restrict__ matrix, const uint8_t* __restrict__ present, uint32_t k,
+    uint32_t total, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint64_t n_vec,
+    CodeArgs* descs) {
+  __shared__ uint8_t lg[256], ex[512];
+  __shared__ uint8_t valid[kMaxIn], miss[kMaxIn + kMaxOut];
+  __shared__ uint8_t w[kMaxIn][2 * kMaxIn];
+  __shared__ uint8_t drow[kMaxIn][kMaxIn];
+  __shared__ int s_nout, s_piv;
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const uint8_t* pres = present + (size_t)s * total;
+  CodeArgs& d = descs[s];
+  if (tid == 0) {
+    uint32_t b = 1;
+    for (uint32_t l = 0; l < 255; ++l) {
+      lg[b] = (uint8_t)l;
+      ex[l] = ex[l + 255] = (uint8_t)b;
+      b <<= 1;
+      if (b & 0x100u) b ^= 0x11Du;
+    }
+    lg[0] = 0;
+    ex[510] = ex[511] = 0;
+    uint32_t nv = 0, nm = 0;
+    for (uint32_t row = 0; row < total; ++row) {
+      if (pres[row]) {
+        if (nv < k) valid[nv++] = (uint8_t)row;
+      } else if (row < k || !data_only) {
+        miss[nm++] = (uint8_t)row;  // data first: indices ascend
+      }
+    }
+    s_nout = (int)nm;
+    d.n_out = nm;
+    d.n_in = k;
+    d.n_stripes = 1;
+    d.stripe_stride = 0;
+    d.n_vec = n_vec;
+    d.len = shard_bytes;
+    d.mismatch = nullptr;
+    d.mode = kStore;
+    d.accumulate = 0;
+  }
+  __syncthreads();
+  const uint32_t n_out = (uint32_t)s_nout;
+  if (n_out == 0) return;  // uniform
+  const uint8_t* sbase = base + (uint64_t)s * total * shard_bytes;
+  for (uint32_t i = tid; i < k; i += nt) d.in[i] = sbase + (uint64_t)valid[i] * shard_bytes;
+  for (uint32_t o = tid; o < n_out; o += nt) {
+    d.out[o] = const_cast<uint8_t*>(sbase) + (uint64_t)miss[o] * shard_bytes;
+    d.cmp[o] = nullptr;
+  }
+  // [M_valid | I] and Gauss-Jordan
+  const uint32_t w2 = 2 * k;
+  for (uint32_t t = tid; t < k * w2; t += nt) {
+    const uint32_t r = t / w2, c = t % w2;
+    w[r][c] = c < k ? matrix[valid[r] * k + c] : (uint8_t)((c - k) == r ? 1 : 0);
+  }
+  __syncthreads();
+  for (uint32_t col = 0; col < k; ++col) {
+    if (tid == 0) {
+      int piv = -1;
+      for (uint32_t r = col; r < k; ++r)
+        if (w[r][col]) { piv = (int)r; break; }
+      s_piv = piv;
+    }
+    __syncthreads();
+    const int piv = s_piv;
+    if (piv < 0) {  // singular: impossible for this MDS code; leave the stripe untouched
+      if (tid == 0) d.n_out = 0;
+      return;
+    }
+    if ((uint32_t)piv != col) {
+      for (uint32_t c = tid; c < w2; c += nt) {
+        const uint8_t t0 = w[col][c];
+        w[col][c] = w[piv][c];
+        w[piv][c] = t0;
+      }
+      __syncthreads();
+    }
+    const uint32_t inv = ex[255 - lg[w[col][col]]];
+    __syncthreads();
+    for (uint32_t c = tid; c < w2; c += nt) w[col][c] = (uint8_t)gmul(lg, ex, inv, w[col][c]);
+    __syncthreads();
+    for (uint32_t t = tid; t < k * w2; t += nt) {
+      const uint32_t r = t / w2, c = t % w2;
+      if (r == col || c == col) continue;
+      const uint32_t f = w[r][col];
+      if (f) w[r][c] ^= (uint8_t)gmul(lg, ex, f, w[col][c]);
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < k; r += nt)
+      if (r != col) w[r][col] = 0;
+    __syncthreads();
+  }
+  // data_row(j): unit vector for a present data shard (always among the valid
+  // rows), row j of the inverse for a missing one.
+  for (uint32_t t = tid; t < k * k; t += nt) {
+    const uint32_t j = t / k, i = t % k;
+    drow[j][i] = (valid[i] == j) ? 1 : 0;
+  }
+  __syncthreads();
+  for (uint32_t t = tid; t < k * k; t += nt) {
+    const uint32_t j = t / k, i = t % k;
+    bool present_j = false;
+    for (uint32_t q = 0; q < k; ++q) present_j |= valid[q] == j;
+    if (!present_j) drow[j][i] = w[j][k + i];
+  }
+  __syncthreads();
+  for (uint32_t t = tid; t < n_out * k; t += nt) {
+    const uint32_t o = t / k, i = t % k, m = miss[o];
+    uint32_t v = 0;
+    if (m < k) {
+      v = drow[m][i];
+    } else {
+      for (uint32_t j = 0; j < k; ++j) v ^= gmul(lg, ex, matrix[m * k + j], drow[j][i]);
+    }
+    d.coef[o][i] = (uint16_t)v;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
@@ -1032,6 +1174,35 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(fn, dim3((uint32_t)gx, (uint32_t)gy, 1), dim3(kBlock, 1, 1), 0, stream, args);
   return hipGetLastError();
+}
+
+hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
+                              uint32_t total, uint32_t data_only, uint8_t* base,
+                              uint64_t shard_bytes, uint32_t n_stripes, CodeArgs* d_descs,
+                              hipStream_t stream) {
+  if (k == 0 || k > (uint32_t)kMaxIn || total - k > (uint32_t)kMaxOut || n_stripes == 0)
+    return hipErrorInvalidValue;
+  const bool al = (reinterpret_cast<uintptr_t>(base) % 16u) == 0 && shard_bytes % 16u == 0;
+  const uint64_t n_vec = al ? shard_bytes / 16u : 0;
+  hipLaunchKernelGGL(gf8_recon_plan_kernel, dim3(n_stripes), dim3(256), 0, stream, d_matrix,
+                     d_present, k, total, data_only, base, shard_bytes, n_vec, d_descs);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t units = n_vec ? n_vec : shard_bytes + 1;
+  uint64_t gx = (2048u + n_stripes - 1) / n_stripes;
+  const uint64_t want = (units + kBlock - 1) / kBlock;
+  if (gx > want) gx = want;
+  if (gx < 1) gx = 1;
+  void (*fn)(const CodeArgs*) =
+      g_opt.nontemporal ? gf8_code_desc_kernel<true> : gf8_code_desc_kernel<false>;
+  for (uint32_t y0 = 0; y0 < n_stripes; y0 += 65535u) {
+    const uint32_t gy = n_stripes - y0 < 65535u ? n_stripes - y0 : 65535u;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)gx, gy, 1),
+                       dim3(kBlock, 1, 1), 0, stream, d_descs + y0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 int set_option(int key, int64_t value) {

@@ -47,6 +47,16 @@ struct CodeArgs {
 // field is 8 or 16.  Returns a hipError_t.
 hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
 
+// Device-resident batched reconstruct (GF(2^8), k <= kMaxIn, p <= kMaxOut):
+// per stripe, plan (partition, inverse, composed rows) into d_descs[stripe]
+// on the device, then code every stripe from its descriptor.  `base` holds
+// n_stripes flat stripes of `total` shards of shard_bytes each; d_present is
+// n_stripes x total flags; d_matrix the (total x k) encoding matrix.
+hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
+                              uint32_t total, uint32_t data_only, uint8_t* base,
+                              uint64_t shard_bytes, uint32_t n_stripes, CodeArgs* d_descs,
+                              hipStream_t stream);
+
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
 int set_option(int key, int64_t value);
 int64_t get_option(int key);

@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 from typing import List, Optional, Sequence, Tuple, Union
 
+import numpy as np
 import torch
 
 from ._lib import load
@@ -53,6 +54,16 @@ def _dev(t: torch.Tensor) -> int:
     if not t.is_cuda:
         raise ValueError("shards must be device (HBM) tensors; use encode_host() for host memory")
     return t.data_ptr()
+
+
+def _check_flat(stripes: torch.Tensor, shard_len: int, n_stripes: int, total: int,
+                field: int) -> None:
+    """The flat calls take a base pointer: refuse a buffer the stripes overrun."""
+    if stripes.dtype != torch.uint8 or not stripes.is_contiguous():
+        raise ValueError("stripes must be a contiguous uint8 tensor")
+    need = n_stripes * total * shard_len * (field // 8)
+    if stripes.numel() < need:
+        raise ValueError(f"stripes holds {stripes.numel()} bytes, {need} needed")
 
 
 def _arrays(shards, field):
@@ -236,6 +247,7 @@ class ReedSolomon:
     def encode_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int = 1) -> None:
         """Encode `n_stripes` consecutive stripes of k+p shards of `shard_len`
         elements each, laid out as wasm/src/lib.rs:45-55's flat buffer."""
+        _check_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
         _raise(_lib.rse_encode_flat(self._h, _dev(stripes), shard_len, n_stripes,
                                     _stream(stripes)))
 
@@ -245,8 +257,26 @@ class ReedSolomon:
         pres = (ctypes.c_uint8 * len(present))(*[1 if p else 0 for p in present])
         if len(present) != self.total_shard_count():
             raise RSError(Error.InvalidShardFlags)
+        _check_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
         _raise(_lib.rse_reconstruct_data_flat(self._h, _dev(stripes), shard_len, n_stripes,
                                               pres, _stream(stripes)))
+
+    def reconstruct_batch(self, stripes: torch.Tensor, shard_len: int, n_stripes: int,
+                          present, data_only: bool = False) -> None:
+        """reconstruct (or reconstruct_data) of `n_stripes` flat stripes, each
+        with its OWN erasure pattern: `present` is n_stripes x (k+p) flags.
+        Per-stripe planning (core.rs:733-923) runs as a HIP kernel."""
+        T = self.total_shard_count()
+        flags = np.ascontiguousarray(np.asarray(
+            present.cpu() if isinstance(present, torch.Tensor) else present, dtype=bool))
+        if flags.shape != (n_stripes, T):
+            raise RSError(Error.InvalidShardFlags)
+        _check_flat(stripes, shard_len, n_stripes, T, self.field)
+        pres = flags.astype(np.uint8)
+        _raise(_lib.rse_reconstruct_batch(
+            self._h, _dev(stripes), shard_len, n_stripes,
+            pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1 if data_only else 0,
+            _stream(stripes)))
 
     def encode_host(self, shards: Sequence) -> None:
         """encode() for shards in HOST memory (numpy arrays or CPU tensors;

@@ -123,6 +123,19 @@ def test_encode_verify_reconstruct_validation():  # tests/mod.rs:1058-1163
     assert L.rse_reconstruct(r2._h, ptrs(4), lens([3] * 4), pres4, 4, None) == 0
 
 
+def test_reconstruct_batch_validation():  # core.rs:747-772 per stripe, before any device work
+    r = R.galois_8.ReedSolomon(3, 2)
+    pres = (ctypes.c_uint8 * 10)(1, 1, 1, 1, 1, 0, 0, 1, 1, 0)  # stripe 1: 2 present
+    assert L.rse_reconstruct_batch(r._h, FAKE, 10, 2, pres, 0, None) == Error.TooFewShardsPresent
+    assert L.rse_reconstruct_batch(r._h, FAKE, 10, 2, pres, 1, None) == Error.TooFewShardsPresent
+    ok = (ctypes.c_uint8 * 10)(*([1] * 10))
+    assert L.rse_reconstruct_batch(r._h, FAKE, 0, 2, ok, 0, None) == Error.EmptyShard
+    assert L.rse_reconstruct_batch(r._h, FAKE, 10, 0, ok, 0, None) == 0
+    assert L.rse_reconstruct_batch(None, FAKE, 10, 2, ok, 0, None) == 100
+    with pytest.raises(R.RSError):  # shape of the flags
+        r.reconstruct_batch(None, 10, 2, [[True] * 5])
+
+
 def test_buffer_and_sep_validation():  # tests/mod.rs:905-964, 2304-2619
     r = R.galois_8.ReedSolomon(3, 2)
     ok = ctypes.c_int()

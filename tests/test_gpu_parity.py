@@ -401,6 +401,82 @@ def test_encode_flat_many_stripes(R):
     assert torch.equal(v[:, :k], ref[:, :k])
 
 
+@pytest.mark.parametrize("field,k,p,n,stripes", [
+    (8, 10, 4, 4096 + 16, 33),     # device planner, aligned
+    (8, 10, 4, 1037, 9),           # device planner, byte path
+    (8, 32, 16, 256, 5),           # device planner at its limits
+    (8, 1, 1, 64, 3),
+    (8, 40, 20, 512, 3),           # host-planner fallback (k > 32)
+    (16, 20, 8, 300, 4),           # host-planner fallback (GF(2^16))
+])
+def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes):
+    """rse_reconstruct_batch: every stripe with its own erasure pattern, against
+    the oracle's reconstruct of each stripe (core.rs:680/690 semantics)."""
+    rng = np.random.default_rng(field * 1000 + k * 31 + p)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    es = field // 8
+    T = k + p
+    full = []
+    for s in range(stripes):
+        st = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(st)
+        full.append(st)
+    for data_only in (False, True):
+        present = np.ones((stripes, T), bool)
+        for s in range(stripes):
+            if s % 4 == 3:
+                continue  # nothing missing
+            ne = int(rng.integers(1, p + 1))
+            present[s, rng.choice(T, ne, replace=False)] = False
+        buf = np.concatenate([np.concatenate(st) for st in full]).copy()
+        v = buf.reshape(stripes, T, n * es)
+        v[~present] = 0x5A
+        want = v.copy()
+        for s in range(stripes):
+            ob = [want[s, i].copy() for i in range(T)]
+            oc.reconstruct(ob, present[s].tolist(), data_only=data_only)
+            want[s] = np.stack(ob)
+        d = dev(buf)
+        r.reconstruct_batch(d, n, stripes, present, data_only=data_only)
+        got = host(d).reshape(stripes, T, n * es)
+        assert (got == want).all(), data_only
+        # every data shard is back; parity back unless data_only
+        for s in range(stripes):
+            for i in range(T):
+                if i < k or not data_only:
+                    assert (got[s, i] == full[s][i]).all(), (s, i, data_only)
+
+
+def test_reconstruct_batch_many_stripes_and_errors(R):
+    """> 65535 stripes (grid.y chunking), tiny unaligned shards, all patterns
+    drawn at random; errors leave every stripe untouched."""
+    k, p, n, stripes = 3, 2, 7, 70_001
+    rng = np.random.default_rng(77)
+    r = R.galois_8.ReedSolomon(k, p)
+    buf = torch.empty(stripes * (k + p) * n, dtype=torch.uint8, device="cuda")
+    buf.copy_(torch.from_numpy(rng.integers(0, 256, buf.numel(), dtype=np.uint8)))
+    r.encode_flat(buf, n, stripes)
+    master = buf.clone()
+    present = np.ones((stripes, k + p), bool)
+    for s in range(stripes):
+        present[s, rng.choice(k + p, int(rng.integers(0, p + 1)), replace=False)] = False
+    v = buf.view(stripes, k + p, n)
+    v[torch.from_numpy(~present).cuda()] = 0
+    r.reconstruct_batch(buf, n, stripes, present)
+    assert torch.equal(buf, master)
+    # one stripe with too few shards: error, nothing written
+    present[12345] = [False, False, False, True, True]
+    v[12345, :3] = 0
+    v[5, 0] = 0
+    present[5] = [False, True, True, True, True]
+    snap = buf.clone()
+    with pytest.raises(R.RSError) as ei:
+        r.reconstruct_batch(buf, n, stripes, present)
+    assert ei.value.error == R.Error.TooFewShardsPresent
+    assert torch.equal(buf, snap)
+
+
 def test_encode_host_matches_device(R):
     rng = np.random.default_rng(23)
     k, p = 10, 4
