@@ -1,0 +1,348 @@
+// rse_bitslice.hip -- bit-sliced GF(2^16) encode/verify kernels for codecs
+// whose parity matrix is known at compile time.
+//
+// Why: the table kernels in rse_kernels.hip spend 4 GF(2^8) constant
+// multiplies (3 v_perm_b32 each) per GF(2^16) coefficient and dword, which
+// makes GF(2^16) VALU-bound far below HBM speed.  Multiplication by a constant
+// c is a GF(2)-linear map on the 16 bits of an element: a 16x16 bit matrix.
+// With the data bit-sliced -- register q holds bit q of 32 elements -- a
+// multiply-accumulate is just the XOR of the input planes selected by each row
+// of that bit matrix, ~64 v_bitop3_b32 (3-input XOR) per 32 elements instead
+// of ~96 v_perm + ~64 XOR.  The encoding matrix of ReedSolomon::new (core.rs:
+// 430-436, V * (V_top)^-1 over galois_16) depends only on (k, p), so for the
+// configurations instantiated here its parity rows, and the bit matrices of
+// every coefficient, are evaluated by constexpr code and the XOR network is
+// straight-line code with no tables and no memory other than the shards.  The
+// host checks that a launch's coefficients equal the compiled ones before
+// dispatching here (anything else takes the table kernels), so a matrix
+// mismatch can only cost speed, never correctness.
+//
+// Lane layout: a workgroup of 256 lanes codes a 16 KiB chunk of every shard.
+// Lane t loads the 16-byte vectors t, t+256, t+512, t+768 of the chunk (each
+// load instruction is 4 KiB contiguous per workgroup), i.e. 16 dwords = 32
+// GF(2^16) elements.  In registers they are split into x-coefficient and
+// constant byte planes with v_perm (H = byte 0, L = byte 1 of every element,
+// galois_16.rs:49-51) and each plane is 8x8-bit transposed within byte lanes:
+// afterwards plane q < 8 holds bit q of the H bytes, plane 8 + q bit q of the
+// L bytes.  Outputs are transposed back the same way (the network is an
+// involution) and merged.  Any element order works as long as input and output
+// use the same one; this one keeps every global access coalesced.
+#include <utility>
+
+#include "rse_kernels.hpp"
+
+namespace rse {
+namespace {
+
+constexpr int kBsBlock = 256;
+constexpr uint64_t kBsChunk = 16384;  // bytes of one shard per workgroup step
+
+// ----------------------------------------------------------- constexpr GF
+// GF(2^8), generating polynomial 0x11D (build.rs:11), log/exp built the way
+// build.rs:27-48 does; GF(2^16) per galois_16.rs:146-162 (x^2 = 2x + 128).
+struct Gf8Tables {
+  uint8_t log[256] = {};
+  uint8_t exp[512] = {};
+  constexpr Gf8Tables() {
+    uint32_t b = 1;
+    for (int l = 0; l < 255; ++l) {
+      log[b] = (uint8_t)l;
+      exp[l] = exp[l + 255] = (uint8_t)b;
+      b <<= 1;
+      if (b & 0x100u) b ^= 0x11Du;
+    }
+  }
+};
+constexpr Gf8Tables kGf8{};
+
+constexpr uint8_t cmul8(uint8_t a, uint8_t b) {
+  return (a && b) ? kGf8.exp[kGf8.log[a] + kGf8.log[b]] : 0;
+}
+constexpr uint16_t cmul16(uint16_t a, uint16_t b) {
+  const uint8_t a1 = a >> 8, a0 = a & 0xFF, b1 = b >> 8, b0 = b & 0xFF;
+  const uint8_t hh = cmul8(a1, b1);
+  const uint8_t x = cmul8(a1, b0) ^ cmul8(a0, b1) ^ cmul8(2, hh);
+  const uint8_t c = cmul8(a0, b0) ^ cmul8(128, hh);
+  return (uint16_t)((x << 8) | c);
+}
+constexpr uint16_t cpow16(uint16_t a, uint32_t n) {  // galois_16.rs:80-93
+  if (n == 0) return 1;
+  if (a == 0) return 0;
+  n %= 65535u;
+  if (n == 0) return 1;
+  uint16_t r = 1, b = a;
+  while (n) {
+    if (n & 1) r = cmul16(r, b);
+    b = cmul16(b, b);
+    n >>= 1;
+  }
+  return r;
+}
+constexpr uint16_t cinv16(uint16_t a) { return cpow16(a, 65534u); }
+
+// Parity rows of the (K + P) x K encoding matrix V * (V[0..K])^-1 with
+// V[r][c] = r^c (matrix.rs:263-276, core.rs:430-436).  The inverse is unique,
+// so Gauss-Jordan here gives the same matrix as matrix.rs:195-261.
+template <int K, int P>
+struct Gf16Parity {
+  uint16_t m[P][K] = {};
+  constexpr Gf16Parity() {
+    uint16_t w[K][2 * K] = {};
+    for (int r = 0; r < K; ++r) {
+      for (int c = 0; c < K; ++c) w[r][c] = cpow16((uint16_t)r, (uint32_t)c);
+      w[r][K + r] = 1;
+    }
+    for (int col = 0; col < K; ++col) {
+      int piv = col;
+      while (w[piv][col] == 0) ++piv;
+      if (piv != col)
+        for (int c = 0; c < 2 * K; ++c) {
+          const uint16_t t = w[col][c];
+          w[col][c] = w[piv][c];
+          w[piv][c] = t;
+        }
+      const uint16_t s = cinv16(w[col][col]);
+      for (int c = 0; c < 2 * K; ++c) w[col][c] = cmul16(s, w[col][c]);
+      for (int r = 0; r < K; ++r) {
+        const uint16_t f = w[r][col];
+        if (r == col || f == 0) continue;
+        for (int c = 0; c < 2 * K; ++c) w[r][c] ^= cmul16(f, w[col][c]);
+      }
+    }
+    for (int o = 0; o < P; ++o)
+      for (int i = 0; i < K; ++i) {
+        uint16_t v = 0;
+        for (int j = 0; j < K; ++j)
+          v ^= cmul16(cpow16((uint16_t)(K + o), (uint32_t)j), w[j][K + i]);
+        m[o][i] = v;
+      }
+  }
+};
+
+// Bit matrices in plane order: plane q < 8 is bit q of the H (x-coefficient)
+// byte = bit q + 8 of the uint16 element, plane q >= 8 bit q - 8 of the L byte
+// = bit q - 8, i.e. uint16 bit (q ^ 8).  sel[o][i][p] = the input planes whose
+// XOR is output plane p of coefficient (o, i).
+template <int K, int P>
+struct Gf16Planes {
+  Gf16Parity<K, P> par{};
+  uint16_t sel[P][K][16] = {};
+  constexpr Gf16Planes() {
+    for (int o = 0; o < P; ++o)
+      for (int i = 0; i < K; ++i)
+        for (int q = 0; q < 16; ++q) {
+          const uint16_t col = cmul16(par.m[o][i], (uint16_t)(1u << (q ^ 8)));
+          for (int p = 0; p < 16; ++p)
+            if ((col >> (p ^ 8)) & 1u) sel[o][i][p] |= (uint16_t)(1u << q);
+        }
+  }
+};
+
+template <int K, int P>
+struct Gf16Code {
+  static constexpr int k = K, p = P;
+  static constexpr Gf16Planes<K, P> planes{};
+};
+
+// ------------------------------------------------------------ bit slicing
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// XOR of acc and the planes selected by M, two at a time.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t (&in)[16]) {
+  if constexpr (M == 0) {
+    return acc;
+  } else {
+    constexpr int q0 = __builtin_ctz(M);
+    constexpr uint32_t m1 = M & (M - 1);
+    if constexpr (m1 == 0) {
+      return acc ^ in[q0];
+    } else {
+      constexpr int q1 = __builtin_ctz(m1);
+      return xacc<m1 & (m1 - 1)>(xor3(acc, in[q0], in[q1]), in);
+    }
+  }
+}
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xinit(const uint32_t (&in)[16]) {
+  if constexpr (M == 0) {
+    return 0u;
+  } else {
+    constexpr int q0 = __builtin_ctz(M);
+    return xacc<M & (M - 1)>(in[q0], in);
+  }
+}
+
+// 8x8 bit transpose inside every byte lane of h[0..7] (an involution): bit b
+// of byte lane L of h[i] moves to bit i of byte lane L of h[b].
+__device__ __forceinline__ void transpose8(uint32_t* h) {
+#pragma unroll
+  for (int s = 4, st = 0; st < 3; s >>= 1, ++st) {
+    const uint32_t m = s == 4 ? 0x0F0F0F0Fu : s == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i & s) continue;
+      const uint32_t a = h[i], b = h[i + s];
+      h[i] = (a & ~(m << s)) | ((b & m) << s);
+      h[i + s] = (b & ~m) | ((a >> s) & m);
+    }
+  }
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// 4 vectors (16 dwords, 32 elements) -> 16 planes.
+__device__ __forceinline__ void slice(const u32x4 (&v)[4], uint32_t (&pl)[16]) {
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const uint32_t x0 = v[m >> 1][(m & 1) * 2], x1 = v[m >> 1][(m & 1) * 2 + 1];
+    pl[m] = __builtin_amdgcn_perm(x1, x0, 0x06040200u);      // H bytes
+    pl[8 + m] = __builtin_amdgcn_perm(x1, x0, 0x07050301u);  // L bytes
+  }
+  transpose8(pl);
+  transpose8(pl + 8);
+}
+
+// 16 planes -> 4 vectors (inverse of slice; clobbers pl).
+__device__ __forceinline__ void unslice(uint32_t (&pl)[16], u32x4 (&v)[4]) {
+  transpose8(pl);
+  transpose8(pl + 8);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    v[m >> 1][(m & 1) * 2] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x05010400u);
+    v[m >> 1][(m & 1) * 2 + 1] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x07030602u);
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ldv(const uint8_t* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void stv(uint8_t* p, u32x4 v) {
+  u32x4* q = reinterpret_cast<u32x4*>(p);
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = ldv<NT>(p + j * (kBsBlock * 16));
+}
+
+// acc[o*16 + p] (^)= plane combination of input I for every output o, plane p.
+template <class C, int I, int... OP>
+__device__ __forceinline__ void mac_input(uint32_t (&acc)[C::p * 16], const uint32_t (&in)[16],
+                                          std::integer_sequence<int, OP...>) {
+  if constexpr (I == 0)
+    ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % 16]>(in)), ...);
+  else
+    ((acc[OP] = xacc<C::planes.sel[OP / 16][I][OP % 16]>(acc[OP], in)), ...);
+}
+
+// Inputs I.. of one chunk: the loads of input I + 1 are issued before input
+// I is coded, so one input's worth of vectors is always in flight.
+template <class C, bool NT, int I>
+__device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
+                                            const CodeArgs& a, uint64_t off) {
+  u32x4 nxt[4];
+  if constexpr (I + 1 < C::k) load4<NT>(nxt, a.in[I + 1] + off);
+  uint32_t pl[16];
+  slice(cur, pl);
+  mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
+  // keep each input's XORs together: without this the compiler reassociates
+  // across inputs and keeps several inputs' planes live (spills)
+#pragma unroll
+  for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+  if constexpr (I + 1 < C::k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    code_inputs<C, NT, I + 1>(acc, cur, a, off);
+  }
+}
+
+// One workgroup step = one 16 KiB chunk of one stripe; chunks of all stripes
+// are one flat index space walked grid-stride.  a.n_vec counts whole chunks'
+// vectors only (the host codes the remainder with the table kernels).
+template <class C, bool NT>
+__global__ __launch_bounds__(kBsBlock, 2) void gf16_bitslice_kernel(const CodeArgs a,
+                                                                   uint64_t chunks_per_stripe) {
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint32_t mode = a.mode;
+  bool diff = false;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+    uint32_t acc[C::p * 16];
+    u32x4 cur[4];
+    load4<NT>(cur, a.in[0] + off);
+    code_inputs<C, NT, 0>(acc, cur, a, off);
+#pragma unroll
+    for (int o = 0; o < C::p; ++o) {
+      uint32_t pl[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
+      u32x4 v[4];
+      unslice(pl, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t o16 = off + j * (kBsBlock * 16);
+        if (mode != kCheck) stv<NT>(a.out[o] + o16, v[j]);
+        if (mode != kStore) {
+          const u32x4 w = ldv<NT>(a.cmp[o] + o16);
+          diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
+        }
+      }
+    }
+  }
+  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+}
+
+using BsFn = void (*)(const CodeArgs, uint64_t);
+struct BsShape {
+  uint32_t k, p;
+  const uint16_t* m;  // P x K parity rows compiled into the kernel
+  BsFn fn[2];         // [nt]
+};
+
+#define BS16(K, P)                                                            \
+  {K, P, &Gf16Code<K, P>::planes.par.m[0][0],                               \
+   {gf16_bitslice_kernel<Gf16Code<K, P>, false>, gf16_bitslice_kernel<Gf16Code<K, P>, true>}}
+static const BsShape kBs16[] = {
+    BS16(20, 8),  // BASELINE configs[4]: galois_16 20+8
+};
+#undef BS16
+
+}  // namespace
+
+hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
+                           hipStream_t stream, bool* handled) {
+  *handled = false;
+  if (field != 16 || a.accumulate || a.n_vec < kBsChunk / 16) return hipSuccess;
+  for (const BsShape& sh : kBs16) {
+    if (sh.k != a.n_in || sh.p != a.n_out) continue;
+    for (uint32_t o = 0; o < sh.p; ++o)
+      for (uint32_t i = 0; i < sh.k; ++i)
+        if (a.coef[o][i] != sh.m[o * sh.k + i]) return hipSuccess;
+    const uint64_t cps = a.n_vec / (kBsChunk / 16);
+    const uint64_t total = cps * a.n_stripes;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : 1024u;
+    if (gx > total) gx = total;
+    if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+    hipLaunchKernelGGL(sh.fn[nt ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    *handled = true;
+    return hipSuccess;
+  }
+  return hipSuccess;
+}
+
+uint64_t bitslice_chunk_bytes() { return kBsChunk; }
+
+}  // namespace rse

@@ -914,7 +914,9 @@ struct Options {
   int64_t grid_x = 0;             // blocks per stripe row (0 = auto)
   int64_t stripes_in_flight = 1;  // gridDim.y (0 = all stripes at once)
   int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
+  int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
 };
+thread_local int64_t g_last_path = 0;  // 1 if the last launch_code used a bit-sliced kernel
 Options g_opt;
 
 // ---------------------------------------------------------------------------
@@ -1156,6 +1158,33 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
   if (args.n_in == 0 || args.n_in > (uint32_t)kMaxIn || args.n_out == 0 ||
       args.n_out > (uint32_t)kMaxOut || args.n_stripes == 0)
     return hipErrorInvalidValue;
+  g_last_path = 0;
+  if (g_opt.bitslice) {
+    bool handled = false;
+    hipError_t e = launch_bitslice(field, args, g_opt.nontemporal != 0, g_opt.grid_x, stream,
+                                   &handled);
+    if (e != hipSuccess) return e;
+    if (handled) {
+      g_last_path = 1;
+      // the bit-sliced kernel codes whole chunks; the rest goes to the table kernels
+      const uint64_t cb = bitslice_chunk_bytes();
+      const uint64_t done = (args.n_vec * 16u / cb) * cb;
+      if (done == args.len) return hipSuccess;
+      CodeArgs r = args;
+      for (uint32_t i = 0; i < r.n_in; ++i) r.in[i] += done;
+      for (uint32_t o = 0; o < r.n_out; ++o) {
+        r.out[o] += done;
+        if (r.cmp[o]) r.cmp[o] += done;
+      }
+      r.len -= done;
+      r.n_vec -= done / 16u;
+      return launch_table(field, r, stream);
+    }
+  }
+  return launch_table(field, args, stream);
+}
+
+hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream) {
   const Variant* var = pick(field, args, g_opt.variant);
   KernelFn fn = var->fn[g_opt.nontemporal ? 1 : 0];
   uint64_t gy = g_opt.stripes_in_flight > 0 ? (uint64_t)g_opt.stripes_in_flight : args.n_stripes;
@@ -1211,6 +1240,7 @@ int set_option(int key, int64_t value) {
     case 2: g_opt.grid_x = value < 0 ? 0 : value; return 0;
     case 3: g_opt.stripes_in_flight = value < 0 ? 0 : value; return 0;
     case 4: g_opt.variant = value; return 0;
+    case 5: g_opt.bitslice = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1221,6 +1251,8 @@ int64_t get_option(int key) {
     case 2: return g_opt.grid_x;
     case 3: return g_opt.stripes_in_flight;
     case 4: return g_opt.variant;
+    case 5: return g_opt.bitslice;
+    case 6: return g_last_path;
     default: return -1;
   }
 }

@@ -57,6 +57,16 @@ hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present,
                               uint64_t shard_bytes, uint32_t n_stripes, CodeArgs* d_descs,
                               hipStream_t stream);
 
+// Table kernels only (launch_code minus the bit-sliced dispatch).
+hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
+
+// Bit-sliced GF(2^16) kernels (rse_bitslice.hip) for codecs whose parity rows
+// are compiled in: sets *handled when it launched (whole 16 KiB chunks of
+// every shard only -- the caller codes the rest).
+hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
+                           hipStream_t stream, bool* handled);
+uint64_t bitslice_chunk_bytes();
+
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
 int set_option(int key, int64_t value);
 int64_t get_option(int key);

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--shard-mib", type=int, default=16)
     ap.add_argument("--op", default="encode", choices=["encode", "reconstruct"])
     ap.add_argument("--variants", type=int, default=1)
+    ap.add_argument("--bitslice", default="1", help="comma list of RSE_OPT_BITSLICE values")
+    ap.add_argument("--shapes", default="", help="gx:gy,gx:gy,... (default: built-in list)")
     args = ap.parse_args()
     lib = R._lib.load()
     k, p, L, S = args.k, args.p, args.shard_mib * MiB, args.stripes
@@ -53,15 +55,19 @@ def main():
 
     nbytes = S * ((k + p) if args.op == "encode" else (k + 2)) * L
     shapes = [(512, 1), (1024, 1), (2048, 1), (4096, 1), (8, 0), (16, 0)]
-    configs = [(nt, gx, gy, var) for var in range(args.variants) for nt in (0, 1)
-               for gx, gy in shapes]
+    if args.shapes:
+        shapes = [tuple(int(x) for x in s.split(":")) for s in args.shapes.split(",")]
+    bss = [int(x) for x in args.bitslice.split(",")]
+    configs = [(nt, gx, gy, var, bs) for bs in bss for var in range(args.variants)
+               for nt in (0, 1) for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for c in configs:
-            nt, gx, gy, var = c
+            nt, gx, gy, var, bs = c
+            lib.rse_set_option(5, bs)
             lib.rse_set_option(1, nt)
             lib.rse_set_option(2, gx)
             lib.rse_set_option(3, gy)
@@ -75,11 +81,11 @@ def main():
         print(f"round {rnd} done", flush=True)
     rows = sorted(((statistics.median(x), min(x), max(x), c) for c, x in res.items()), reverse=True)
     print(f"{args.op} GF(2^{args.field}) {k}+{p} x {args.shard_mib} MiB, {S} stripes; GB/s (1e9)")
-    for med, lo, hi, (nt, gx, gy, var) in rows:
-        print(f"  variant={var} nt={nt} grid_x={gx:<5} stripes_in_flight={gy:<3}  median "
+    for med, lo, hi, (nt, gx, gy, var, bs) in rows:
+        print(f"  bitslice={bs} variant={var} nt={nt} grid_x={gx:<5} stripes_in_flight={gy:<3}  median "
               f"{med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
-    print(json.dumps({"best": {"variant": b[3], "nt": b[0], "grid_x": b[1],
+    print(json.dumps({"best": {"bitslice": b[4], "variant": b[3], "nt": b[0], "grid_x": b[1],
                                "stripes_in_flight": b[2], "GBps": round(rows[0][0], 1)}}))
 
 
