@@ -167,7 +167,8 @@ int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *l
 
 /* ---- launch-shape options (performance only; results never change) ----- */
 #define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */
-#define RSE_OPT_GRID_X 2            /* workgroups per stripe row; 0 = automatic */
+#define RSE_OPT_GRID_X 2            /* table kernels: workgroups per stripe row; bit-sliced
+                                       kernels: total workgroups; 0 = automatic */
 #define RSE_OPT_STRIPES_IN_FLIGHT 3 /* stripes coded concurrently (grid.y); 0 = all */
 #define RSE_OPT_KERNEL_VARIANT 4    /* compiled variant of a tuned shape; -1 = tuned default */
 #define RSE_OPT_BITSLICE 5          /* 1: bit-sliced kernels for compiled codecs (default) */

@@ -80,16 +80,41 @@ constexpr uint16_t cpow16(uint16_t a, uint32_t n) {  // galois_16.rs:80-93
 }
 constexpr uint16_t cinv16(uint16_t a) { return cpow16(a, 65534u); }
 
+constexpr uint8_t cexp8(uint8_t a, uint32_t n) {  // galois_8.rs:87-103
+  if (n == 0) return 1;
+  if (a == 0) return 0;
+  return kGf8.exp[(kGf8.log[a] * n) % 255];
+}
+
+// Field policies for the constexpr matrix code.
+struct CF8 {
+  static constexpr int kPlanes = 8;
+  static constexpr uint16_t mul(uint16_t a, uint16_t b) { return cmul8((uint8_t)a, (uint8_t)b); }
+  static constexpr uint16_t pow(uint16_t a, uint32_t n) { return cexp8((uint8_t)a, n); }
+  static constexpr uint16_t inv(uint16_t a) { return kGf8.exp[255 - kGf8.log[a]]; }
+  // plane q = bit q of the byte
+  static constexpr int bit(int q) { return q; }
+};
+struct CF16 {
+  static constexpr int kPlanes = 16;
+  static constexpr uint16_t mul(uint16_t a, uint16_t b) { return cmul16(a, b); }
+  static constexpr uint16_t pow(uint16_t a, uint32_t n) { return cpow16(a, n); }
+  static constexpr uint16_t inv(uint16_t a) { return cinv16(a); }
+  // plane q < 8: bit q of the H (x-coefficient) byte = uint16 bit q + 8;
+  // plane q >= 8: bit q - 8 of the L byte = uint16 bit q - 8
+  static constexpr int bit(int q) { return q ^ 8; }
+};
+
 // Parity rows of the (K + P) x K encoding matrix V * (V[0..K])^-1 with
 // V[r][c] = r^c (matrix.rs:263-276, core.rs:430-436).  The inverse is unique,
 // so Gauss-Jordan here gives the same matrix as matrix.rs:195-261.
-template <int K, int P>
-struct Gf16Parity {
+template <class F, int K, int P>
+struct Parity {
   uint16_t m[P][K] = {};
-  constexpr Gf16Parity() {
+  constexpr Parity() {
     uint16_t w[K][2 * K] = {};
     for (int r = 0; r < K; ++r) {
-      for (int c = 0; c < K; ++c) w[r][c] = cpow16((uint16_t)r, (uint32_t)c);
+      for (int c = 0; c < K; ++c) w[r][c] = F::pow((uint16_t)r, (uint32_t)c);
       w[r][K + r] = 1;
     }
     for (int col = 0; col < K; ++col) {
@@ -101,47 +126,48 @@ struct Gf16Parity {
           w[col][c] = w[piv][c];
           w[piv][c] = t;
         }
-      const uint16_t s = cinv16(w[col][col]);
-      for (int c = 0; c < 2 * K; ++c) w[col][c] = cmul16(s, w[col][c]);
+      const uint16_t s = F::inv(w[col][col]);
+      for (int c = 0; c < 2 * K; ++c) w[col][c] = F::mul(s, w[col][c]);
       for (int r = 0; r < K; ++r) {
         const uint16_t f = w[r][col];
         if (r == col || f == 0) continue;
-        for (int c = 0; c < 2 * K; ++c) w[r][c] ^= cmul16(f, w[col][c]);
+        for (int c = 0; c < 2 * K; ++c) w[r][c] ^= F::mul(f, w[col][c]);
       }
     }
     for (int o = 0; o < P; ++o)
       for (int i = 0; i < K; ++i) {
         uint16_t v = 0;
-        for (int j = 0; j < K; ++j)
-          v ^= cmul16(cpow16((uint16_t)(K + o), (uint32_t)j), w[j][K + i]);
+        for (int j = 0; j < K; ++j) v ^= F::mul(F::pow((uint16_t)(K + o), (uint32_t)j), w[j][K + i]);
         m[o][i] = v;
       }
   }
 };
 
-// Bit matrices in plane order: plane q < 8 is bit q of the H (x-coefficient)
-// byte = bit q + 8 of the uint16 element, plane q >= 8 bit q - 8 of the L byte
-// = bit q - 8, i.e. uint16 bit (q ^ 8).  sel[o][i][p] = the input planes whose
-// XOR is output plane p of coefficient (o, i).
-template <int K, int P>
-struct Gf16Planes {
-  Gf16Parity<K, P> par{};
-  uint16_t sel[P][K][16] = {};
-  constexpr Gf16Planes() {
+// sel[o][i][p] = the input planes whose XOR is output plane p of the product
+// by coefficient (o, i): column q of the bit matrix is c * (element with only
+// plane q's bit set).
+template <class F, int K, int P>
+struct Planes {
+  Parity<F, K, P> par{};
+  uint16_t sel[P][K][F::kPlanes] = {};
+  constexpr Planes() {
     for (int o = 0; o < P; ++o)
       for (int i = 0; i < K; ++i)
-        for (int q = 0; q < 16; ++q) {
-          const uint16_t col = cmul16(par.m[o][i], (uint16_t)(1u << (q ^ 8)));
-          for (int p = 0; p < 16; ++p)
-            if ((col >> (p ^ 8)) & 1u) sel[o][i][p] |= (uint16_t)(1u << q);
+        for (int q = 0; q < F::kPlanes; ++q) {
+          const uint16_t col = F::mul(par.m[o][i], (uint16_t)(1u << F::bit(q)));
+          for (int p = 0; p < F::kPlanes; ++p)
+            if ((col >> F::bit(p)) & 1u) sel[o][i][p] |= (uint16_t)(1u << q);
         }
   }
 };
 
-template <int K, int P>
-struct Gf16Code {
+// A compiled codec: NP planes per group, NG groups per lane-chunk (16 dwords).
+template <class F, int K, int P>
+struct Code {
+  using Field = F;
   static constexpr int k = K, p = P;
-  static constexpr Gf16Planes<K, P> planes{};
+  static constexpr int NP = F::kPlanes, NG = 16 / F::kPlanes;
+  static constexpr Planes<F, K, P> planes{};
 };
 
 // ------------------------------------------------------------ bit slicing
@@ -151,7 +177,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 // XOR of acc and the planes selected by M, two at a time.
 template <uint32_t M>
-__device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t (&in)[16]) {
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t* in) {
   if constexpr (M == 0) {
     return acc;
   } else {
@@ -166,7 +192,7 @@ __device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t (&in)[16])
   }
 }
 template <uint32_t M>
-__device__ __forceinline__ uint32_t xinit(const uint32_t (&in)[16]) {
+__device__ __forceinline__ uint32_t xinit(const uint32_t* in) {
   if constexpr (M == 0) {
     return 0u;
   } else {
@@ -193,26 +219,42 @@ __device__ __forceinline__ void transpose8(uint32_t* h) {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// 4 vectors (16 dwords, 32 elements) -> 16 planes.
+// 4 vectors (16 dwords) -> NG groups of NP planes.
+//  GF(2^16): 32 elements; split into H/L byte planes (v_perm), then 8x8
+//            transposes: pl[q] = bit q of H, pl[8 + q] = bit q of L.
+//  GF(2^8):  64 bytes as two groups of 8 dwords (vectors 0-1, 2-3), each
+//            8x8-transposed: pl[8g + q] = bit q of group g's 32 bytes.
+template <class F>
 __device__ __forceinline__ void slice(const u32x4 (&v)[4], uint32_t (&pl)[16]) {
+  if constexpr (F::kPlanes == 16) {
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const uint32_t x0 = v[m >> 1][(m & 1) * 2], x1 = v[m >> 1][(m & 1) * 2 + 1];
-    pl[m] = __builtin_amdgcn_perm(x1, x0, 0x06040200u);      // H bytes
-    pl[8 + m] = __builtin_amdgcn_perm(x1, x0, 0x07050301u);  // L bytes
+    for (int m = 0; m < 8; ++m) {
+      const uint32_t x0 = v[m >> 1][(m & 1) * 2], x1 = v[m >> 1][(m & 1) * 2 + 1];
+      pl[m] = __builtin_amdgcn_perm(x1, x0, 0x06040200u);      // H bytes
+      pl[8 + m] = __builtin_amdgcn_perm(x1, x0, 0x07050301u);  // L bytes
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) pl[d] = v[d >> 2][d & 3];
   }
   transpose8(pl);
   transpose8(pl + 8);
 }
 
-// 16 planes -> 4 vectors (inverse of slice; clobbers pl).
+// Inverse of slice (clobbers pl).
+template <class F>
 __device__ __forceinline__ void unslice(uint32_t (&pl)[16], u32x4 (&v)[4]) {
   transpose8(pl);
   transpose8(pl + 8);
+  if constexpr (F::kPlanes == 16) {
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    v[m >> 1][(m & 1) * 2] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x05010400u);
-    v[m >> 1][(m & 1) * 2 + 1] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x07030602u);
+    for (int m = 0; m < 8; ++m) {
+      v[m >> 1][(m & 1) * 2] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x05010400u);
+      v[m >> 1][(m & 1) * 2 + 1] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x07030602u);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) v[d >> 2][d & 3] = pl[d];
   }
 }
 
@@ -235,14 +277,18 @@ __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
   for (int j = 0; j < 4; ++j) v[j] = ldv<NT>(p + j * (kBsBlock * 16));
 }
 
-// acc[o*16 + p] (^)= plane combination of input I for every output o, plane p.
+// acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
+// every output o, group g and plane p.
 template <class C, int I, int... OP>
 __device__ __forceinline__ void mac_input(uint32_t (&acc)[C::p * 16], const uint32_t (&in)[16],
                                           std::integer_sequence<int, OP...>) {
   if constexpr (I == 0)
-    ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % 16]>(in)), ...);
+    ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),
+     ...);
   else
-    ((acc[OP] = xacc<C::planes.sel[OP / 16][I][OP % 16]>(acc[OP], in)), ...);
+    ((acc[OP] = xacc<C::planes.sel[OP / 16][I][OP % C::NP]>(acc[OP],
+                                                              in + (OP % 16) / C::NP * C::NP)),
+     ...);
 }
 
 // Inputs I.. of one chunk: the loads of input I + 1 are issued before input
@@ -253,7 +299,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   u32x4 nxt[4];
   if constexpr (I + 1 < C::k) load4<NT>(nxt, a.in[I + 1] + off);
   uint32_t pl[16];
-  slice(cur, pl);
+  slice<typename C::Field>(cur, pl);
   mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
   // keep each input's XORs together: without this the compiler reassociates
   // across inputs and keeps several inputs' planes live (spills)
@@ -270,8 +316,8 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 // are one flat index space walked grid-stride.  a.n_vec counts whole chunks'
 // vectors only (the host codes the remainder with the table kernels).
 template <class C, bool NT>
-__global__ __launch_bounds__(kBsBlock, 2) void gf16_bitslice_kernel(const CodeArgs a,
-                                                                   uint64_t chunks_per_stripe) {
+__global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
+    const CodeArgs a, uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
   const uint32_t mode = a.mode;
   bool diff = false;
@@ -288,7 +334,7 @@ __global__ __launch_bounds__(kBsBlock, 2) void gf16_bitslice_kernel(const CodeAr
 #pragma unroll
       for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
       u32x4 v[4];
-      unslice(pl, v);
+      unslice<typename C::Field>(pl, v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint64_t o16 = off + j * (kBsBlock * 16);
@@ -305,33 +351,36 @@ __global__ __launch_bounds__(kBsBlock, 2) void gf16_bitslice_kernel(const CodeAr
 
 using BsFn = void (*)(const CodeArgs, uint64_t);
 struct BsShape {
+  int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
   BsFn fn[2];         // [nt]
 };
 
-#define BS16(K, P)                                                            \
-  {K, P, &Gf16Code<K, P>::planes.par.m[0][0],                               \
-   {gf16_bitslice_kernel<Gf16Code<K, P>, false>, gf16_bitslice_kernel<Gf16Code<K, P>, true>}}
-static const BsShape kBs16[] = {
-    BS16(20, 8),  // BASELINE configs[4]: galois_16 20+8
+#define BS(F, FIELD, K, P)                                                   \
+  {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                          \
+   {bitslice_kernel<Code<F, K, P>, false>, bitslice_kernel<Code<F, K, P>, true>}}
+static const BsShape kBsShapes[] = {
+    BS(CF8, 8, 10, 4),    // BASELINE headline: galois_8 10+4
+    BS(CF8, 8, 10, 2),    // benches/bandwidth.rs 10+2
+    BS(CF16, 16, 20, 8),  // BASELINE configs[4]: galois_16 20+8
 };
-#undef BS16
+#undef BS
 
 }  // namespace
 
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                            hipStream_t stream, bool* handled) {
   *handled = false;
-  if (field != 16 || a.accumulate || a.n_vec < kBsChunk / 16) return hipSuccess;
-  for (const BsShape& sh : kBs16) {
-    if (sh.k != a.n_in || sh.p != a.n_out) continue;
+  if (a.accumulate || a.n_vec < kBsChunk / 16) return hipSuccess;
+  for (const BsShape& sh : kBsShapes) {
+    if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
     for (uint32_t o = 0; o < sh.p; ++o)
       for (uint32_t i = 0; i < sh.k; ++i)
         if (a.coef[o][i] != sh.m[o * sh.k + i]) return hipSuccess;
     const uint64_t cps = a.n_vec / (kBsChunk / 16);
     const uint64_t total = cps * a.n_stripes;
-    uint64_t gx = grid > 0 ? (uint64_t)grid : 1024u;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;  // tools/tune.py sweeps
     if (gx > total) gx = total;
     if (gx > 0x7fffffffu) gx = 0x7fffffffu;
     hipLaunchKernelGGL(sh.fn[nt ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
