@@ -130,7 +130,47 @@ def cpu_baseline(k, p, shard_bytes, seconds):
                       f"({dt:.1f} s, 1 thread, reference simd_c kernel -O3 -march=haswell)"}
 
 
-def load_traffic(workload):
+def cpu_baseline_parallel(k, p, shard_bytes, seconds, threads):
+    """Stripe-parallel CPU leg: `threads` host threads, each
+    encoding its own stripe with the reference kernel (ctypes drops the GIL
+    for the foreign call), for ~`seconds`.  Reported beside cpu_baseline."""
+    import threading
+
+    import numpy as np
+    from oracle import oracle as O
+    if not O.ref_available():
+        return None
+    ref = O.ref()
+    rows = np.ascontiguousarray(O.Codec(8, k, p).matrix()[k:])
+    stripes = [([O.splitmix_bytes(SEED + t, i, shard_bytes) for i in range(k)],
+                [np.zeros(shard_bytes, np.uint8) for _ in range(p)]) for t in range(threads)]
+    counts = [0] * threads
+    stop = threading.Event()
+
+    def work(t):
+        data, par = stripes[t]
+        dp, pp = O._ptrs(data), O._ptrs(par)
+        while not stop.is_set():
+            ref.ref_gf8_code_some_slices(rows.ctypes.data_as(O._u8p), p, k, dp, pp, shard_bytes)
+            counts[t] += 1
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    time.sleep(seconds)
+    stop.set()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    n = sum(counts)
+    return {"value": round(n * (k + p) * shard_bytes / dt / MiB, 1), "unit": "MB/s",
+            "cores": threads, "kind": "reference",
+            "sample": f"{n} encodes of {threads} independent {k}+{p} x {shard_bytes // MiB} MiB "
+                      f"stripes ({dt:.1f} s, {threads} threads, reference simd_c kernel)"}
+
+
+def load_traffic(workload, kernel):
     """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary for
     this workload (profiles/*pmc_traffic*.json, written by
     tools/pmc_traffic.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
@@ -140,7 +180,7 @@ def load_traffic(workload):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel_family", "table") == kernel:
             best = d
     return best
 
@@ -187,6 +227,8 @@ def main(argv=None):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # which kernel family coded the launches (RSE_OPT_LAST_PATH)
+    kernel = "bitslice" if R._lib.load().rse_get_option(6) == 1 else "table"
     # correctness gate: global stripe 0's parity equals the reference's digest
     check = None
     if rank == 0 and (k, p, L) == (10, 4, 16 * MiB):
@@ -227,15 +269,17 @@ def main(argv=None):
         mean_ms = sum(kern_ms) / len(kern_ms) / launches
         achieved = per_launch_bytes / (mean_ms * 1e-3) / 1e9
         workload = f"gf8 {k}+{p} x {args.shard_mib} MiB encode, {pool} stripes/launch"
-        tr = load_traffic(workload)
+        tr = load_traffic(workload, kernel)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
-                "kernel_ms_per_launch": round(mean_ms, 4),
+                "kernel": kernel, "kernel_ms_per_launch": round(mean_ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch_bytes)}
-        cpu = None
+        cpu = cpu_par = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(k, p, L, args.cpu_seconds)
+            cpu_par = cpu_baseline_parallel(k, p, L, args.cpu_seconds,
+                                            min(16, len(os.sched_getaffinity(0))))
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -249,6 +293,8 @@ def main(argv=None):
                        "parity_check_vs_reference": check},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if cpu_par:
+            line["cpu_baseline_all_cores"] = cpu_par
         line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def run(counter, outdir, bench_args):
-    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "gf8_code|gf8_pipe",
+    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "gf8_code|gf8_pipe|bitslice_kernel",
            "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-extras"] + bench_args
     out = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
@@ -52,6 +52,7 @@ def main():
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
     res = {
         "workload": bench["config"]["workload"],
+        "kernel_family": bench["roofline"].get("kernel", "table"),
         "kernel": [r["Kernel_Name"] for r in fetch][0],
         "dispatches": len(f),
         "fetch_size_kb_raw_mean": sum(f) / len(f),
