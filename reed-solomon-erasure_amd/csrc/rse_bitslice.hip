@@ -29,7 +29,7 @@
 // use the same one; this one keeps every global access coalesced.
 #include <utility>
 
-#include "rse_kernels.hpp"
+#include "rse_device.hpp"
 
 namespace rse {
 namespace {
@@ -171,10 +171,6 @@ struct Code {
 };
 
 // ------------------------------------------------------------ bit slicing
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
 // XOR of acc and the planes selected by M, two at a time.
 template <uint32_t M>
 __device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t* in) {
@@ -216,8 +212,6 @@ __device__ __forceinline__ void transpose8(uint32_t* h) {
     }
   }
 }
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // 4 vectors (16 dwords) -> NG groups of NP planes.
 //  GF(2^16): 32 elements; split into H/L byte planes (v_perm), then 8x8
