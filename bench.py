@@ -224,11 +224,12 @@ def main(argv=None):
             r.encode_flat(buf, L, cnt)
             done += cnt
 
+    lib = R._lib.load()
+    n_bs = lib.rse_get_option(6)  # RSE_OPT_BITSLICE_LAUNCHES
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # which kernel family coded the launches (RSE_OPT_LAST_PATH)
-    kernel = "bitslice" if R._lib.load().rse_get_option(6) == 1 else "table"
+    kernel = "bitslice" if lib.rse_get_option(6) > n_bs else "table"
     # correctness gate: global stripe 0's parity equals the reference's digest
     check = None
     if rank == 0 and (k, p, L) == (10, 4, 16 * MiB):

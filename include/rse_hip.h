@@ -172,8 +172,8 @@ int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *l
 #define RSE_OPT_STRIPES_IN_FLIGHT 3 /* stripes coded concurrently (grid.y); 0 = all */
 #define RSE_OPT_KERNEL_VARIANT 4    /* compiled variant of a tuned shape; -1 = tuned default */
 #define RSE_OPT_BITSLICE 5          /* 1: bit-sliced kernels for compiled codecs (default) */
-#define RSE_OPT_LAST_PATH 6         /* read-only, per thread: 1 if the last coding launch was
-                                       bit-sliced, 0 if it used the table kernels */
+#define RSE_OPT_BITSLICE_LAUNCHES 6 /* read-only, per thread: number of bit-sliced kernel
+                                       launches so far (diagnostics / tests) */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

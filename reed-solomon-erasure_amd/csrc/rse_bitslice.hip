@@ -343,17 +343,166 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }
 
+// ------------------------------------------------------------ reconstruct
+// Bit-sliced syndrome reconstruct (BsReconArgs in rse_kernels.hpp).  The input
+// sequence is the present data shards, then the syndrome parity shards; the
+// next present input's loads are issued before the current one is coded.
+
+// Input index J < k is data shard J, J >= k parity shard J - k.
+__device__ __forceinline__ const uint8_t* recon_ptr(const BsReconArgs& a, uint32_t k, uint32_t j) {
+  return j < k ? a.data[j] : a.par[j - k];
+}
+// Mask of all inputs read: data present bits, then syndrome rows shifted by k.
+__device__ __forceinline__ uint64_t recon_mask(const BsReconArgs& a, uint32_t k) {
+  return (uint64_t)a.present | ((uint64_t)a.synd << k);
+}
+
+template <class C, bool NT, int I>
+__device__ __forceinline__ void recon_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
+                                             const BsReconArgs& a, uint64_t mask, uint64_t off) {
+  if constexpr (I < C::k + C::p) {
+    if ((mask >> I) & 1u) {
+      const uint64_t rest = mask >> (I + 1);
+      u32x4 nxt[4];
+      if (rest) load4<NT>(nxt, recon_ptr(a, C::k, I + 1 + __builtin_ctzll(rest)) + off);
+      uint32_t pl[16];
+      slice<typename C::Field>(cur, pl);
+      if constexpr (I < C::k) {
+        // every sigma row, needed or not: straight-line XOR networks (a
+        // branch per row costs more in register pressure than the XORs)
+        mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
+      } else {  // syndrome: s_r = sigma_r ^ parity_r (slicing is linear)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[(I - C::k) * 16 + q] ^= pl[q];
+      }
+#pragma unroll
+      for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      if (rest) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+    recon_inputs<C, NT, I + 1>(acc, cur, a, mask, off);
+  }
+}
+
+// v (4 vectors of elements) times a table-coded constant, XORed into o.
+template <class F>
+__device__ __forceinline__ void mac_vectors(u32x4 (&o)[4], const uint32_t* v, const uint4* tq,
+                                            const uint32_t* tt2, int idx) {
+  if constexpr (F::kPlanes == 8) {
+    const Gf8Tab t = read_tab(tq, tt2, idx);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) o[d >> 2][d & 3] ^= gf8_mul4(t, make_sel(v[d]));
+  } else {
+    const Gf8Tab hh = read_tab(tq, tt2, idx * 4 + 0), lh = read_tab(tq, tt2, idx * 4 + 1);
+    const Gf8Tab hl = read_tab(tq, tt2, idx * 4 + 2), ll = read_tab(tq, tt2, idx * 4 + 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t h0, l0, h1, l1;
+      split_planes(make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]), h0, l0, h1, l1);
+      const Sel sh0 = make_sel(h0), sl0 = make_sel(l0), sh1 = make_sel(h1), sl1 = make_sel(l1);
+      const uint4 m = merge_planes(xor3(gf8_mul4(hh, sh0), gf8_mul4(lh, sl0), 0u),
+                                   xor3(gf8_mul4(hl, sh0), gf8_mul4(ll, sl0), 0u),
+                                   xor3(gf8_mul4(hh, sh1), gf8_mul4(lh, sl1), 0u),
+                                   xor3(gf8_mul4(hl, sh1), gf8_mul4(ll, sl1), 0u));
+      o[j] ^= (u32x4){m.x, m.y, m.z, m.w};
+    }
+  }
+}
+
+template <class C, bool NT>
+__global__ __launch_bounds__(kBsBlock, 2) void bitslice_recon_kernel(const BsReconArgs a,
+                                                                     uint64_t chunks_per_stripe) {
+  using F = typename C::Field;
+  constexpr int TPC = F::kPlanes == 16 ? 4 : 1;  // GF(2^8) tables per coefficient
+  __shared__ uint4 tq[kMaxOut * C::p * TPC];
+  __shared__ uint32_t tt2[kMaxOut * C::p * TPC];
+  const uint32_t n_out = a.n_out;
+  for (uint32_t t = threadIdx.x; t < n_out * C::p; t += kBsBlock) {
+    const uint32_t c = a.w[t / C::p][t % C::p];
+    if constexpr (TPC == 1) {
+      write_tab(tq, tt2, t, make_gf8_tab(c));
+    } else {
+      uint32_t sub[4];
+      gf16_sub_coefs(c, sub);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) write_tab(tq, tt2, t * 4 + q, make_gf8_tab(sub[q]));
+    }
+  }
+  __syncthreads();
+  const uint64_t mask = recon_mask(a, C::k);
+  const int first = __builtin_ctzll(mask);  // host guarantees mask != 0
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+    uint32_t acc[C::p * 16];
+#pragma unroll
+    for (int q = 0; q < C::p * 16; ++q) acc[q] = 0u;
+    u32x4 cur[4];
+    load4<NT>(cur, recon_ptr(a, C::k, first) + off);
+    recon_inputs<C, NT, 0>(acc, cur, a, mask, off);
+    // back to element order, in place
+#pragma unroll
+    for (int r = 0; r < C::p; ++r) {
+      if (!((a.sigma >> r) & 1u)) continue;
+      uint32_t pl[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pl[q] = acc[r * 16 + q];
+      u32x4 v[4];
+      unslice<F>(pl, v);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[r * 16 + q] = v[q >> 2][q & 3];
+    }
+#pragma unroll 1
+    for (uint32_t o = 0; o < n_out; ++o) {
+      // opaque per output: otherwise LICM hoists every row's byte-plane split
+      // and selectors out of this loop (hundreds of VGPRs -> scratch)
+#pragma unroll
+      for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      u32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (u32x4){0u, 0u, 0u, 0u};
+      const int os = a.out_sigma[o];
+#pragma unroll
+      for (int r = 0; r < C::p; ++r) {
+        if (os == r) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] ^= acc[r * 16 + q];
+        }
+        // one row's tables at a time: the opaque offset (ordered after the
+        // previous row's pins) keeps hipcc from loading every row's tables
+        // up front, which spills
+        const uint32_t lb = opaque_zero();
+        if (((a.synd >> r) & 1u) && a.w[o][r] != 0)
+          mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * C::p + r));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(v[j][w]));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stv<NT>(a.out[o] + off + j * (kBsBlock * 16), v[j]);
+    }
+  }
+}
+
+using BsRecFn = void (*)(const BsReconArgs, uint64_t);
+
 using BsFn = void (*)(const CodeArgs, uint64_t);
 struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
   BsFn fn[2];         // [nt]
+  BsRecFn rec[2];     // [nt]
 };
 
-#define BS(F, FIELD, K, P)                                                   \
-  {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                          \
-   {bitslice_kernel<Code<F, K, P>, false>, bitslice_kernel<Code<F, K, P>, true>}}
+#define BS(F, FIELD, K, P)                                                      \
+  {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                             \
+   {bitslice_kernel<Code<F, K, P>, false>, bitslice_kernel<Code<F, K, P>, true>}, \
+   {bitslice_recon_kernel<Code<F, K, P>, false>, bitslice_recon_kernel<Code<F, K, P>, true>}}
 static const BsShape kBsShapes[] = {
     BS(CF8, 8, 10, 4),    // BASELINE headline: galois_8 10+4
     BS(CF8, 8, 10, 2),    // benches/bandwidth.rs 10+2
@@ -380,6 +529,34 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     hipLaunchKernelGGL(sh.fn[nt ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    *handled = true;
+    return hipSuccess;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
+                                 const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
+                                 bool* handled) {
+  *handled = false;
+  if (!get_option(5) || n_vec < kBsChunk / 16 || a.n_out == 0 || a.n_out > (uint32_t)kMaxOut ||
+      (a.present == 0 && a.synd == 0))
+    return hipSuccess;
+  for (const BsShape& sh : kBsShapes) {
+    if (sh.field != field || sh.k != k || sh.p != p) continue;
+    for (uint32_t i = 0; i < k * p; ++i)
+      if (parity_rows[i] != sh.m[i]) return hipSuccess;
+    const uint64_t cps = n_vec / (kBsChunk / 16);
+    const uint64_t total = cps * a.n_stripes;
+    const int64_t grid = get_option(2);
+    uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;
+    if (gx > total) gx = total;
+    if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+    hipLaunchKernelGGL(sh.rec[get_option(1) ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
+                       a, cps);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    count_bitslice_launch();
     *handled = true;
     return hipSuccess;
   }

@@ -70,6 +70,9 @@ struct rse_codec {
   uint16_t mul(uint16_t a, uint16_t b) const {
     return field == 16 ? rse::Gf16Field::mul(a, b) : rse::Gf8Field::mul(a, b);
   }
+  uint16_t inv(uint16_t a) const {
+    return field == 16 ? rse::Gf16Field::inv(a) : rse::Gf8Field::inv(a);
+  }
 };
 
 namespace {
@@ -398,15 +401,143 @@ int plan_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens
   return RSE_OK;
 }
 
+// Bit-sliced syndrome reconstruct (rse_kernels.hpp BsReconArgs) for codecs
+// whose parity rows are compiled into rse_bitslice.hip, over the whole 16 KiB
+// chunks of every shard; *done = bytes per shard it coded (0 if it does not
+// apply).  Same outputs as the composed-row plan: missing data, and missing
+// parity unless data_only.  The e present parity rows used for syndromes are
+// the first e present ones -- exactly the parity rows among the reference's
+// `valid` set (core.rs:801-841) -- and P[R][S] is invertible for any choice
+// (any k rows of the systematic MDS matrix are independent), so the result
+// is the reference's.  Shards are already validated by plan_reconstruct.
+int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const uint8_t* present,
+                         bool data_only, size_t len_bytes, uint64_t stripe_stride,
+                         size_t n_stripes, hipStream_t s, size_t* done) {
+  *done = 0;
+  const size_t k = c->k, p = c->p;
+  const uint64_t cb = rse::bitslice_chunk_bytes();
+  if (k > (size_t)kMaxIn || p > (size_t)kMaxOut || len_bytes < cb || stripe_stride % 16u ||
+      !rse::get_option(RSE_OPT_BITSLICE))
+    return RSE_OK;
+  rse::BsReconArgs a;
+  std::memset(&a, 0, sizeof a);
+  std::vector<size_t> S, R, M;
+  for (size_t d = 0; d < k; ++d) {
+    if (present[d]) {
+      a.present |= 1u << d;
+      a.data[d] = shards[d];
+    } else {
+      S.push_back(d);
+    }
+  }
+  for (size_t r = 0; r < p; ++r) {
+    if (present[k + r]) {
+      if (R.size() < S.size()) R.push_back(r);
+    } else if (!data_only) {
+      M.push_back(r);
+    }
+  }
+  const size_t e = S.size();
+  if (e + M.size() == 0 || R.size() != e) return RSE_OK;
+  for (size_t d = 0; d < k; ++d)
+    if (present[d] && !aligned16(shards[d])) return RSE_OK;
+  for (size_t r : R)
+    if (!aligned16(shards[k + r])) return RSE_OK;
+  for (size_t j : S)
+    if (!aligned16(shards[j])) return RSE_OK;
+  for (size_t r : M)
+    if (!aligned16(shards[k + r])) return RSE_OK;
+  // A = P[R][S] and its inverse (Gauss-Jordan; A is invertible, see above)
+  std::vector<uint16_t> w(e * 2 * e, 0);
+  for (size_t t = 0; t < e; ++t) {
+    for (size_t u = 0; u < e; ++u) w[t * 2 * e + u] = c->mat(k + R[t], S[u]);
+    w[t * 2 * e + e + t] = 1;
+  }
+  for (size_t col = 0; col < e; ++col) {
+    size_t piv = col;
+    while (piv < e && w[piv * 2 * e + col] == 0) ++piv;
+    if (piv == e) return RSE_OK;  // cannot happen for this code; stay on the table path
+    for (size_t x = 0; x < 2 * e; ++x) std::swap(w[col * 2 * e + x], w[piv * 2 * e + x]);
+    const uint16_t sc = c->inv(w[col * 2 * e + col]);
+    for (size_t x = 0; x < 2 * e; ++x) w[col * 2 * e + x] = c->mul(sc, w[col * 2 * e + x]);
+    for (size_t r = 0; r < e; ++r) {
+      const uint16_t f = w[r * 2 * e + col];
+      if (r == col || !f) continue;
+      for (size_t x = 0; x < 2 * e; ++x) w[r * 2 * e + x] ^= c->mul(f, w[col * 2 * e + x]);
+    }
+  }
+  auto ainv = [&](size_t u, size_t t) { return w[u * 2 * e + e + t]; };
+  uint32_t o = 0;
+  for (size_t u = 0; u < e; ++u, ++o) {  // missing data S[u] = sum_t Ainv[u][t] s_t
+    a.out[o] = const_cast<uint8_t*>(shards[S[u]]);
+    a.out_sigma[o] = -1;
+    for (size_t t = 0; t < e; ++t) a.w[o][R[t]] = ainv(u, t);
+  }
+  for (size_t r : M) {  // missing parity r = sigma_r ^ sum_t (P[r][S] Ainv)[t] s_t
+    a.out[o] = const_cast<uint8_t*>(shards[k + r]);
+    a.out_sigma[o] = (int32_t)r;
+    for (size_t t = 0; t < e; ++t) {
+      uint16_t v = 0;
+      for (size_t u = 0; u < e; ++u) v ^= c->mul(c->mat(k + r, S[u]), ainv(u, t));
+      a.w[o][R[t]] = v;
+    }
+    ++o;
+  }
+  a.n_out = o;
+  for (size_t t = 0; t < e; ++t) {
+    a.synd |= 1u << R[t];
+    a.sigma |= 1u << R[t];
+    a.par[R[t]] = shards[k + R[t]];
+  }
+  for (size_t r : M) a.sigma |= 1u << r;
+  a.stripe_stride = stripe_stride;
+  std::vector<uint16_t> rows(p * k);
+  for (size_t r = 0; r < p; ++r)
+    for (size_t j = 0; j < k; ++j) rows[r * k + j] = c->mat(k + r, j);
+  bool handled = false;
+  for (size_t s0 = 0; s0 < n_stripes; s0 += 0x7fffffffu) {
+    rse::BsReconArgs b = a;
+    const size_t cnt = std::min<size_t>(n_stripes - s0, 0x7fffffffu);
+    const uint64_t adv = (uint64_t)s0 * stripe_stride;
+    b.n_stripes = (uint32_t)cnt;
+    for (size_t d = 0; d < k; ++d)
+      if (b.data[d]) b.data[d] += adv;
+    for (size_t r = 0; r < p; ++r)
+      if (b.par[r]) b.par[r] += adv;
+    for (uint32_t q = 0; q < b.n_out; ++q) b.out[q] += adv;
+    RSE_HIP(rse::launch_bitslice_recon(c->field, (uint32_t)k, (uint32_t)p, rows.data(), b,
+                                       len_bytes / 16u, s, &handled));
+    if (!handled) return RSE_OK;  // first batch decides; nothing launched
+  }
+  *done = (len_bytes / cb) * cb;
+  return RSE_OK;
+}
+
+// Codes plan.rows over [off, len) of every shard (the table kernels).
+int run_plan_tail(const rse_codec* c, const ReconPlan& plan, size_t off, uint64_t stripe_stride,
+                  size_t n_stripes, hipStream_t s) {
+  const size_t len = plan.len * c->esize();
+  if (off >= len) return RSE_OK;
+  std::vector<const uint8_t*> in(plan.in);
+  std::vector<uint8_t*> out(plan.out);
+  for (auto& q : in) q += off;
+  for (auto& q : out) q += off;
+  Job j{c->field, &plan.rows, in.data(), out.data(), nullptr, len - off, rse::kStore, false,
+        nullptr, stripe_stride, n_stripes};
+  return run_job(j, s);
+}
+
 int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens,
                      const uint8_t* present, size_t n, bool data_only, hipStream_t s) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   ReconPlan plan;
   int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
-  Job j{c->field, &plan.rows, plan.in.data(), plan.out.data(), nullptr, plan.len * c->esize(),
-        rse::kStore, false, nullptr, 0, 1};
-  return run_job(j, s);
+  size_t done = 0;
+  rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(shards), present, data_only,
+                            plan.len * c->esize(), 0, 1, s, &done);
+  if (rc) return rc;
+  return run_plan_tail(c, plan, done, 0, 1, s);
 }
 
 int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* data_lens,
@@ -649,9 +780,11 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
   ReconPlan plan;
   int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, true, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
-  Job j{c->field, &plan.rows, plan.in.data(), plan.out.data(), nullptr, sb, rse::kStore, false,
-        nullptr, (uint64_t)c->total * sb, n_stripes};
-  return run_job(j, (hipStream_t)stream);
+  size_t done = 0;
+  rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(ptrs.data()), present, true,
+                            sb, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream, &done);
+  if (rc) return rc;
+  return run_plan_tail(c, plan, done, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream);
 }
 
 // Many stripes, each with its own erasure pattern, in two launches: the plan

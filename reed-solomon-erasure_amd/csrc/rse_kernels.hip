@@ -751,7 +751,7 @@ struct Options {
   int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
   int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
 };
-thread_local int64_t g_last_path = 0;  // 1 if the last launch_code used a bit-sliced kernel
+thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
 
 // ---------------------------------------------------------------------------
@@ -993,14 +993,13 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
   if (args.n_in == 0 || args.n_in > (uint32_t)kMaxIn || args.n_out == 0 ||
       args.n_out > (uint32_t)kMaxOut || args.n_stripes == 0)
     return hipErrorInvalidValue;
-  g_last_path = 0;
   if (g_opt.bitslice) {
     bool handled = false;
     hipError_t e = launch_bitslice(field, args, g_opt.nontemporal != 0, g_opt.grid_x, stream,
                                    &handled);
     if (e != hipSuccess) return e;
     if (handled) {
-      g_last_path = 1;
+      ++g_bs_launches;
       // the bit-sliced kernel codes whole chunks; the rest goes to the table kernels
       const uint64_t cb = bitslice_chunk_bytes();
       const uint64_t done = (args.n_vec * 16u / cb) * cb;
@@ -1080,6 +1079,8 @@ int set_option(int key, int64_t value) {
   }
 }
 
+void count_bitslice_launch() { ++g_bs_launches; }
+
 int64_t get_option(int key) {
   switch (key) {
     case 1: return g_opt.nontemporal;
@@ -1087,7 +1088,7 @@ int64_t get_option(int key) {
     case 3: return g_opt.stripes_in_flight;
     case 4: return g_opt.variant;
     case 5: return g_opt.bitslice;
-    case 6: return g_last_path;
+    case 6: return g_bs_launches;
     default: return -1;
   }
 }

@@ -60,16 +60,44 @@ hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present,
 // Table kernels only (launch_code minus the bit-sliced dispatch).
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
 
-// Bit-sliced GF(2^16) kernels (rse_bitslice.hip) for codecs whose parity rows
-// are compiled in: sets *handled when it launched (whole 16 KiB chunks of
-// every shard only -- the caller codes the rest).
+// Bit-sliced kernels (rse_bitslice.hip) for codecs whose parity rows are
+// compiled in: sets *handled when it launched (whole 16 KiB chunks of every
+// shard only -- the caller codes the rest).
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                            hipStream_t stream, bool* handled);
 uint64_t bitslice_chunk_bytes();
 
+// Bit-sliced syndrome reconstruct for compiled codecs (rse_bitslice.hip).
+// With P the compiled parity rows, S the e missing data shards and R e
+// present parity rows:  sigma_r = sum over present data d of P[r][d] * shard_d
+// (compile-time XOR networks), syndrome s_r = sigma_r ^ parity_r for r in R,
+// and every output o = (out_sigma[o] >= 0 ? sigma_{out_sigma[o]} : 0)
+//                      ^ sum over r in R of w[o][r] * s_r
+// (missing data: w = rows of (P[R][S])^-1; missing parity r: out_sigma = r,
+// w = P[r][S] (P[R][S])^-1).  One pass over k surviving shards.
+struct BsReconArgs {
+  const uint8_t* data[kMaxIn];    // data shard d (read when present)
+  const uint8_t* par[kMaxOut];    // parity shard r (read when a syndrome row)
+  uint8_t* out[kMaxOut];          // output o
+  uint64_t stripe_stride;
+  uint32_t n_stripes;
+  uint32_t present;               // bit d: data shard d present
+  uint32_t sigma;                 // bit r: sigma_r is needed
+  uint32_t synd;                  // bit r: parity row r is a syndrome row (R)
+  uint32_t n_out;
+  int32_t out_sigma[kMaxOut];     // sigma row XORed into output o, -1 for none
+  uint16_t w[kMaxOut][kMaxOut];   // [o][r], zero unless r is in R
+};
+// parity_rows: the codec's p x k parity rows (row-major); must equal the
+// compiled ones for *handled to be set.  n_vec: 16-byte vectors per shard.
+hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
+                                 const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
+                                 bool* handled);
+
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
 int set_option(int key, int64_t value);
 int64_t get_option(int key);
+void count_bitslice_launch();  // RSE_OPT_BITSLICE_LAUNCHES
 
 // Fill nbytes of device memory with the splitmix64 byte stream of
 // (seed, shard_id) -- identical to oracle/oracle.py: splitmix_bytes.

@@ -499,9 +499,10 @@ def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra
             assert lib.rse_set_option(5, bs) == 0
             t = [dev(x).reshape(shape) for x in full[:k]] + \
                 [torch.zeros(shape, dtype=torch.uint8, device="cuda") for _ in range(p)]
+            n0 = lib.rse_get_option(6)
             r.encode(t)
             torch.cuda.synchronize()
-            assert lib.rse_get_option(6) == bs
+            assert lib.rse_get_option(6) - n0 == bs
             outs[bs] = [host(x).reshape(-1) for x in t[k:]]
             assert r.verify(t)
             flat = t[k + p - 1].view(-1)
@@ -520,15 +521,72 @@ def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra
             buf[(s * (k + p) + k) * nbytes:(s + 1) * (k + p) * nbytes] = 0
         d = dev(buf)
         assert lib.rse_set_option(5, 1) == 0
+        n0 = lib.rse_get_option(6)
         r.encode_flat(d, n_elems, stripes)
         # a stripe stride that is not a multiple of 16 B cannot be vectorised
-        assert lib.rse_get_option(6) == (1 if nbytes % 16 == 0 else 0)
+        assert lib.rse_get_option(6) - n0 == (1 if nbytes % 16 == 0 else 0)
         got = host(d).reshape(stripes, k + p, nbytes)
         for s in range(stripes):
             for i in range(k + p):
                 assert (got[s, i] == full[i]).all(), (s, i)
     finally:
         lib.rse_set_option(5, 1)
+
+
+@pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
+def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
+    """Syndrome reconstruct on the bit-sliced kernels (compiled parity rows,
+    runtime erasure pattern) against the oracle: every number of erased
+    shards 1..p, data and/or parity, reconstruct and reconstruct_data, a
+    length with whole chunks plus a table-coded tail; then the flat
+    many-stripe reconstruct_data."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 2 * 16384 + 48 * es
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(k * 100 + p + field)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    patterns = []
+    for ne in range(1, p + 1):
+        patterns.append(sorted(rng.choice(k + p, ne, replace=False).tolist()))
+    patterns += [list(range(min(p, k))), list(range(k, k + p)), [0, k + p - 1]]
+    for trial, erased in enumerate(patterns):
+        present = [i not in erased for i in range(k + p)]
+        for data_only in (False, True):
+            tb = [dev(x).reshape(shape) for x in full]
+            for e in erased:
+                tb[e].fill_(0x33)
+            n0 = lib.rse_get_option(6)
+            (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+            torch.cuda.synchronize()
+            only_parity_missing = all(e >= k for e in erased)
+            if not (data_only and only_parity_missing):
+                assert lib.rse_get_option(6) - n0 == 1, (erased, data_only)
+            for i in range(k + p):
+                got = host(tb[i]).reshape(-1)
+                if data_only and i >= k and i in erased:
+                    assert (got == 0x33).all()
+                else:
+                    assert (got == full[i]).all(), (erased, data_only, i)
+    # flat, several stripes, one pattern
+    stripes, erased = 3, [1, 4] if p >= 2 else [1]
+    buf = np.concatenate([np.concatenate(full)] * stripes)
+    d = dev(buf)
+    v = d.view(stripes, k + p, nbytes)
+    for e in erased:
+        v[:, e].fill_(0)
+    n0 = lib.rse_get_option(6)
+    r.reconstruct_data_flat(d, n_elems, stripes, [i not in erased for i in range(k + p)])
+    torch.cuda.synchronize()
+    assert lib.rse_get_option(6) - n0 == 1
+    got = host(d).reshape(stripes, k + p, nbytes)
+    for s_ in range(stripes):
+        for i in range(k):
+            assert (got[s_, i] == full[i]).all(), (s_, i)
 
 
 def test_encode_host_matches_device(R):
