@@ -273,8 +273,8 @@ __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 
 // acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
 // every output o, group g and plane p.
-template <class C, int I, int... OP>
-__device__ __forceinline__ void mac_input(uint32_t (&acc)[C::p * 16], const uint32_t (&in)[16],
+template <class C, int I, int N, int... OP>
+__device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&in)[16],
                                           std::integer_sequence<int, OP...>) {
   if constexpr (I == 0)
     ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),
@@ -357,10 +357,12 @@ __device__ __forceinline__ uint64_t recon_mask(const BsReconArgs& a, uint32_t k)
   return (uint64_t)a.present | ((uint64_t)a.synd << k);
 }
 
-template <class C, bool NT, int I>
-__device__ __forceinline__ void recon_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
+// NS: sigma rows computed (rows 0..NS-1; the host picks NS above every row it
+// needs), so a reconstruct pays for the rows it uses, not all p.
+template <class C, bool NT, int NS, int I>
+__device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&cur)[4],
                                              const BsReconArgs& a, uint64_t mask, uint64_t off) {
-  if constexpr (I < C::k + C::p) {
+  if constexpr (I < C::k + NS) {
     if ((mask >> I) & 1u) {
       const uint64_t rest = mask >> (I + 1);
       u32x4 nxt[4];
@@ -370,19 +372,19 @@ __device__ __forceinline__ void recon_inputs(uint32_t (&acc)[C::p * 16], u32x4 (
       if constexpr (I < C::k) {
         // every sigma row, needed or not: straight-line XOR networks (a
         // branch per row costs more in register pressure than the XORs)
-        mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
+        mac_input<C, I>(acc, pl, std::make_integer_sequence<int, NS * 16>{});
       } else {  // syndrome: s_r = sigma_r ^ parity_r (slicing is linear)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[(I - C::k) * 16 + q] ^= pl[q];
       }
 #pragma unroll
-      for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
       if (rest) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
       }
     }
-    recon_inputs<C, NT, I + 1>(acc, cur, a, mask, off);
+    recon_inputs<C, NT, NS, I + 1>(acc, cur, a, mask, off);
   }
 }
 
@@ -411,16 +413,16 @@ __device__ __forceinline__ void mac_vectors(u32x4 (&o)[4], const uint32_t* v, co
   }
 }
 
-template <class C, bool NT>
-__global__ __launch_bounds__(kBsBlock, 2) void bitslice_recon_kernel(const BsReconArgs a,
-                                                                     uint64_t chunks_per_stripe) {
+template <class C, bool NT, int NS>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_kernel(
+    const BsReconArgs a, uint64_t chunks_per_stripe) {
   using F = typename C::Field;
   constexpr int TPC = F::kPlanes == 16 ? 4 : 1;  // GF(2^8) tables per coefficient
-  __shared__ uint4 tq[kMaxOut * C::p * TPC];
-  __shared__ uint32_t tt2[kMaxOut * C::p * TPC];
+  __shared__ uint4 tq[kMaxOut * NS * TPC];
+  __shared__ uint32_t tt2[kMaxOut * NS * TPC];
   const uint32_t n_out = a.n_out;
-  for (uint32_t t = threadIdx.x; t < n_out * C::p; t += kBsBlock) {
-    const uint32_t c = a.w[t / C::p][t % C::p];
+  for (uint32_t t = threadIdx.x; t < n_out * NS; t += kBsBlock) {
+    const uint32_t c = a.w[t / NS][t % NS];
     if constexpr (TPC == 1) {
       write_tab(tq, tt2, t, make_gf8_tab(c));
     } else {
@@ -437,15 +439,15 @@ __global__ __launch_bounds__(kBsBlock, 2) void bitslice_recon_kernel(const BsRec
   for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
     const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
-    uint32_t acc[C::p * 16];
+    uint32_t acc[NS * 16];
 #pragma unroll
-    for (int q = 0; q < C::p * 16; ++q) acc[q] = 0u;
+    for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
     u32x4 cur[4];
     load4<NT>(cur, recon_ptr(a, C::k, first) + off);
-    recon_inputs<C, NT, 0>(acc, cur, a, mask, off);
+    recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
     // back to element order, in place
 #pragma unroll
-    for (int r = 0; r < C::p; ++r) {
+    for (int r = 0; r < NS; ++r) {
       if (!((a.sigma >> r) & 1u)) continue;
       uint32_t pl[16];
 #pragma unroll
@@ -460,13 +462,13 @@ __global__ __launch_bounds__(kBsBlock, 2) void bitslice_recon_kernel(const BsRec
       // opaque per output: otherwise LICM hoists every row's byte-plane split
       // and selectors out of this loop (hundreds of VGPRs -> scratch)
 #pragma unroll
-      for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
       u32x4 v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (u32x4){0u, 0u, 0u, 0u};
       const int os = a.out_sigma[o];
 #pragma unroll
-      for (int r = 0; r < C::p; ++r) {
+      for (int r = 0; r < NS; ++r) {
         if (os == r) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] ^= acc[r * 16 + q];
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(kBsBlock, 2) void bitslice_recon_kernel(const BsRec
         // up front, which spills
         const uint32_t lb = opaque_zero();
         if (((a.synd >> r) & 1u) && a.w[o][r] != 0)
-          mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * C::p + r));
+          mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * NS + r));
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -496,13 +498,19 @@ struct BsShape {
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
   BsFn fn[2];         // [nt]
-  BsRecFn rec[2];     // [nt]
+  BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
 };
 
+template <class C, int NS>
+constexpr BsRecFn rec_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS>;
+  else return nullptr;
+}
 #define BS(F, FIELD, K, P)                                                      \
   {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                             \
    {bitslice_kernel<Code<F, K, P>, false>, bitslice_kernel<Code<F, K, P>, true>}, \
-   {bitslice_recon_kernel<Code<F, K, P>, false>, bitslice_recon_kernel<Code<F, K, P>, true>}}
+   {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
+    rec_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
     BS(CF8, 8, 10, 4),    // BASELINE headline: galois_8 10+4
     BS(CF8, 8, 10, 2),    // benches/bandwidth.rs 10+2
@@ -552,8 +560,13 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;
     if (gx > total) gx = total;
     if (gx > 0x7fffffffu) gx = 0x7fffffffu;
-    hipLaunchKernelGGL(sh.rec[get_option(1) ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
-                       a, cps);
+    // rows needed: sigma (R and missing parity); NS = smallest compiled cover
+    const uint32_t need = 32u - (uint32_t)__builtin_clz(a.sigma | 1u);
+    int slot = -1;
+    for (int q = 0; q < 4 && slot < 0; ++q)
+      if (sh.rec[q] && (1u << q) >= need) slot = q;
+    if (slot < 0) return hipSuccess;
+    hipLaunchKernelGGL(sh.rec[slot], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     count_bitslice_launch();

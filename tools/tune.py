@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--variants", type=int, default=1)
     ap.add_argument("--bitslice", default="1", help="comma list of RSE_OPT_BITSLICE values")
     ap.add_argument("--shapes", default="", help="gx:gy,gx:gy,... (default: built-in list)")
+    ap.add_argument("--erase", default="0,1", help="reconstruct: erased shard indices")
+    ap.add_argument("--nt-only", action="store_true", help="only non-temporal configurations")
     args = ap.parse_args()
     lib = R._lib.load()
     k, p, L, S = args.k, args.p, args.shard_mib * MiB, args.stripes
@@ -45,7 +47,8 @@ def main():
             fill_splitmix(v[s, i], 1, (s << 8) | i)
     r = R.core.ReedSolomon(k, p, args.field)
     elems = L // (args.field // 8)
-    present = [i not in (0, 1) for i in range(k + p)]
+    erased = [int(x) for x in args.erase.split(",")]
+    present = [i not in erased for i in range(k + p)]
 
     def op():
         if args.op == "encode":
@@ -53,13 +56,14 @@ def main():
         else:
             r.reconstruct_data_flat(buf, elems, S, present)
 
-    nbytes = S * ((k + p) if args.op == "encode" else (k + 2)) * L
+    nbytes = S * ((k + p) if args.op == "encode" else (k + len(erased))) * L
     shapes = [(512, 1), (1024, 1), (2048, 1), (4096, 1), (8, 0), (16, 0)]
     if args.shapes:
         shapes = [tuple(int(x) for x in s.split(":")) for s in args.shapes.split(",")]
     bss = [int(x) for x in args.bitslice.split(",")]
+    nts = (0, 1) if not args.nt_only else (1,)
     configs = [(nt, gx, gy, var, bs) for bs in bss for var in range(args.variants)
-               for nt in (0, 1) for gx, gy in shapes]
+               for nt in nts for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
@@ -80,7 +84,8 @@ def main():
             res[c].append(nbytes / (a.elapsed_time(b) * 1e-3) / 1e9)
         print(f"round {rnd} done", flush=True)
     rows = sorted(((statistics.median(x), min(x), max(x), c) for c, x in res.items()), reverse=True)
-    print(f"{args.op} GF(2^{args.field}) {k}+{p} x {args.shard_mib} MiB, {S} stripes; GB/s (1e9)")
+    what = f" erased {erased}" if args.op == "reconstruct" else ""
+    print(f"{args.op} GF(2^{args.field}) {k}+{p} x {args.shard_mib} MiB, {S} stripes{what}; GB/s (1e9)")
     for med, lo, hi, (nt, gx, gy, var, bs) in rows:
         print(f"  bitslice={bs} variant={var} nt={nt} grid_x={gx:<5} stripes_in_flight={gy:<3}  median "
               f"{med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
