@@ -336,6 +336,22 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     out["end_to_end_pinned_host"] = {
         "what": "rse_encode_host, 1 stripe from pinned host memory (H2D data + kernel + D2H parity)",
         "MB_per_s": round((k + p) * L / dt / MiB, 1), "parity_matches_device": ok}
+    # many stripes through one pipeline (rse_encode_host_flat)
+    ns = min(8, n_stripes)
+    hflat = v[:ns].reshape(-1).cpu().pin_memory()
+    hflat.view(ns, k + p, L)[:, k:].zero_()
+    r.encode_host_flat(hflat, L, ns)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        r.encode_host_flat(hflat, L, ns)
+    dt = (time.perf_counter() - t0) / reps
+    ok = torch.equal(hflat.view(ns, k + p, L)[:, k:], v[:ns, k:].cpu())
+    out["end_to_end_pinned_host_flat"] = {
+        "what": f"rse_encode_host_flat, {ns} stripes from pinned host memory, one "
+                "H2D/kernel/D2H pipeline",
+        "MB_per_s": round(ns * (k + p) * L / dt / MiB, 1),
+        "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1), "parity_matches_device": ok}
     return out
 
 

@@ -164,6 +164,10 @@ int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, si
  * staged D2H, chunked and double-buffered on `stream`.  Synchronous. */
 int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *lens,
                     size_t n_shards, rse_stream_t stream);
+/* Flat host stripes (rse_encode_flat layout, HOST memory): the same pipeline
+ * over every chunk of every stripe, so PCIe stays busy across stripes. */
+int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len,
+                         size_t n_stripes, rse_stream_t stream);
 
 /* ---- launch-shape options (performance only; results never change) ----- */
 #define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */

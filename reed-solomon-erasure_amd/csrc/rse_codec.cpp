@@ -877,11 +877,85 @@ int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, si
   return RSE_OK;
 }
 
-// Host shards in, host parity out: chunks of every shard are staged H2D, coded
-// and staged D2H on two streams in turn, so chunk c+1's copies overlap chunk c's
-// kernel (and H2D overlaps D2H on the full-duplex link).  Pinned host memory
-// gives truly asynchronous DMA; pageable memory still works (the runtime
-// stages it) but serialises the copies.
+// Host shards in, host parity out: a three-stage pipeline over chunks of every
+// shard (H2D of the data chunk on one stream, the coding kernel on a second,
+// D2H of the parity chunk on a third), with a ring of kRing device buffer
+// sets so chunk c's H2D overlaps chunk c-1's kernel and chunk c-2's D2H (and
+// H2D overlaps D2H on the full-duplex link).  Pinned host memory gives truly
+// asynchronous DMA; pageable memory works (the runtime stages it) but
+// serialises the copies.  `stripes` lists, per stripe, the k data pointers
+// then the p parity pointers.
+int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& stripes,
+                         size_t bytes, hipStream_t user) {
+  constexpr int kRing = 3;
+  const size_t chunk = std::min<size_t>(bytes, (size_t)4 << 20);
+  const size_t per_stripe = (bytes + chunk - 1) / chunk;
+  const size_t nchunks = per_stripe * stripes.size();
+  hipStream_t st[3] = {nullptr, nullptr, nullptr};  // h2d, kernel, d2h
+  hipEvent_t done[3][kRing] = {};                   // [stage][ring slot]
+  uint8_t* dbuf = nullptr;
+  hipError_t e = hipSuccess;
+  for (int q = 0; q < 3 && e == hipSuccess; ++q)
+    e = hipStreamCreateWithFlags(&st[q], hipStreamNonBlocking);
+  for (int q = 0; q < 3 && e == hipSuccess; ++q)
+    for (int b = 0; b < kRing && e == hipSuccess; ++b)
+      e = hipEventCreateWithFlags(&done[q][b], hipEventDisableTiming);
+  hipEvent_t start = nullptr;
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&start, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), kRing * c->total * chunk, user);
+  if (e == hipSuccess) e = hipEventRecord(start, user);  // everything starts after the caller's work
+  for (int q = 0; q < 3 && e == hipSuccess; ++q) e = hipStreamWaitEvent(st[q], start, 0);
+  const Rows rows = parity_rows(c);
+  std::vector<const uint8_t*> in(c->k);
+  std::vector<uint8_t*> out(c->p);
+  int rc = RSE_OK;
+  for (size_t ci = 0; e == hipSuccess && rc == RSE_OK && ci < nchunks; ++ci) {
+    void* const* sh = stripes[ci / per_stripe];
+    const size_t off = (ci % per_stripe) * chunk, sz = std::min(chunk, bytes - off);
+    const int b = (int)(ci % kRing);
+    uint8_t* set = dbuf + b * c->total * chunk;
+    // H2D: the slot's previous D2H must have drained
+    if (ci >= (size_t)kRing) e = hipStreamWaitEvent(st[0], done[2][b], 0);
+    for (size_t i = 0; e == hipSuccess && i < c->k; ++i) {
+      e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(sh[i]) + off, sz,
+                         hipMemcpyHostToDevice, st[0]);
+      in[i] = set + i * chunk;
+    }
+    if (e == hipSuccess) e = hipEventRecord(done[0][b], st[0]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st[1], done[0][b], 0);
+    if (e != hipSuccess) break;
+    for (size_t r = 0; r < c->p; ++r) out[r] = set + (c->k + r) * chunk;
+    Job j{c->field, &rows, in.data(), out.data(), nullptr, sz, rse::kStore, false, nullptr, 0, 1};
+    rc = run_job(j, st[1]);
+    if (rc) break;
+    e = hipEventRecord(done[1][b], st[1]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st[2], done[1][b], 0);
+    for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
+      e = hipMemcpyAsync(static_cast<uint8_t*>(sh[c->k + r]) + off, out[r], sz,
+                         hipMemcpyDeviceToHost, st[2]);
+    if (e == hipSuccess) e = hipEventRecord(done[2][b], st[2]);
+  }
+  // join: the caller's stream waits for all three, frees the ring, syncs
+  hipError_t e2 = hipSuccess;
+  for (int q = 0; q < 3 && e2 == hipSuccess; ++q)
+    if (st[q]) {
+      e2 = hipEventRecord(start, st[q]);
+      if (e2 == hipSuccess) e2 = hipStreamWaitEvent(user, start, 0);
+    }
+  if (dbuf) (void)hipFreeAsync(dbuf, user);
+  if (e2 == hipSuccess) e2 = hipStreamSynchronize(user);
+  for (int q = 0; q < 3; ++q) {
+    for (int b = 0; b < kRing; ++b)
+      if (done[q][b]) (void)hipEventDestroy(done[q][b]);
+    if (st[q]) (void)hipStreamDestroy(st[q]);
+  }
+  if (start) (void)hipEventDestroy(start);
+  if (rc) return rc;
+  if (e != hipSuccess) return dev_fail(e);
+  if (e2 != hipSuccess) return dev_fail(e2);
+  return RSE_OK;
+}
+
 int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
                     rse_stream_t stream) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
@@ -891,48 +965,23 @@ int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens,
   if ((rc = check_multi(lens, n))) return rc;
   for (size_t i = 0; i < n; ++i)
     if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
-  hipStream_t s0 = (hipStream_t)stream, s1 = nullptr;
-  const size_t bytes = lens[0] * c->esize();
-  const size_t chunk = std::min<size_t>(bytes, (size_t)8 << 20);
-  const size_t nchunks = (bytes + chunk - 1) / chunk;
-  uint8_t* dbuf = nullptr;
-  hipEvent_t ev = nullptr;
-  RSE_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
-  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), 2 * c->total * chunk, s0);
-  if (e == hipSuccess) e = hipEventRecord(ev, s0);  // s1 starts after s0's prior work
-  if (e == hipSuccess) e = hipStreamWaitEvent(s1, ev, 0);
-  const Rows rows = parity_rows(c);
-  std::vector<const uint8_t*> in(c->k);
-  std::vector<uint8_t*> out(c->p);
-  for (size_t ci = 0; e == hipSuccess && ci < nchunks; ++ci) {
-    const size_t off = ci * chunk, sz = std::min(chunk, bytes - off);
-    hipStream_t st = (ci & 1) ? s1 : s0;
-    uint8_t* set = dbuf + (ci & 1) * c->total * chunk;
-    for (size_t i = 0; e == hipSuccess && i < c->k; ++i) {
-      e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(shards[i]) + off, sz,
-                         hipMemcpyHostToDevice, st);
-      in[i] = set + i * chunk;
-    }
-    for (size_t r = 0; r < c->p; ++r) out[r] = set + (c->k + r) * chunk;
-    if (e != hipSuccess) break;
-    Job j{c->field, &rows, in.data(), out.data(), nullptr, sz, rse::kStore, false, nullptr, 0, 1};
-    rc = run_job(j, st);
-    if (rc) break;
-    for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
-      e = hipMemcpyAsync(static_cast<uint8_t*>(shards[c->k + r]) + off, out[r], sz,
-                         hipMemcpyDeviceToHost, st);
+  return encode_host_pipeline(c, {shards}, lens[0] * c->esize(), (hipStream_t)stream);
+}
+
+int rse_encode_host_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
+                         rse_stream_t stream) {
+  if (!c || !stripes) return RSE_ERR_INVALID_ARGUMENT;
+  if (n_stripes == 0) return RSE_OK;
+  if (shard_len == 0) return RSE_EMPTY_SHARD;
+  const size_t sb = shard_len * c->esize();
+  std::vector<void*> ptrs(n_stripes * c->total);
+  std::vector<void* const*> list(n_stripes);
+  for (size_t s = 0; s < n_stripes; ++s) {
+    for (size_t i = 0; i < c->total; ++i)
+      ptrs[s * c->total + i] = static_cast<uint8_t*>(stripes) + (s * c->total + i) * sb;
+    list[s] = &ptrs[s * c->total];
   }
-  hipError_t e2 = hipEventRecord(ev, s1);
-  if (e2 == hipSuccess) e2 = hipStreamWaitEvent(s0, ev, 0);
-  if (dbuf) (void)hipFreeAsync(dbuf, s0);
-  if (e2 == hipSuccess) e2 = hipStreamSynchronize(s0);
-  if (ev) (void)hipEventDestroy(ev);
-  (void)hipStreamDestroy(s1);
-  if (rc) return rc;
-  if (e != hipSuccess) return dev_fail(e);
-  if (e2 != hipSuccess) return dev_fail(e2);
-  return RSE_OK;
+  return encode_host_pipeline(c, list, sb, (hipStream_t)stream);
 }
 
 int rse_set_option(int key, int64_t value) {

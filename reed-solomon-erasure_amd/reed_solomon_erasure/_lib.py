@@ -21,7 +21,7 @@ EXPORTS = (
     "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
     "rse_encode_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
     "rse_code_shards",
-    "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_fill_splitmix",
+    "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_encode_host_flat", "rse_fill_splitmix",
     "rse_set_option", "rse_get_option",
 )
 
@@ -54,6 +54,7 @@ _SIGS = {
     "rse_encode_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _vp]),
     "rse_reconstruct_data_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
     "rse_reconstruct_batch": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _c.c_int, _vp]),
+    "rse_encode_host_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _vp]),
     "rse_code_shards": (_c.c_int, [_c.c_int, _u8p, _sz, _sz, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_gf8_mul_slice": (_c.c_int, [_c.c_uint8, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),

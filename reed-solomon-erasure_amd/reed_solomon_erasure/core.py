@@ -298,6 +298,19 @@ class ReedSolomon:
         la = (ctypes.c_size_t * max(1, n))(*lens)
         _raise(_lib.rse_encode_host(self._h, pa, la, n, _stream()))
 
+    def encode_host_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int) -> None:
+        """encode_flat() for a HOST buffer (pinned for overlapped DMA): one
+        H2D / kernel / D2H pipeline across all stripes.  Synchronous."""
+        if stripes.is_cuda:
+            raise ValueError("encode_host_flat takes host memory")
+        if stripes.dtype != torch.uint8 or not stripes.is_contiguous():
+            raise ValueError("stripes must be a contiguous uint8 tensor")
+        need = n_stripes * self.total_shard_count() * shard_len * (self.field // 8)
+        if stripes.numel() < need:
+            raise ValueError(f"stripes holds {stripes.numel()} bytes, {need} needed")
+        _raise(_lib.rse_encode_host_flat(self._h, stripes.data_ptr(), shard_len, n_stripes,
+                                         _stream()))
+
 
 def _first(shards):
     return shards[0] if len(shards) else None

@@ -603,6 +603,17 @@ def test_encode_host_matches_device(R):
         r.encode(ds)
         for i in range(p):
             assert (hs[k + i].numpy() == host(ds[k + i])).all()
+    # flat host stripes through one pipeline, pinned and pageable
+    for pin in (True, False):
+        n, stripes = (4 << 20) + 100, 3
+        rng2 = np.random.default_rng(pin)
+        h = torch.from_numpy(rng2.integers(0, 256, stripes * (k + p) * n, dtype=np.uint8))
+        if pin:
+            h = h.pin_memory()
+        d = h.cuda()
+        r.encode_host_flat(h, n, stripes)
+        r.encode_flat(d, n, stripes)
+        assert torch.equal(h, d.cpu())
     # pageable numpy memory works too
     data = rand_shards(rng, k, 5000)
     hs = data + [np.zeros(5000, np.uint8) for _ in range(p)]
