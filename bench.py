@@ -192,9 +192,19 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
+    # RSE_BENCH_REHEARSAL=1: every rank on cuda:0 over gloo, so the N > 1 path
+    # can be exercised on a one-GPU box (tests/test_gpu_parity.py); the
+    # driver's multi-GPU runs use one GPU per rank over RCCL ("nccl")
+    rehearsal = os.environ.get("RSE_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    coll_dev = None if rehearsal else "cuda"
     import reed_solomon_erasure as R
     from reed_solomon_erasure.core import fill_splitmix
 
@@ -257,7 +267,7 @@ def main(argv=None):
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    elapsed = reduce_timing(elapsed, world, device="cuda")
+    elapsed = reduce_timing(elapsed, world, device=coll_dev)
     value = job_throughput(args.steps, n_local, world, stripe_bytes, elapsed)
 
     extras = {}

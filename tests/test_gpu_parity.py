@@ -727,3 +727,25 @@ def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
     finally:
         for key, val in zip((1, 2, 3, 4), saved):
             lib.rse_set_option(key, val)
+
+
+# ------------------------------------------------------------ bench, N > 1
+def test_bench_two_ranks_rehearsal(tmp_path):
+    """bench.py's multi-rank path (torch.distributed.run, barrier, max-over-
+    ranks timing, whole-job value) with 2 ranks sharing the one GPU over gloo."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSE_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--stripes", "4", "--no-cpu",
+           "--no-extras"]
+    out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_stripes_per_step"] == 8
+    assert d["config"]["parity_check_vs_reference"] is True
+    assert d["value"] > 0 and d["roofline"]["achieved"] > 0
