@@ -557,7 +557,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const uint64_t cps = n_vec / (kBsChunk / 16);
     const uint64_t total = cps * a.n_stripes;
     const int64_t grid = get_option(2);
-    uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;  // tools/tune.py --op reconstruct sweeps
     if (gx > total) gx = total;
     if (gx > 0x7fffffffu) gx = 0x7fffffffu;
     // rows needed: sigma (R and missing parity); NS = smallest compiled cover
