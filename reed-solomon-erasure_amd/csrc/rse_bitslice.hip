@@ -36,6 +36,7 @@ namespace {
 
 constexpr int kBsBlock = 256;
 constexpr uint64_t kBsChunk = 16384;  // bytes of one shard per workgroup step
+constexpr int kBsDefaultVariant = 0;  // bitslice_kernel variant (tools/tune.py sweeps)
 
 // ----------------------------------------------------------- constexpr GF
 // GF(2^8), generating polynomial 0x11D (build.rs:11), log/exp built the way
@@ -287,11 +288,21 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&i
 
 // Inputs I.. of one chunk: the loads of input I + 1 are issued before input
 // I is coded, so one input's worth of vectors is always in flight.
-template <class C, bool NT, int I>
+//  SB: a scheduling barrier keeps those loads ahead of input I's XOR network;
+//      without it the scheduler sinks them next to their first use (register
+//      pressure heuristics), which serialises HBM latency and compute.
+//  XC: the last input prefetches input 0 of the workgroup's next chunk
+//      (next_off, ~0 if none) into cur, so the output phase overlaps it too.
+template <class C, bool NT, bool SB, bool XC, int I>
 __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
-                                            const CodeArgs& a, uint64_t off) {
+                                            const CodeArgs& a, uint64_t off, uint64_t next_off) {
   u32x4 nxt[4];
-  if constexpr (I + 1 < C::k) load4<NT>(nxt, a.in[I + 1] + off);
+  if constexpr (I + 1 < C::k) {
+    load4<NT>(nxt, a.in[I + 1] + off);
+  } else if constexpr (XC) {
+    if (next_off != ~0ull) load4<NT>(nxt, a.in[0] + next_off);
+  }
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   uint32_t pl[16];
   slice<typename C::Field>(cur, pl);
   mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
@@ -302,26 +313,37 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   if constexpr (I + 1 < C::k) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    code_inputs<C, NT, I + 1>(acc, cur, a, off);
+    code_inputs<C, NT, SB, XC, I + 1>(acc, cur, a, off, next_off);
+  } else if constexpr (XC) {
+    if (next_off != ~0ull) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
   }
 }
 
 // One workgroup step = one 16 KiB chunk of one stripe; chunks of all stripes
 // are one flat index space walked grid-stride.  a.n_vec counts whole chunks'
 // vectors only (the host codes the remainder with the table kernels).
-template <class C, bool NT>
+template <class C, bool NT, bool SB, bool XC>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
   const uint32_t mode = a.mode;
   bool diff = false;
-  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+  auto chunk_off = [&](uint64_t idx) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+    return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+  };
+  u32x4 cur[4];
+  if (XC && blockIdx.x < total) load4<NT>(cur, a.in[0] + chunk_off(blockIdx.x));
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t off = chunk_off(idx);
+    const uint64_t nidx = idx + gridDim.x;
+    const uint64_t next_off = (XC && nidx < total) ? chunk_off(nidx) : ~0ull;
     uint32_t acc[C::p * 16];
-    u32x4 cur[4];
-    load4<NT>(cur, a.in[0] + off);
-    code_inputs<C, NT, 0>(acc, cur, a, off);
+    if (!XC) load4<NT>(cur, a.in[0] + off);
+    code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
 #pragma unroll
     for (int o = 0; o < C::p; ++o) {
       uint32_t pl[16];
@@ -367,6 +389,7 @@ __device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&c
       const uint64_t rest = mask >> (I + 1);
       u32x4 nxt[4];
       if (rest) load4<NT>(nxt, recon_ptr(a, C::k, I + 1 + __builtin_ctzll(rest)) + off);
+      __builtin_amdgcn_sched_barrier(0);  // as in code_inputs (SB)
       uint32_t pl[16];
       slice<typename C::Field>(cur, pl);
       if constexpr (I < C::k) {
@@ -497,7 +520,7 @@ struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
-  BsFn fn[2];         // [nt]
+  BsFn fn[3][2];      // [variant: 0 plain, 1 +sched barrier, 2 +cross-chunk prefetch][nt]
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
 };
 
@@ -508,7 +531,10 @@ constexpr BsRecFn rec_fn() {
 }
 #define BS(F, FIELD, K, P)                                                      \
   {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                             \
-   {bitslice_kernel<Code<F, K, P>, false>, bitslice_kernel<Code<F, K, P>, true>}, \
+   {{bitslice_kernel<Code<F, K, P>, false, false, false>,                        \
+     bitslice_kernel<Code<F, K, P>, true, false, false>},                         \
+    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false>},                 \
+    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, true>}},                 \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
@@ -534,7 +560,12 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;  // tools/tune.py sweeps
     if (gx > total) gx = total;
     if (gx > 0x7fffffffu) gx = 0x7fffffffu;
-    hipLaunchKernelGGL(sh.fn[nt ? 1 : 0], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
+    // RSE_OPT_KERNEL_VARIANT picks a bit-sliced variant too (-1: default)
+    const int64_t vopt = get_option(4);
+    int v = (vopt >= 0 && vopt < 3) ? (int)vopt : kBsDefaultVariant;
+    BsFn fn = sh.fn[v][nt ? 1 : 0];
+    if (!fn) fn = sh.fn[v][1];
+    hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     *handled = true;

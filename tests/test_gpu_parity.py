@@ -534,6 +534,41 @@ def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra
 
 
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
+def test_bitslice_kernel_variants(R, field, k, p):
+    """Every compiled bit-sliced encode variant (plain, scheduling barrier,
+    cross-chunk prefetch) x nt, over several stripes and workgroup counts so
+    that workgroups run 0, 1 and many chunks."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 5 * 16384
+    rng = np.random.default_rng(field + k + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    stripes = 3
+    base = np.concatenate([np.concatenate(full)] * stripes)
+    r = R.core.ReedSolomon(k, p, field)
+    try:
+        for var in (0, 1, 2):
+            for nt in (0, 1):
+                for gx in (1, 7, 4096):
+                    lib.rse_set_option(4, var)
+                    lib.rse_set_option(1, nt)
+                    lib.rse_set_option(2, gx)
+                    d = dev(base)
+                    d.view(stripes, k + p, nbytes)[:, k:].fill_(0)
+                    n0 = lib.rse_get_option(6)
+                    r.encode_flat(d, nbytes // es, stripes)
+                    torch.cuda.synchronize()
+                    assert lib.rse_get_option(6) - n0 == 1
+                    assert (host(d) == base).all(), (var, nt, gx)
+    finally:
+        lib.rse_set_option(4, -1)
+        lib.rse_set_option(1, 1)
+        lib.rse_set_option(2, 0)
+
+
+@pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
 def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
     """Syndrome reconstruct on the bit-sliced kernels (compiled parity rows,
     runtime erasure pattern) against the oracle: every number of erased
