@@ -36,7 +36,7 @@ namespace {
 
 constexpr int kBsBlock = 256;
 constexpr uint64_t kBsChunk = 16384;  // bytes of one shard per workgroup step
-constexpr int kBsDefaultVariant = 0;  // bitslice_kernel variant (tools/tune.py sweeps)
+constexpr int kBsDefaultVariant = 1;  // bitslice_kernel variant (tools/tune.py sweeps)
 
 // ----------------------------------------------------------- constexpr GF
 // GF(2^8), generating polynomial 0x11D (build.rs:11), log/exp built the way
