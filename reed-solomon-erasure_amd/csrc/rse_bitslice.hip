@@ -286,6 +286,30 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&i
      ...);
 }
 
+// Output phase of one chunk: un-slice every output's planes and store them
+// (kStore), compare them with the stored parity (kCheck), or both.
+template <class C, bool NT>
+__device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const CodeArgs& a,
+                                              uint64_t off, uint32_t mode, bool& diff) {
+#pragma unroll
+  for (int o = 0; o < C::p; ++o) {
+    uint32_t pl[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
+    u32x4 v[4];
+    unslice<typename C::Field>(pl, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t o16 = off + j * (kBsBlock * 16);
+      if (mode != kCheck) stv<NT>(a.out[o] + o16, v[j]);
+      if (mode != kStore) {
+        const u32x4 w = ldv<NT>(a.cmp[o] + o16);
+        diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
+      }
+    }
+  }
+}
+
 // Inputs I.. of one chunk: the loads of input I + 1 are issued before input
 // I is coded, so one input's worth of vectors is always in flight.
 //  SB: a scheduling barrier keeps those loads ahead of input I's XOR network;
@@ -344,24 +368,115 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     uint32_t acc[C::p * 16];
     if (!XC) load4<NT>(cur, a.in[0] + off);
     code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
-#pragma unroll
-    for (int o = 0; o < C::p; ++o) {
-      uint32_t pl[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
-      u32x4 v[4];
-      unslice<typename C::Field>(pl, v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t o16 = off + j * (kBsBlock * 16);
-        if (mode != kCheck) stv<NT>(a.out[o] + o16, v[j]);
-        if (mode != kStore) {
-          const u32x4 w = ldv<NT>(a.cmp[o] + o16);
-          diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
-        }
-      }
-    }
+    store_outputs<C, NT>(acc, a, off, mode, diff);
   }
+  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+}
+
+// ----------------------------------------------- LDS-DMA input ring variant
+// The same kernel with the shard loads issued as global_load_lds_dwordx4
+// (LDS-DMA, no VGPR destination) into a per-wave ring of D input slots, D - 1
+// inputs ahead, across chunk boundaries.  Register-safe by construction: hipcc
+// never sees a VGPR written by an in-flight load.  Completion is counted by
+// hand (MI355X_MICROARCH.md: vmcnt counts loads, stores and LDS-DMA together,
+// in issue order): waiting for step g's DMA leaves the DMAs of the steps
+// issued after it plus, right after a chunk boundary, the previous chunk's
+// output-phase operations (S per chunk) outstanding.
+
+// s_waitcnt vmcnt(n), n a run-time value (wave-uniform) clamped to 63.
+__device__ __forceinline__ void wait_vmcnt(uint32_t n) {
+  switch (n > 63u ? 63u : n) {
+#define RSE_W(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    RSE_W(0) RSE_W(1) RSE_W(2) RSE_W(3) RSE_W(4) RSE_W(5) RSE_W(6) RSE_W(7) RSE_W(8) RSE_W(9)
+    RSE_W(10) RSE_W(11) RSE_W(12) RSE_W(13) RSE_W(14) RSE_W(15) RSE_W(16) RSE_W(17) RSE_W(18)
+    RSE_W(19) RSE_W(20) RSE_W(21) RSE_W(22) RSE_W(23) RSE_W(24) RSE_W(25) RSE_W(26) RSE_W(27)
+    RSE_W(28) RSE_W(29) RSE_W(30) RSE_W(31) RSE_W(32) RSE_W(33) RSE_W(34) RSE_W(35) RSE_W(36)
+    RSE_W(37) RSE_W(38) RSE_W(39) RSE_W(40) RSE_W(41) RSE_W(42) RSE_W(43) RSE_W(44) RSE_W(45)
+    RSE_W(46) RSE_W(47) RSE_W(48) RSE_W(49) RSE_W(50) RSE_W(51) RSE_W(52) RSE_W(53) RSE_W(54)
+    RSE_W(55) RSE_W(56) RSE_W(57) RSE_W(58) RSE_W(59) RSE_W(60) RSE_W(61) RSE_W(62)
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+#undef RSE_W
+  }
+}
+
+// One 16-byte LDS-DMA per lane: LDS[lds + lane * 16] = *g (non-temporal).
+// M0 is saved and restored in the same statement (guide §5.7).
+__device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
+template <class C, int D>
+struct DmaRing {
+  const CodeArgs& a;
+  uint64_t cps, total, steps;
+  uint32_t ring_lds;  // this wave's ring, LDS byte address (wave-uniform)
+  __device__ uint64_t chunk_off(uint64_t idx) const {
+    const uint64_t stripe = idx / cps, chunk = idx - stripe * cps;
+    return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+  }
+  // step h = (chunk h / k of this workgroup, input h % k) into slot h % D
+  __device__ void issue(uint64_t h) const {
+    const uint64_t idx = blockIdx.x + (h / C::k) * gridDim.x;
+    const uint8_t* g = a.in[h % C::k] + chunk_off(idx);
+    const uint32_t l = ring_lds + (uint32_t)(h % D) * 4096u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(g + j * (kBsBlock * 16), l + j * 1024u);
+  }
+};
+
+template <class C, int D, int I>
+__device__ __forceinline__ void dma_inputs(uint32_t (&acc)[C::p * 16], const DmaRing<C, D>& ring,
+                                           const uint8_t* ring_ptr, uint64_t g0, bool after_chunk,
+                                           uint32_t s_ops) {
+  if constexpr (I < C::k) {
+    const uint64_t g = g0 + I;
+    if (g + D - 1 < ring.steps) ring.issue(g + D - 1);
+    const uint64_t ahead = ring.steps - 1 - g;
+    uint32_t n = 4u * (uint32_t)(ahead < (uint64_t)(D - 1) ? ahead : (uint64_t)(D - 1));
+    if (I < D - 1 && after_chunk) n += s_ops;
+    wait_vmcnt(n);
+    u32x4 cur[4];
+    const uint8_t* slot = ring_ptr + (uint32_t)(g % D) * 4096u + (threadIdx.x & 63u) * 16u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const u32x4*>(slot + j * 1024);
+    uint32_t pl[16];
+    slice<typename C::Field>(cur, pl);
+    mac_input<C, I>(acc, pl, std::make_integer_sequence<int, C::p * 16>{});
+#pragma unroll
+    for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+    dma_inputs<C, D, I + 1>(acc, ring, ring_ptr, g0, after_chunk, s_ops);
+  }
+}
+
+template <class C, int D>
+__global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_dma_kernel(
+    const CodeArgs a, uint64_t chunks_per_stripe) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kBsBlock / 64][D][4096];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint8_t* ring_ptr = &ring_mem[wave][0][0];
+  DmaRing<C, D> ring{a, chunks_per_stripe, chunks_per_stripe * a.n_stripes, 0,
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)ring_ptr)};
+  const uint64_t my_chunks =
+      blockIdx.x < ring.total ? (ring.total - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+  ring.steps = my_chunks * C::k;
+  const uint32_t mode = a.mode;
+  const uint32_t s_ops = (mode == kCheckStore ? 8u : 4u) * C::p;  // output phase VMEM ops
+  bool diff = false;
+  for (uint64_t h = 0; h + 1 < (uint64_t)D && h < ring.steps; ++h) ring.issue(h);
+  for (uint64_t c = 0; c < my_chunks; ++c) {
+    const uint64_t off = ring.chunk_off(blockIdx.x + c * gridDim.x);
+    uint32_t acc[C::p * 16];
+    dma_inputs<C, D, 0>(acc, ring, ring_ptr, c * C::k, c > 0, s_ops);
+    store_outputs<C, true>(acc, a, off, mode, diff);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }
 
@@ -520,7 +635,8 @@ struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
-  BsFn fn[3][2];      // [variant: 0 plain, 1 +sched barrier, 2 +cross-chunk prefetch][nt]
+  BsFn fn[5][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
+                      // prefetch, 3/4 LDS-DMA input ring of 3/2 slots (nt only)
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
 };
 
@@ -534,7 +650,9 @@ constexpr BsRecFn rec_fn() {
    {{bitslice_kernel<Code<F, K, P>, false, false, false>,                        \
      bitslice_kernel<Code<F, K, P>, true, false, false>},                         \
     {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false>},                 \
-    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, true>}},                 \
+    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, true>},                  \
+    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 3>},                             \
+    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 2>}},                            \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
@@ -562,7 +680,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     if (gx > 0x7fffffffu) gx = 0x7fffffffu;
     // RSE_OPT_KERNEL_VARIANT picks a bit-sliced variant too (-1: default)
     const int64_t vopt = get_option(4);
-    int v = (vopt >= 0 && vopt < 3) ? (int)vopt : kBsDefaultVariant;
+    int v = (vopt >= 0 && vopt < 5) ? (int)vopt : kBsDefaultVariant;
     BsFn fn = sh.fn[v][nt ? 1 : 0];
     if (!fn) fn = sh.fn[v][1];
     hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);

@@ -536,8 +536,9 @@ def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
 def test_bitslice_kernel_variants(R, field, k, p):
     """Every compiled bit-sliced encode variant (plain, scheduling barrier,
-    cross-chunk prefetch) x nt, over several stripes and workgroup counts so
-    that workgroups run 0, 1 and many chunks."""
+    cross-chunk prefetch, LDS-DMA rings of 3 and 2 slots) x nt, in store and
+    check modes, over several stripes and workgroup counts so that workgroups
+    run 0, 1 and many chunks."""
     lib = R._lib.load()
     es = field // 8
     nbytes = 5 * 16384
@@ -549,7 +550,7 @@ def test_bitslice_kernel_variants(R, field, k, p):
     base = np.concatenate([np.concatenate(full)] * stripes)
     r = R.core.ReedSolomon(k, p, field)
     try:
-        for var in (0, 1, 2):
+        for var in (0, 1, 2, 3, 4):
             for nt in (0, 1):
                 for gx in (1, 7, 4096):
                     lib.rse_set_option(4, var)
@@ -562,6 +563,17 @@ def test_bitslice_kernel_variants(R, field, k, p):
                     torch.cuda.synchronize()
                     assert lib.rse_get_option(6) - n0 == 1
                     assert (host(d) == base).all(), (var, nt, gx)
+                    # check mode (verify) on the same variant: clean, then one flipped byte
+                    for s_ in range(stripes):
+                        sh = [d.view(stripes, k + p, nbytes)[s_, i].view(-1) for i in range(k + p)]
+                        if field == 16:
+                            sh = [x.view(-1, 2) for x in sh]
+                        assert r.verify(sh), (var, nt, gx, s_)
+                    d.view(stripes, k + p, nbytes)[1, k + p - 1, 77] ^= 4
+                    sh = [d.view(stripes, k + p, nbytes)[1, i].view(-1) for i in range(k + p)]
+                    if field == 16:
+                        sh = [x.view(-1, 2) for x in sh]
+                    assert not r.verify(sh), (var, nt, gx)
     finally:
         lib.rse_set_option(4, -1)
         lib.rse_set_option(1, 1)
