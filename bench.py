@@ -333,6 +333,15 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased",
                           "stripes": n_stripes, "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
                           "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
+    # verify (check mode: k+p reads, no writes), stripe by stripe as the API is
+    shards = [[v[s_, i] for i in range(k + p)] for s_ in range(n_stripes)]
+    assert all(r.verify(sh) for sh in shards[:2])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok = all(r.verify(sh) for sh in shards)
+    dt = time.perf_counter() - t0
+    out["verify"] = {"what": f"verify, {n_stripes} stripes, one call each (synchronous)",
+                     "all_ok": ok, "algorithmic_GB_per_s": round(n_stripes * (k + p) * L / dt / 1e9, 1)}
     # end to end from pinned host memory: one stripe, H2D data, D2H parity
     hs = [v[0, i].cpu().pin_memory() for i in range(k)] + \
          [torch.empty(L, dtype=torch.uint8).pin_memory() for _ in range(p)]
