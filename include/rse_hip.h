@@ -178,6 +178,8 @@ int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len
 #define RSE_OPT_BITSLICE 5          /* 1: bit-sliced kernels for compiled codecs (default) */
 #define RSE_OPT_BITSLICE_LAUNCHES 6 /* read-only, per thread: number of bit-sliced kernel
                                        launches so far (diagnostics / tests) */
+#define RSE_OPT_HOST_CHUNK_KIB 7    /* rse_encode_host*: bytes per shard per pipeline chunk, KiB */
+#define RSE_OPT_HOST_H2D_STREAMS 8  /* rse_encode_host*: streams carrying H2D copies (1..4) */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

@@ -878,77 +878,83 @@ int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, si
 }
 
 // Host shards in, host parity out: a three-stage pipeline over chunks of every
-// shard (H2D of the data chunk on one stream, the coding kernel on a second,
-// D2H of the parity chunk on a third), with a ring of kRing device buffer
-// sets so chunk c's H2D overlaps chunk c-1's kernel and chunk c-2's D2H (and
-// H2D overlaps D2H on the full-duplex link).  Pinned host memory gives truly
+// shard (H2D of the data chunk on one of RSE_OPT_HOST_H2D_STREAMS streams, the
+// coding kernel on another, D2H of the parity chunk on a third), with a ring
+// of device buffer sets so chunk c's H2D overlaps chunk c-1's kernel and chunk
+// c-2's D2H (and H2D overlaps D2H on the full-duplex link).  Pinned host memory gives truly
 // asynchronous DMA; pageable memory works (the runtime stages it) but
 // serialises the copies.  `stripes` lists, per stripe, the k data pointers
 // then the p parity pointers.
 int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& stripes,
                          size_t bytes, hipStream_t user) {
-  constexpr int kRing = 3;
-  const size_t chunk = std::min<size_t>(bytes, (size_t)4 << 20);
+  const int64_t chunk_kib = rse::get_option(RSE_OPT_HOST_CHUNK_KIB);
+  const int nh = (int)std::max<int64_t>(1, std::min<int64_t>(4, rse::get_option(RSE_OPT_HOST_H2D_STREAMS)));
+  const int ring = std::max(3, nh + 2);  // slots: nh filling, one coding, one draining
+  const size_t chunk = std::min<size_t>(bytes, (size_t)std::max<int64_t>(64, chunk_kib) << 10);
   const size_t per_stripe = (bytes + chunk - 1) / chunk;
   const size_t nchunks = per_stripe * stripes.size();
-  hipStream_t st[3] = {nullptr, nullptr, nullptr};  // h2d, kernel, d2h
-  hipEvent_t done[3][kRing] = {};                   // [stage][ring slot]
+  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H
+  std::vector<hipStream_t> st(nh + 2, nullptr);
+  std::vector<hipEvent_t> h2d(ring, nullptr), coded(ring, nullptr), d2h(ring, nullptr);
   uint8_t* dbuf = nullptr;
-  hipError_t e = hipSuccess;
-  for (int q = 0; q < 3 && e == hipSuccess; ++q)
-    e = hipStreamCreateWithFlags(&st[q], hipStreamNonBlocking);
-  for (int q = 0; q < 3 && e == hipSuccess; ++q)
-    for (int b = 0; b < kRing && e == hipSuccess; ++b)
-      e = hipEventCreateWithFlags(&done[q][b], hipEventDisableTiming);
   hipEvent_t start = nullptr;
+  hipError_t e = hipSuccess;
+  for (auto& q : st)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+  for (auto* ev : {&h2d, &coded, &d2h})
+    for (auto& q : *ev)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), kRing * c->total * chunk, user);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), ring * c->total * chunk, user);
   if (e == hipSuccess) e = hipEventRecord(start, user);  // everything starts after the caller's work
-  for (int q = 0; q < 3 && e == hipSuccess; ++q) e = hipStreamWaitEvent(st[q], start, 0);
+  for (auto& q : st)
+    if (e == hipSuccess) e = hipStreamWaitEvent(q, start, 0);
   const Rows rows = parity_rows(c);
   std::vector<const uint8_t*> in(c->k);
   std::vector<uint8_t*> out(c->p);
+  hipStream_t kst = st[nh], dst = st[nh + 1];
   int rc = RSE_OK;
   for (size_t ci = 0; e == hipSuccess && rc == RSE_OK && ci < nchunks; ++ci) {
     void* const* sh = stripes[ci / per_stripe];
     const size_t off = (ci % per_stripe) * chunk, sz = std::min(chunk, bytes - off);
-    const int b = (int)(ci % kRing);
+    const int b = (int)(ci % ring);
+    hipStream_t hst = st[ci % nh];
     uint8_t* set = dbuf + b * c->total * chunk;
     // H2D: the slot's previous D2H must have drained
-    if (ci >= (size_t)kRing) e = hipStreamWaitEvent(st[0], done[2][b], 0);
+    if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);
     for (size_t i = 0; e == hipSuccess && i < c->k; ++i) {
       e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(sh[i]) + off, sz,
-                         hipMemcpyHostToDevice, st[0]);
+                         hipMemcpyHostToDevice, hst);
       in[i] = set + i * chunk;
     }
-    if (e == hipSuccess) e = hipEventRecord(done[0][b], st[0]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(st[1], done[0][b], 0);
+    if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
+    if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
     if (e != hipSuccess) break;
     for (size_t r = 0; r < c->p; ++r) out[r] = set + (c->k + r) * chunk;
     Job j{c->field, &rows, in.data(), out.data(), nullptr, sz, rse::kStore, false, nullptr, 0, 1};
-    rc = run_job(j, st[1]);
+    rc = run_job(j, kst);
     if (rc) break;
-    e = hipEventRecord(done[1][b], st[1]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(st[2], done[1][b], 0);
+    e = hipEventRecord(coded[b], kst);
+    if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
     for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
       e = hipMemcpyAsync(static_cast<uint8_t*>(sh[c->k + r]) + off, out[r], sz,
-                         hipMemcpyDeviceToHost, st[2]);
-    if (e == hipSuccess) e = hipEventRecord(done[2][b], st[2]);
+                         hipMemcpyDeviceToHost, dst);
+    if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
   }
-  // join: the caller's stream waits for all three, frees the ring, syncs
+  // join: the caller's stream waits for every stream, frees the ring, syncs
   hipError_t e2 = hipSuccess;
-  for (int q = 0; q < 3 && e2 == hipSuccess; ++q)
-    if (st[q]) {
-      e2 = hipEventRecord(start, st[q]);
+  for (auto& q : st)
+    if (q && e2 == hipSuccess) {
+      e2 = hipEventRecord(start, q);
       if (e2 == hipSuccess) e2 = hipStreamWaitEvent(user, start, 0);
     }
   if (dbuf) (void)hipFreeAsync(dbuf, user);
   if (e2 == hipSuccess) e2 = hipStreamSynchronize(user);
-  for (int q = 0; q < 3; ++q) {
-    for (int b = 0; b < kRing; ++b)
-      if (done[q][b]) (void)hipEventDestroy(done[q][b]);
-    if (st[q]) (void)hipStreamDestroy(st[q]);
-  }
+  for (auto* ev : {&h2d, &coded, &d2h})
+    for (auto& q : *ev)
+      if (q) (void)hipEventDestroy(q);
+  for (auto& q : st)
+    if (q) (void)hipStreamDestroy(q);
   if (start) (void)hipEventDestroy(start);
   if (rc) return rc;
   if (e != hipSuccess) return dev_fail(e);

@@ -750,6 +750,8 @@ struct Options {
   int64_t stripes_in_flight = 1;  // gridDim.y (0 = all stripes at once)
   int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
   int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
+  int64_t host_chunk_kib = 4096;  // host pipeline chunk per shard (rse_encode_host*)
+  int64_t host_h2d_streams = 1;   // host pipeline H2D streams
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1075,6 +1077,8 @@ int set_option(int key, int64_t value) {
     case 3: g_opt.stripes_in_flight = value < 0 ? 0 : value; return 0;
     case 4: g_opt.variant = value; return 0;
     case 5: g_opt.bitslice = value ? 1 : 0; return 0;
+    case 7: g_opt.host_chunk_kib = value < 64 ? 64 : value; return 0;
+    case 8: g_opt.host_h2d_streams = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     default: return -1;
   }
 }
@@ -1089,6 +1093,8 @@ int64_t get_option(int key) {
     case 4: return g_opt.variant;
     case 5: return g_opt.bitslice;
     case 6: return g_bs_launches;
+    case 7: return g_opt.host_chunk_kib;
+    case 8: return g_opt.host_h2d_streams;
     default: return -1;
   }
 }
