@@ -922,10 +922,19 @@ int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& st
     uint8_t* set = dbuf + b * c->total * chunk;
     // H2D: the slot's previous D2H must have drained
     if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);
-    for (size_t i = 0; e == hipSuccess && i < c->k; ++i) {
-      e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(sh[i]) + off, sz,
-                         hipMemcpyHostToDevice, hst);
-      in[i] = set + i * chunk;
+    for (size_t i = 0; i < c->k; ++i) in[i] = set + i * chunk;
+    // equally spaced host shards (flat stripes): one 2D copy for all k chunks
+    const ptrdiff_t pitch = c->k > 1 ? static_cast<uint8_t*>(sh[1]) - static_cast<uint8_t*>(sh[0]) : 0;
+    bool strided = c->k > 1 && pitch > 0 && (size_t)pitch >= sz;
+    for (size_t i = 2; strided && i < c->total; ++i)
+      strided = static_cast<uint8_t*>(sh[i]) - static_cast<uint8_t*>(sh[i - 1]) == pitch;
+    if (e == hipSuccess && strided) {
+      e = hipMemcpy2DAsync(set, chunk, static_cast<uint8_t*>(sh[0]) + off, (size_t)pitch, sz, c->k,
+                           hipMemcpyHostToDevice, hst);
+    } else {
+      for (size_t i = 0; e == hipSuccess && i < c->k; ++i)
+        e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(sh[i]) + off, sz,
+                           hipMemcpyHostToDevice, hst);
     }
     if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
     if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
@@ -936,9 +945,14 @@ int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& st
     if (rc) break;
     e = hipEventRecord(coded[b], kst);
     if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
-    for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
-      e = hipMemcpyAsync(static_cast<uint8_t*>(sh[c->k + r]) + off, out[r], sz,
-                         hipMemcpyDeviceToHost, dst);
+    if (e == hipSuccess && strided && c->p > 1) {
+      e = hipMemcpy2DAsync(static_cast<uint8_t*>(sh[c->k]) + off, (size_t)pitch, out[0], chunk, sz,
+                           c->p, hipMemcpyDeviceToHost, dst);
+    } else {
+      for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
+        e = hipMemcpyAsync(static_cast<uint8_t*>(sh[c->k + r]) + off, out[r], sz,
+                           hipMemcpyDeviceToHost, dst);
+    }
     if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
   }
   // join: the caller's stream waits for every stream, frees the ring, syncs

@@ -751,7 +751,7 @@ struct Options {
   int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
   int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
   int64_t host_chunk_kib = 4096;  // host pipeline chunk per shard (rse_encode_host*)
-  int64_t host_h2d_streams = 1;   // host pipeline H2D streams
+  int64_t host_h2d_streams = 2;   // host pipeline H2D streams (tools/host_e2e.py)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;

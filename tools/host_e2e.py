@@ -81,7 +81,7 @@ def main():
                 best = (rate, chunk, nh)
     print(f"best: chunk={best[1]} KiB h2d_streams={best[2]} {best[0] / 1e9:.1f} GB/s")
     lib.rse_set_option(7, 4096)
-    lib.rse_set_option(8, 1)
+    lib.rse_set_option(8, 2)
 
 
 if __name__ == "__main__":
