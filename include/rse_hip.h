@@ -80,6 +80,17 @@ size_t rse_codec_parity_shard_count(const rse_codec *codec); /* core.rs:473 */
 size_t rse_codec_total_shard_count(const rse_codec *codec);  /* core.rs:477 */
 /* Copy the (k+p) x k encoding matrix, row-major, elem bytes per element. */
 int rse_codec_matrix(const rse_codec *codec, uint8_t *out, size_t out_bytes);
+/* Which kernels code this codec's whole 16 KiB chunks (no reference counterpart;
+ * results are identical either way).  Codecs other than the compiled-in ones
+ * with p <= 8 and k <= 32 get bit-sliced kernels specialised at run time:
+ * rse_codec_new starts a hiprtc compile of the codec's parity rows on a
+ * background thread (host CPU only).  wait != 0 blocks until it has finished. */
+#define RSE_KERNELS_TABLE 0             /* table kernels (rse_kernels.hip) */
+#define RSE_KERNELS_COMPILED 1          /* bit-sliced, compiled into the library */
+#define RSE_KERNELS_SPECIALISED 2       /* bit-sliced, specialised at run time, ready */
+#define RSE_KERNELS_SPECIALISING 3      /* compile in flight (wait == 0) */
+#define RSE_KERNELS_SPECIALISE_FAILED 4 /* compile failed: table kernels */
+int rse_codec_kernel_kind(const rse_codec *codec, int wait);
 
 /* encode (core.rs:597-611): shards[0..k] data, shards[k..k+p] parity (overwritten). */
 int rse_encode(const rse_codec *codec, void *const *shards, const size_t *lens,
@@ -180,6 +191,9 @@ int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len
                                        launches so far (diagnostics / tests) */
 #define RSE_OPT_HOST_CHUNK_KIB 7    /* rse_encode_host*: bytes per shard per pipeline chunk, KiB */
 #define RSE_OPT_HOST_H2D_STREAMS 8  /* rse_encode_host*: streams carrying H2D copies (1..4) */
+#define RSE_OPT_JIT 9               /* run-time specialised kernels: 0 off, 1 used once built
+                                       (default), 2 the first launch waits for the build */
+#define RSE_OPT_JIT_MODULES 10      /* read-only: specialised modules built in this process */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

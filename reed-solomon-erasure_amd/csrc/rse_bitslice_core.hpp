@@ -1,0 +1,403 @@
+// rse_bitslice_core.hpp -- device code of the bit-sliced coding kernels, shared
+// by the codecs compiled into rse_bitslice.hip and by the modules rse_jit.cpp
+// specialises at run time (hiprtc compiles this header as source text, so it
+// may only depend on rse_device.hpp / rse_kernels.hpp).
+//
+// Multiplication by a constant c is a GF(2)-linear map: an 8x8 (GF(2^8)) or
+// 16x16 (GF(2^16)) bit matrix.  With the data bit-sliced -- register q holds
+// bit q of 32 bytes (GF(2^8)) or of 32 elements (GF(2^16)) -- a
+// multiply-accumulate is the XOR of the input planes each row of that bit
+// matrix selects, three at a time in gfx950's v_bitop3_b32: no tables, no
+// v_perm in the network.  A codec type C supplies the matrices as constants:
+//   using Field = BitsF8 | BitsF16 (planes per group and their bit order);
+//   static constexpr int k, p, NP;
+//   static constexpr ... planes.sel[o][i][q]: bit j set iff input plane j
+//     contributes to output plane q of coefficient (o, i).
+//
+// Lane layout: a workgroup of 256 lanes codes a 16 KiB chunk of every shard.
+// Lane t loads the 16-byte vectors t, t+256, t+512, t+768 of the chunk (each
+// load instruction is 4 KiB contiguous per workgroup), i.e. 16 dwords.  GF(2^8):
+// two groups of 8 dwords, each 8x8-bit transposed inside byte lanes.  GF(2^16):
+// 32 elements split into x-coefficient and constant byte planes with v_perm
+// (galois_16.rs:49-51), each 8x8-bit transposed.  Outputs are transposed back
+// the same way (the network is an involution).  Any element order works as
+// long as input and output use the same one; this one keeps every global
+// access coalesced.
+#pragma once
+
+#include "rse_device.hpp"
+
+namespace rse {
+namespace {
+
+constexpr int kBsBlock = 256;
+constexpr uint64_t kBsChunk = 16384;  // bytes of one shard per workgroup step
+
+// std::integer_sequence without <utility> (hiprtc has no C++ library headers)
+template <class T, T... I>
+struct int_seq {};
+template <int N>
+using make_int_seq = __make_integer_seq<int_seq, int, N>;
+
+// Plane order of the two fields.
+struct BitsF8 {
+  static constexpr int kPlanes = 8;
+  // plane q = bit q of the byte
+  static constexpr int bit(int q) { return q; }
+};
+struct BitsF16 {
+  static constexpr int kPlanes = 16;
+  // plane q < 8: bit q of the H (x-coefficient) byte = uint16 bit q + 8;
+  // plane q >= 8: bit q - 8 of the L byte = uint16 bit q - 8
+  static constexpr int bit(int q) { return q ^ 8; }
+};
+
+// ------------------------------------------------------------ bit slicing
+// XOR of acc and the planes selected by M, two at a time.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t* in) {
+  if constexpr (M == 0) {
+    return acc;
+  } else {
+    constexpr int q0 = __builtin_ctz(M);
+    constexpr uint32_t m1 = M & (M - 1);
+    if constexpr (m1 == 0) {
+      return acc ^ in[q0];
+    } else {
+      constexpr int q1 = __builtin_ctz(m1);
+      return xacc<m1 & (m1 - 1)>(xor3(acc, in[q0], in[q1]), in);
+    }
+  }
+}
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xinit(const uint32_t* in) {
+  if constexpr (M == 0) {
+    return 0u;
+  } else {
+    constexpr int q0 = __builtin_ctz(M);
+    return xacc<M & (M - 1)>(in[q0], in);
+  }
+}
+
+// 8x8 bit transpose inside every byte lane of h[0..7] (an involution): bit b
+// of byte lane L of h[i] moves to bit i of byte lane L of h[b].
+__device__ __forceinline__ void transpose8(uint32_t* h) {
+#pragma unroll
+  for (int s = 4, st = 0; st < 3; s >>= 1, ++st) {
+    const uint32_t m = s == 4 ? 0x0F0F0F0Fu : s == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i & s) continue;
+      const uint32_t a = h[i], b = h[i + s];
+      h[i] = (a & ~(m << s)) | ((b & m) << s);
+      h[i + s] = (b & ~m) | ((a >> s) & m);
+    }
+  }
+}
+
+// 4 vectors (16 dwords) -> 16 planes (two groups of 8 for GF(2^8)).
+template <class F>
+__device__ __forceinline__ void slice(const u32x4 (&v)[4], uint32_t (&pl)[16]) {
+  if constexpr (F::kPlanes == 16) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const uint32_t x0 = v[m >> 1][(m & 1) * 2], x1 = v[m >> 1][(m & 1) * 2 + 1];
+      pl[m] = __builtin_amdgcn_perm(x1, x0, 0x06040200u);      // H bytes
+      pl[8 + m] = __builtin_amdgcn_perm(x1, x0, 0x07050301u);  // L bytes
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) pl[d] = v[d >> 2][d & 3];
+  }
+  transpose8(pl);
+  transpose8(pl + 8);
+}
+
+// Inverse of slice (clobbers pl).
+template <class F>
+__device__ __forceinline__ void unslice(uint32_t (&pl)[16], u32x4 (&v)[4]) {
+  transpose8(pl);
+  transpose8(pl + 8);
+  if constexpr (F::kPlanes == 16) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      v[m >> 1][(m & 1) * 2] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x05010400u);
+      v[m >> 1][(m & 1) * 2 + 1] = __builtin_amdgcn_perm(pl[8 + m], pl[m], 0x07030602u);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) v[d >> 2][d & 3] = pl[d];
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ldv(const uint8_t* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void stv(uint8_t* p, u32x4 v) {
+  u32x4* q = reinterpret_cast<u32x4*>(p);
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = ldv<NT>(p + j * (kBsBlock * 16));
+}
+
+// acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
+// every output o, group g and plane p.
+template <class C, int I, int N, int... OP>
+__device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&in)[16],
+                                          int_seq<int, OP...>) {
+  if constexpr (I == 0)
+    ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),
+     ...);
+  else
+    ((acc[OP] = xacc<C::planes.sel[OP / 16][I][OP % C::NP]>(acc[OP],
+                                                              in + (OP % 16) / C::NP * C::NP)),
+     ...);
+}
+
+// Output phase of one chunk: un-slice every output's planes and store them
+// (kStore), compare them with the stored parity (kCheck), or both.
+template <class C, bool NT>
+__device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const CodeArgs& a,
+                                              uint64_t off, uint32_t mode, bool& diff) {
+#pragma unroll
+  for (int o = 0; o < C::p; ++o) {
+    uint32_t pl[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
+    u32x4 v[4];
+    unslice<typename C::Field>(pl, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t o16 = off + j * (kBsBlock * 16);
+      if (mode != kCheck) stv<NT>(a.out[o] + o16, v[j]);
+      if (mode != kStore) {
+        const u32x4 w = ldv<NT>(a.cmp[o] + o16);
+        diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
+      }
+    }
+  }
+}
+
+// Inputs I.. of one chunk: the loads of input I + 1 are issued before input
+// I is coded, so one input's worth of vectors is always in flight.
+//  SB: a scheduling barrier keeps those loads ahead of input I's XOR network;
+//      without it the scheduler sinks them next to their first use (register
+//      pressure heuristics), which serialises HBM latency and compute.
+//  XC: the last input prefetches input 0 of the workgroup's next chunk
+//      (next_off, ~0 if none) into cur, so the output phase overlaps it too.
+template <class C, bool NT, bool SB, bool XC, int I>
+__device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
+                                            const CodeArgs& a, uint64_t off, uint64_t next_off) {
+  u32x4 nxt[4];
+  if constexpr (I + 1 < C::k) {
+    load4<NT>(nxt, a.in[I + 1] + off);
+  } else if constexpr (XC) {
+    if (next_off != ~0ull) load4<NT>(nxt, a.in[0] + next_off);
+  }
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+  uint32_t pl[16];
+  slice<typename C::Field>(cur, pl);
+  mac_input<C, I>(acc, pl, make_int_seq<C::p * 16>{});
+  // keep each input's XORs together: without this the compiler reassociates
+  // across inputs and keeps several inputs' planes live (spills)
+#pragma unroll
+  for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+  if constexpr (I + 1 < C::k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    code_inputs<C, NT, SB, XC, I + 1>(acc, cur, a, off, next_off);
+  } else if constexpr (XC) {
+    if (next_off != ~0ull) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
+  }
+}
+
+// Encode / verify body.  One workgroup step = one 16 KiB chunk of one stripe;
+// chunks of all stripes are one flat index space walked grid-stride.  a.n_vec
+// counts whole chunks' vectors only (the host codes the remainder with the
+// table kernels).  Launch bounds: kBsBlock lanes, C::p > 4 ? 2 : 3 waves/SIMD.
+template <class C, bool NT, bool SB, bool XC>
+__device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint32_t mode = a.mode;
+  bool diff = false;
+  auto chunk_off = [&](uint64_t idx) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+  };
+  u32x4 cur[4];
+  if (XC && blockIdx.x < total) load4<NT>(cur, a.in[0] + chunk_off(blockIdx.x));
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t off = chunk_off(idx);
+    const uint64_t nidx = idx + gridDim.x;
+    const uint64_t next_off = (XC && nidx < total) ? chunk_off(nidx) : ~0ull;
+    uint32_t acc[C::p * 16];
+    if (!XC) load4<NT>(cur, a.in[0] + off);
+    code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
+    store_outputs<C, NT>(acc, a, off, mode, diff);
+  }
+  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+}
+
+// ------------------------------------------------------------ reconstruct
+// Bit-sliced syndrome reconstruct (BsReconArgs in rse_kernels.hpp).  The input
+// sequence is the present data shards, then the syndrome parity shards; the
+// next present input's loads are issued before the current one is coded.
+
+// Input index J < k is data shard J, J >= k parity shard J - k.
+__device__ __forceinline__ const uint8_t* recon_ptr(const BsReconArgs& a, uint32_t k, uint32_t j) {
+  return j < k ? a.data[j] : a.par[j - k];
+}
+// Mask of all inputs read: data present bits, then syndrome rows shifted by k.
+__device__ __forceinline__ uint64_t recon_mask(const BsReconArgs& a, uint32_t k) {
+  return (uint64_t)a.present | ((uint64_t)a.synd << k);
+}
+
+// NS: sigma rows computed (rows 0..NS-1; the host picks NS above every row it
+// needs), so a reconstruct pays for the rows it uses, not all p.
+template <class C, bool NT, int NS, int I>
+__device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&cur)[4],
+                                             const BsReconArgs& a, uint64_t mask, uint64_t off) {
+  if constexpr (I < C::k + NS) {
+    if ((mask >> I) & 1u) {
+      const uint64_t rest = mask >> (I + 1);
+      u32x4 nxt[4];
+      if (rest) load4<NT>(nxt, recon_ptr(a, C::k, I + 1 + __builtin_ctzll(rest)) + off);
+      __builtin_amdgcn_sched_barrier(0);  // as in code_inputs (SB)
+      uint32_t pl[16];
+      slice<typename C::Field>(cur, pl);
+      if constexpr (I < C::k) {
+        // every sigma row, needed or not: straight-line XOR networks (a
+        // branch per row costs more in register pressure than the XORs)
+        mac_input<C, I>(acc, pl, make_int_seq<NS * 16>{});
+      } else {  // syndrome: s_r = sigma_r ^ parity_r (slicing is linear)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[(I - C::k) * 16 + q] ^= pl[q];
+      }
+#pragma unroll
+      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      if (rest) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+    recon_inputs<C, NT, NS, I + 1>(acc, cur, a, mask, off);
+  }
+}
+
+// v (4 vectors of elements) times a table-coded constant, XORed into o.
+template <class F>
+__device__ __forceinline__ void mac_vectors(u32x4 (&o)[4], const uint32_t* v, const uint4* tq,
+                                            const uint32_t* tt2, int idx) {
+  if constexpr (F::kPlanes == 8) {
+    const Gf8Tab t = read_tab(tq, tt2, idx);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) o[d >> 2][d & 3] ^= gf8_mul4(t, make_sel(v[d]));
+  } else {
+    const Gf8Tab hh = read_tab(tq, tt2, idx * 4 + 0), lh = read_tab(tq, tt2, idx * 4 + 1);
+    const Gf8Tab hl = read_tab(tq, tt2, idx * 4 + 2), ll = read_tab(tq, tt2, idx * 4 + 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t h0, l0, h1, l1;
+      split_planes(make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]), h0, l0, h1, l1);
+      const Sel sh0 = make_sel(h0), sl0 = make_sel(l0), sh1 = make_sel(h1), sl1 = make_sel(l1);
+      const uint4 m = merge_planes(xor3(gf8_mul4(hh, sh0), gf8_mul4(lh, sl0), 0u),
+                                   xor3(gf8_mul4(hl, sh0), gf8_mul4(ll, sl0), 0u),
+                                   xor3(gf8_mul4(hh, sh1), gf8_mul4(lh, sl1), 0u),
+                                   xor3(gf8_mul4(hl, sh1), gf8_mul4(ll, sl1), 0u));
+      o[j] ^= (u32x4){m.x, m.y, m.z, m.w};
+    }
+  }
+}
+
+// Reconstruct body.  Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
+                                                    uint64_t chunks_per_stripe) {
+  using F = typename C::Field;
+  constexpr int TPC = F::kPlanes == 16 ? 4 : 1;  // GF(2^8) tables per coefficient
+  __shared__ uint4 tq[kMaxOut * NS * TPC];
+  __shared__ uint32_t tt2[kMaxOut * NS * TPC];
+  const uint32_t n_out = a.n_out;
+  for (uint32_t t = threadIdx.x; t < n_out * NS; t += kBsBlock) {
+    const uint32_t c = a.w[t / NS][t % NS];
+    if constexpr (TPC == 1) {
+      write_tab(tq, tt2, t, make_gf8_tab(c));
+    } else {
+      uint32_t sub[4];
+      gf16_sub_coefs(c, sub);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) write_tab(tq, tt2, t * 4 + q, make_gf8_tab(sub[q]));
+    }
+  }
+  __syncthreads();
+  const uint64_t mask = recon_mask(a, C::k);
+  const int first = __builtin_ctzll(mask);  // host guarantees mask != 0
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+    uint32_t acc[NS * 16];
+#pragma unroll
+    for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
+    u32x4 cur[4];
+    load4<NT>(cur, recon_ptr(a, C::k, first) + off);
+    recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
+    // back to element order, in place
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      if (!((a.sigma >> r) & 1u)) continue;
+      uint32_t pl[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pl[q] = acc[r * 16 + q];
+      u32x4 v[4];
+      unslice<F>(pl, v);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[r * 16 + q] = v[q >> 2][q & 3];
+    }
+#pragma unroll 1
+    for (uint32_t o = 0; o < n_out; ++o) {
+      // opaque per output: otherwise LICM hoists every row's byte-plane split
+      // and selectors out of this loop (hundreds of VGPRs -> scratch)
+#pragma unroll
+      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      u32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (u32x4){0u, 0u, 0u, 0u};
+      const int os = a.out_sigma[o];
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        if (os == r) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] ^= acc[r * 16 + q];
+        }
+        // one row's tables at a time: the opaque offset (ordered after the
+        // previous row's pins) keeps hipcc from loading every row's tables
+        // up front, which spills
+        const uint32_t lb = opaque_zero();
+        if (((a.synd >> r) & 1u) && a.w[o][r] != 0)
+          mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * NS + r));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(v[j][w]));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stv<NT>(a.out[o] + off + j * (kBsBlock * 16), v[j]);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace rse

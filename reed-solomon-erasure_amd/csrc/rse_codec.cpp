@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <list>
 #include <map>
@@ -64,6 +65,8 @@ struct rse_codec {
   mutable std::mutex mu;
   mutable std::list<std::pair<std::vector<size_t>, std::vector<uint16_t>>> lru;
   mutable std::map<std::vector<size_t>, decltype(lru)::iterator> index;
+  // run-time specialisation requested (rse_jit.cpp; see want_bitslice)
+  mutable std::atomic<bool> jit_requested{false};
 
   size_t esize() const { return field == 16 ? 2 : 1; }
   uint16_t mat(size_t r, size_t c) const { return field == 16 ? m16.at(r, c) : m8.at(r, c); }
@@ -252,6 +255,21 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
   return r;
 }
 
+// Codecs without compiled-in bit-sliced kernels get them built for their
+// parity rows at run time (rse_jit.cpp: hiprtc on a background thread, host
+// CPU only).  The first call that codes at least one whole bit-sliced chunk
+// requests it, so codecs only ever used on short shards never pay for a build.
+void want_bitslice(const rse_codec* c, size_t len_bytes) {
+  if (len_bytes < rse::bitslice_chunk_bytes() || c->jit_requested.load(std::memory_order_relaxed))
+    return;
+  c->jit_requested.store(true, std::memory_order_relaxed);
+  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p) || c->k > (size_t)kMaxIn ||
+      c->p > rse::kJitMaxOut)
+    return;
+  const Rows rows = parity_rows(c);
+  rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data());
+}
+
 Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, core.rs:492-509
   Rows r;
   r.n_out = c->p;
@@ -416,6 +434,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
   *done = 0;
   const size_t k = c->k, p = c->p;
   const uint64_t cb = rse::bitslice_chunk_bytes();
+  want_bitslice(c, len_bytes);
   if (k > (size_t)kMaxIn || p > (size_t)kMaxOut || len_bytes < cb || stripe_stride % 16u ||
       !rse::get_option(RSE_OPT_BITSLICE))
     return RSE_OK;
@@ -551,6 +570,7 @@ int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* d
   if ((rc = check_multi(data_lens, n_data))) return rc;
   if ((rc = check_multi(parity_lens, n_parity))) return rc;
   if (data_lens[0] != parity_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
+  want_bitslice(c, data_lens[0] * c->esize());
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(data),
         reinterpret_cast<uint8_t* const*>(parity), nullptr, data_lens[0] * c->esize(),
@@ -591,6 +611,7 @@ int verify_impl(const rse_codec* c, const void* const* shards, const size_t* len
     if ((rc = check_multi(buf_lens, n_buf))) return rc;
     if (lens[0] != buf_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
   }
+  want_bitslice(c, lens[0] * c->esize());
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(shards),
         with_buffer ? reinterpret_cast<uint8_t* const*>(buffer) : nullptr,
@@ -673,6 +694,18 @@ int rse_codec_field(const rse_codec* c) { return c ? c->field : 0; }
 size_t rse_codec_data_shard_count(const rse_codec* c) { return c ? c->k : 0; }
 size_t rse_codec_parity_shard_count(const rse_codec* c) { return c ? c->p : 0; }
 size_t rse_codec_total_shard_count(const rse_codec* c) { return c ? c->total : 0; }
+
+int rse_codec_kernel_kind(const rse_codec* c, int wait) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
+  if (wait) want_bitslice(c, rse::bitslice_chunk_bytes());
+  switch (rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, wait != 0)) {
+    case 2: return RSE_KERNELS_SPECIALISED;
+    case 1: return RSE_KERNELS_SPECIALISING;
+    case -1: return RSE_KERNELS_SPECIALISE_FAILED;
+    default: return RSE_KERNELS_TABLE;
+  }
+}
 
 int rse_codec_matrix(const rse_codec* c, uint8_t* out, size_t out_bytes) {
   if (!c || !out) return RSE_ERR_INVALID_ARGUMENT;
@@ -762,6 +795,7 @@ int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t 
   std::vector<uint8_t*> out(c->p);
   for (size_t i = 0; i < c->k; ++i) in[i] = base + i * sb;
   for (size_t r = 0; r < c->p; ++r) out[r] = base + (c->k + r) * sb;
+  want_bitslice(c, sb);
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
         (uint64_t)c->total * sb, n_stripes};
@@ -909,6 +943,7 @@ int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& st
   if (e == hipSuccess) e = hipEventRecord(start, user);  // everything starts after the caller's work
   for (auto& q : st)
     if (e == hipSuccess) e = hipStreamWaitEvent(q, start, 0);
+  want_bitslice(c, chunk);
   const Rows rows = parity_rows(c);
   std::vector<const uint8_t*> in(c->k);
   std::vector<uint8_t*> out(c->p);

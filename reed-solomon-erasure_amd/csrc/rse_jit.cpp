@@ -1,0 +1,346 @@
+// rse_jit.cpp -- run-time specialisation of the bit-sliced kernels for codecs
+// that are not compiled into the library.
+//
+// The bit-sliced kernels (rse_bitslice_core.hpp) are fastest because every
+// coefficient's 8x8 / 16x16 bit matrix is a compile-time constant: the
+// multiply-accumulate becomes straight-line v_bitop3 XOR networks.  The
+// encoding matrix of ReedSolomon::new (core.rs:430-436) depends only on the
+// field and (k, p), so when a codec is created its parity rows are known and a
+// module can be built for them: this file turns the rows into the constant
+// plane-selection table the kernels take (the same algebra as the constexpr
+// Planes of rse_bitslice.hip), appends it and the kernel entry points to the
+// device source of rse_bitslice_core.hpp (embedded at build time), and
+// compiles that for gfx950 with hiprtc on a background thread.  hiprtc runs on
+// the host CPU only; the code object is loaded on a device the first time a
+// launch there needs it.  Until the module is ready the table kernels serve the
+// codec (RSE_OPT_JIT 1), or the first launch waits for it (RSE_OPT_JIT 2).
+// Which kernel runs never changes a result.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <cstdio>
+#include <cstdlib>
+#include <future>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "rse_field.hpp"
+#include "rse_kernels.hpp"
+
+namespace rse {
+namespace {
+
+// rse_kernels.hpp + rse_device.hpp + rse_bitslice_core.hpp, concatenated with
+// their #include "..." lines removed (Makefile: build/rse_jit_src.inc).
+const char kJitSource[] =
+#include "rse_jit_src.inc"
+    ;
+
+struct Compiled {
+  bool ok = false;
+  std::string code;  // gfx950 code object
+  std::string log;
+  double ms = 0;
+};
+
+// Two modules per codec, built in this order: the encode/verify kernel
+// (needed first, ~2 s of hiprtc), then the reconstruct kernels (~8 s).
+enum Stage { kEnc = 0, kRec = 1 };
+
+struct Entry {
+  int field = 0;
+  uint32_t k = 0, p = 0;
+  std::vector<uint16_t> rows;  // p x k parity rows
+  std::promise<std::shared_ptr<const Compiled>> promise[2];
+  std::shared_future<std::shared_ptr<const Compiled>> built[2];
+  std::mutex mu;  // guards loaded
+  struct Loaded {
+    int dev;
+    bool have_rec = false;
+    JitFns fns;
+  };
+  std::vector<Loaded> loaded;
+};
+
+std::mutex g_mu;  // guards the registry and the job queues
+std::condition_variable g_cv;
+std::deque<Entry*> g_jobs[2];  // per stage; every encode job runs before any reconstruct job
+std::atomic<int64_t> g_built{0};
+
+std::vector<std::unique_ptr<Entry>>& registry() {
+  static std::vector<std::unique_ptr<Entry>> v;
+  return v;
+}
+
+Entry* find_entry(int field, uint32_t k, uint32_t p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& e : registry())
+    if (e->field == field && e->k == k && e->p == p) return e.get();
+  return nullptr;
+}
+
+// Sigma-row counts of the reconstruct kernels: 1, 2, 4, 8 up to p, and p.
+int recon_ns(uint32_t p, int* ns) {
+  int n = 0;
+  for (int v : {1, 2, 4, 8})
+    if ((uint32_t)v <= p) ns[n++] = v;
+  if (ns[n - 1] != (int)p) ns[n++] = (int)p;
+  return n;
+}
+
+// The device source of one codec: the shared kernel code, the codec's
+// plane-selection table, and extern "C" entry points.
+std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
+                        int stage) {
+  const int np = field == 16 ? 16 : 8;
+  auto bit = [&](int q) { return field == 16 ? (q ^ 8) : q; };
+  auto mul = [&](uint16_t a, uint16_t b) {
+    return field == 16 ? Gf16Field::mul(a, b) : Gf8Field::mul(a, b);
+  };
+  std::string s;
+  s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * np);
+  // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
+  // types in __hip_internal
+  s += "#define RSE_JIT 1\n"
+       "using __hip_internal::uint8_t;\nusing __hip_internal::uint16_t;\n"
+       "using __hip_internal::uint32_t;\nusing __hip_internal::uint64_t;\n"
+       "using __hip_internal::int32_t;\n";
+  s += kJitSource;
+  char buf[512];
+  std::snprintf(buf, sizeof buf,
+                "\nnamespace rse {\nnamespace {\n"
+                "struct JitPlanes {\n  uint16_t sel[%u][%u][%d];\n};\n"
+                "struct JitCode {\n  using Field = %s;\n"
+                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d;\n"
+                "  static constexpr JitPlanes planes = {{",
+                p, k, np, field == 16 ? "BitsF16" : "BitsF8", k, p, np, 16 / np);
+  s += buf;
+  // sel[o][i][q]: bit j set iff input plane j feeds output plane q -- column j
+  // of the bit matrix of rows[o][i] is rows[o][i] * (the element with only
+  // plane j's bit set)
+  for (uint32_t o = 0; o < p; ++o) {
+    s += "{";
+    for (uint32_t i = 0; i < k; ++i) {
+      uint16_t sel[16] = {};
+      for (int j = 0; j < np; ++j) {
+        const uint16_t col = mul(rows[o * k + i], (uint16_t)(1u << bit(j)));
+        for (int q = 0; q < np; ++q)
+          if ((col >> bit(q)) & 1u) sel[q] |= (uint16_t)(1u << j);
+      }
+      s += "{";
+      for (int q = 0; q < np; ++q) {
+        std::snprintf(buf, sizeof buf, "%u,", (unsigned)sel[q]);
+        s += buf;
+      }
+      s += "},";
+    }
+    s += "},";
+  }
+  s += "}};\n};\n}  // namespace\n}  // namespace rse\n";
+  if (stage == kEnc) {
+    std::snprintf(buf, sizeof buf,
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode(\n"
+                  "    const rse::CodeArgs a, uint64_t cps) {\n"
+                  "  rse::bitslice_body<rse::JitCode, true, true, false>(a, cps);\n}\n",
+                  p > 4 ? 2 : 3);
+    s += buf;
+    return s;
+  }
+  int ns[5];
+  const int n = recon_ns(p, ns);
+  for (int q = 0; q < n; ++q) {
+    std::snprintf(buf, sizeof buf,
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
+                  "    const rse::BsReconArgs a, uint64_t cps) {\n"
+                  "  rse::bitslice_recon_body<rse::JitCode, true, %d>(a, cps);\n}\n",
+                  ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
+    s += buf;
+  }
+  return s;
+}
+
+std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
+  auto out = std::make_shared<Compiled>();
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage);
+  const auto t0 = std::chrono::steady_clock::now();
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rse_jit.hip", 0, nullptr, nullptr) !=
+      HIPRTC_SUCCESS) {
+    out->log = "hiprtcCreateProgram failed";
+    return out;
+  }
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  size_t n = 0;
+  if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
+    out->log.assign(n, '\0');
+    hiprtcGetProgramLog(prog, &out->log[0]);
+  }
+  if (r == HIPRTC_SUCCESS && hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0) {
+    out->code.assign(n, '\0');
+    out->ok = hiprtcGetCode(prog, &out->code[0]) == HIPRTC_SUCCESS;
+  }
+  hiprtcDestroyProgram(&prog);
+  out->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (const char* dir = std::getenv("RSE_JIT_DUMP")) {  // debugging aid
+    char path[1024];
+    std::snprintf(path, sizeof path, "%s/rse_jit_gf%d_%u_%u_%s.hip", dir, e.field, e.k, e.p,
+                  stage == kEnc ? "encode" : "reconstruct");
+    if (FILE* f = std::fopen(path, "w")) {
+      std::fputs(src.c_str(), f);
+      std::fprintf(f, "\n/* %s, %.0f ms\n%s\n*/\n", out->ok ? "ok" : "FAILED", out->ms,
+                   out->log.c_str());
+      std::fclose(f);
+    }
+  }
+  if (out->ok) ++g_built;
+  return out;
+}
+
+// One background compiler thread, started with the first registration and
+// joined when the library is unloaded (a compile in flight finishes first; jobs
+// still queued then are completed as failed so nothing waits forever).
+class Worker {
+ public:
+  void start() {
+    if (!th_.joinable()) th_ = std::thread([this] { run(); });
+  }
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      stop_ = true;
+    }
+    g_cv.notify_all();
+    if (th_.joinable()) th_.join();
+    for (auto& q : g_jobs)
+      for (Entry* e : q) e->promise[&q - g_jobs].set_value(std::make_shared<Compiled>());
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      Entry* e = nullptr;
+      int stage = 0;
+      {
+        std::unique_lock<std::mutex> g(g_mu);
+        g_cv.wait(g, [&] { return stop_ || !g_jobs[kEnc].empty() || !g_jobs[kRec].empty(); });
+        if (stop_) return;
+        stage = g_jobs[kEnc].empty() ? kRec : kEnc;
+        e = g_jobs[stage].front();
+        g_jobs[stage].pop_front();
+      }
+      e->promise[stage].set_value(compile(*e, stage));
+    }
+  }
+  std::thread th_;
+  bool stop_ = false;
+};
+
+Worker& worker() {
+  static Worker w;  // constructed after registry(): destroyed (joined) before it
+  return w;
+}
+
+}  // namespace
+
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
+  if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || k > (uint32_t)kMaxIn ||
+      p == 0 || p > kJitMaxOut || bitslice_compiled(field, k, p))
+    return 0;
+  registry();
+  Worker& w = worker();
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& e : registry())
+    if (e->field == field && e->k == k && e->p == p) return 1;
+  auto e = std::make_unique<Entry>();
+  e->field = field;
+  e->k = k;
+  e->p = p;
+  e->rows.assign(rows, rows + (size_t)k * p);
+  for (int st = 0; st < 2; ++st) {
+    e->built[st] = e->promise[st].get_future().share();
+    g_jobs[st].push_back(e.get());
+  }
+  registry().push_back(std::move(e));
+  w.start();
+  g_cv.notify_all();
+  return 1;
+}
+
+int jit_status(int field, uint32_t k, uint32_t p, bool wait) {
+  Entry* e = find_entry(field, k, p);
+  if (!e) return 0;
+  for (auto& b : e->built) {
+    if (wait) b.wait();
+    else if (b.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 1;
+  }
+  return e->built[kEnc].get()->ok && e->built[kRec].get()->ok ? 2 : -1;
+}
+
+bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
+              JitFns* out, hipError_t* err) {
+  *err = hipSuccess;
+  const int64_t mode = get_option(9);
+  if (mode == 0 || p > kJitMaxOut) return false;
+  Entry* e = find_entry(field, k, p);
+  if (!e) return false;
+  for (uint32_t o = 0; o < p; ++o)
+    for (uint32_t i = 0; i < k; ++i)
+      if (rows[o * stride + i] != e->rows[o * k + i]) return false;
+  auto& b = e->built[stage];
+  if (mode >= 2) b.wait();
+  else if (b.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;
+  const std::shared_ptr<const Compiled> c = b.get();
+  if (!c->ok) return false;
+  int dev = 0;
+  hipError_t he = hipGetDevice(&dev);
+  if (he != hipSuccess) {
+    *err = he;
+    return false;
+  }
+  std::lock_guard<std::mutex> g(e->mu);
+  Entry::Loaded* l = nullptr;
+  for (auto& d : e->loaded)
+    if (d.dev == dev) l = &d;
+  if (!l) {
+    e->loaded.push_back(Entry::Loaded{dev});
+    l = &e->loaded.back();
+  }
+  const bool have = stage == kEnc ? l->fns.enc != nullptr : l->have_rec;
+  if (!have) {  // load this stage's module on this device; it stays loaded
+    hipModule_t m = nullptr;
+    he = hipModuleLoadData(&m, c->code.data());
+    JitFns f = l->fns;
+    if (stage == kEnc) {
+      if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
+    } else {
+      f.n_rec = recon_ns(p, f.rec_ns);
+      for (int q = 0; q < f.n_rec && he == hipSuccess; ++q) {
+        char name[32];
+        std::snprintf(name, sizeof name, "rse_jit_recon%d", f.rec_ns[q]);
+        he = hipModuleGetFunction(&f.rec[q], m, name);
+      }
+    }
+    if (he != hipSuccess) {
+      if (m) (void)hipModuleUnload(m);
+      *err = he;
+      return false;
+    }
+    l->fns = f;
+    if (stage == kRec) l->have_rec = true;
+  }
+  *out = l->fns;
+  return true;
+}
+
+int64_t jit_modules_built() { return g_built.load(); }
+
+}  // namespace rse

@@ -752,6 +752,7 @@ struct Options {
   int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
   int64_t host_chunk_kib = 4096;  // host pipeline chunk per shard (rse_encode_host*)
   int64_t host_h2d_streams = 2;   // host pipeline H2D streams (tools/host_e2e.py)
+  int64_t jit = 1;                // run-time specialised bit-sliced kernels (rse_jit.cpp)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1079,6 +1080,7 @@ int set_option(int key, int64_t value) {
     case 5: g_opt.bitslice = value ? 1 : 0; return 0;
     case 7: g_opt.host_chunk_kib = value < 64 ? 64 : value; return 0;
     case 8: g_opt.host_h2d_streams = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
+    case 9: g_opt.jit = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     default: return -1;
   }
 }
@@ -1095,6 +1097,8 @@ int64_t get_option(int key) {
     case 6: return g_bs_launches;
     case 7: return g_opt.host_chunk_kib;
     case 8: return g_opt.host_h2d_streams;
+    case 9: return g_opt.jit;
+    case 10: return jit_modules_built();
     default: return -1;
   }
 }

@@ -1,5 +1,6 @@
 // rse_kernels.hpp -- internal launch interface between the host codec
-// (rse_codec.cpp) and the CDNA4 kernels (rse_kernels.hip).
+// (rse_codec.cpp) and the CDNA4 kernels (rse_kernels.hip, rse_bitslice.hip,
+// and the run-time specialised modules of rse_jit.cpp).
 //
 // One fused kernel family replaces the reference's whole code_some_slices
 // (core.rs:481-509): every input shard byte is read once from HBM, every output
@@ -7,11 +8,16 @@
 // in VGPRs.  The same launch also serves check_some_slices_with_buffer
 // (core.rs:511-532) through the CHECK modes, so verify never round-trips parity
 // through HBM twice.
+//
+// The argument blocks below are also compiled by hiprtc (RSE_JIT defined): that
+// part must stay free of host-only headers and declarations.
 #pragma once
 
+#ifndef RSE_JIT
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 namespace rse {
 
@@ -43,6 +49,30 @@ struct CodeArgs {
   uint16_t coef[kMaxOut][kMaxIn];
 };
 
+// Bit-sliced syndrome reconstruct for codecs with bit-sliced kernels
+// (rse_bitslice.hip, rse_jit.cpp).  With P the codec's parity rows, S the e
+// missing data shards and R e present parity rows:
+//   sigma_r = sum over present data d of P[r][d] * shard_d   (XOR networks)
+//   syndrome s_r = sigma_r ^ parity_r for r in R
+//   output o = (out_sigma[o] >= 0 ? sigma_{out_sigma[o]} : 0)
+//              ^ sum over r in R of w[o][r] * s_r
+// (missing data: w = rows of (P[R][S])^-1; missing parity r: out_sigma = r,
+// w = P[r][S] (P[R][S])^-1).  One pass over k surviving shards.
+struct BsReconArgs {
+  const uint8_t* data[kMaxIn];    // data shard d (read when present)
+  const uint8_t* par[kMaxOut];    // parity shard r (read when a syndrome row)
+  uint8_t* out[kMaxOut];          // output o
+  uint64_t stripe_stride;
+  uint32_t n_stripes;
+  uint32_t present;               // bit d: data shard d present
+  uint32_t sigma;                 // bit r: sigma_r is needed
+  uint32_t synd;                  // bit r: parity row r is a syndrome row (R)
+  uint32_t n_out;
+  int32_t out_sigma[kMaxOut];     // sigma row XORed into output o, -1 for none
+  uint16_t w[kMaxOut][kMaxOut];   // [o][r], zero unless r is in R
+};
+
+#ifndef RSE_JIT
 // Launch the fused coding kernel over args.n_stripes stripes on `stream`.
 // field is 8 or 16.  Returns a hipError_t.
 hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
@@ -61,38 +91,48 @@ hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present,
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
 
 // Bit-sliced kernels (rse_bitslice.hip) for codecs whose parity rows are
-// compiled in: sets *handled when it launched (whole 16 KiB chunks of every
-// shard only -- the caller codes the rest).
+// compiled in or were specialised at run time (rse_jit.cpp): sets *handled when
+// it launched (whole 16 KiB chunks of every shard only -- the caller codes the
+// rest).
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                            hipStream_t stream, bool* handled);
 uint64_t bitslice_chunk_bytes();
+// 1 if (field, k, p) has bit-sliced kernels compiled into the library.
+int bitslice_compiled(int field, uint32_t k, uint32_t p);
 
-// Bit-sliced syndrome reconstruct for compiled codecs (rse_bitslice.hip).
-// With P the compiled parity rows, S the e missing data shards and R e
-// present parity rows:  sigma_r = sum over present data d of P[r][d] * shard_d
-// (compile-time XOR networks), syndrome s_r = sigma_r ^ parity_r for r in R,
-// and every output o = (out_sigma[o] >= 0 ? sigma_{out_sigma[o]} : 0)
-//                      ^ sum over r in R of w[o][r] * s_r
-// (missing data: w = rows of (P[R][S])^-1; missing parity r: out_sigma = r,
-// w = P[r][S] (P[R][S])^-1).  One pass over k surviving shards.
-struct BsReconArgs {
-  const uint8_t* data[kMaxIn];    // data shard d (read when present)
-  const uint8_t* par[kMaxOut];    // parity shard r (read when a syndrome row)
-  uint8_t* out[kMaxOut];          // output o
-  uint64_t stripe_stride;
-  uint32_t n_stripes;
-  uint32_t present;               // bit d: data shard d present
-  uint32_t sigma;                 // bit r: sigma_r is needed
-  uint32_t synd;                  // bit r: parity row r is a syndrome row (R)
-  uint32_t n_out;
-  int32_t out_sigma[kMaxOut];     // sigma row XORed into output o, -1 for none
-  uint16_t w[kMaxOut][kMaxOut];   // [o][r], zero unless r is in R
-};
 // parity_rows: the codec's p x k parity rows (row-major); must equal the
-// compiled ones for *handled to be set.  n_vec: 16-byte vectors per shard.
+// compiled (or run-time specialised) ones for *handled to be set.  n_vec:
+// 16-byte vectors per shard.
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
                                  bool* handled);
+
+// ---- run-time specialisation (rse_jit.cpp) ----------------------------------
+// Bit-sliced kernels for codecs not compiled into the library: the XOR networks
+// of the codec's parity rows are generated as source and compiled for gfx950
+// with hiprtc (host CPU only; no device work), then loaded per device on first
+// use.  Results never depend on which kernel runs.
+constexpr uint32_t kJitMaxOut = 8;  // p' <= 8: 16 x p' accumulator VGPRs
+// Registers the rows and starts the compile on a background thread (no-op if
+// already registered or not eligible).  Returns 1 if eligible.
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows);
+// 2 ready, 1 compiling, 0 not registered / not eligible, -1 compile failed.
+// wait != 0 blocks until the compile has finished.
+int jit_status(int field, uint32_t k, uint32_t p, bool wait);
+struct JitFns {
+  hipFunction_t enc = nullptr;  // bitslice encode/verify (CodeArgs, chunks per stripe)
+  int n_rec = 0;
+  int rec_ns[5] = {};           // sigma rows of rec[i], ascending
+  hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
+};
+// Kernels of `stage` (0: encode/verify, 1: reconstruct) for a launch whose
+// coefficients rows[o * stride + i] equal a registered codec's parity rows,
+// loaded on the current device.  Returns false (and *err = hipSuccess) if there
+// are none (yet: RSE_OPT_JIT 1 does not wait for a compile in flight, 2 does);
+// *err is set on a module-load failure.
+bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
+              JitFns* out, hipError_t* err);
+int64_t jit_modules_built();  // RSE_OPT_JIT_MODULES
 
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
 int set_option(int key, int64_t value);
@@ -109,5 +149,6 @@ hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed,
 // singular[b] receives 1 for a singular matrix.
 hipError_t launch_gf8_invert(const uint8_t* in, uint8_t* out, uint32_t* singular,
                              uint32_t n, uint32_t batch, hipStream_t stream);
+#endif  // RSE_JIT
 
 }  // namespace rse

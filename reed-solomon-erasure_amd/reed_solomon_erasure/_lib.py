@@ -16,7 +16,7 @@ EXPORTS = (
     "rse_strerror", "rse_last_device_error", "rse_version",
     "rse_codec_new", "rse_codec_free", "rse_codec_field",
     "rse_codec_data_shard_count", "rse_codec_parity_shard_count",
-    "rse_codec_total_shard_count", "rse_codec_matrix",
+    "rse_codec_total_shard_count", "rse_codec_matrix", "rse_codec_kernel_kind",
     "rse_encode", "rse_encode_sep", "rse_encode_single", "rse_encode_single_sep",
     "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
     "rse_encode_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
@@ -43,6 +43,7 @@ _SIGS = {
     "rse_codec_parity_shard_count": (_sz, [_vp]),
     "rse_codec_total_shard_count": (_sz, [_vp]),
     "rse_codec_matrix": (_c.c_int, [_vp, _u8p, _sz]),
+    "rse_codec_kernel_kind": (_c.c_int, [_vp, _c.c_int]),
     "rse_encode": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
     "rse_encode_sep": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _vp]),
     "rse_encode_single": (_c.c_int, [_vp, _sz, _vp, _szp, _sz, _vp]),

@@ -118,6 +118,18 @@ class ReedSolomon:
     def total_shard_count(self) -> int:
         return self._k + self._p
 
+    # rse_codec_kernel_kind values (include/rse_hip.h); no reference counterpart
+    KERNELS = {0: "table", 1: "bitslice-compiled", 2: "bitslice-specialised",
+               3: "specialising", 4: "specialise-failed"}
+
+    def kernel_kind(self, wait: bool = False) -> str:
+        """Which kernels code this codec (results are identical either way):
+        bit-sliced kernels compiled into the library, bit-sliced kernels
+        specialised for this codec at run time (hiprtc, started by the
+        constructor; ``wait`` blocks until that build has finished), or the
+        table kernels."""
+        return self.KERNELS[_lib.rse_codec_kernel_kind(self._h, 1 if wait else 0)]
+
     def matrix(self) -> "list":
         """The (k+p) x k systematic encoding matrix (core.rs:430-436) as nested
         lists of ints (GF(2^16): (coef_of_x << 8) | constant)."""

@@ -175,3 +175,25 @@ def test_null_arguments_are_rejected():
     assert L.rse_encode(None, ptrs(2), lens([1, 1]), 2, None) == 100
     assert L.rse_code_shards(8, None, 1, 1, ptrs(1), ptrs(1), 1, 0, None) == 100
     assert L.rse_gf8_invert_batch(None, None, None, 3, 1, None) == 100
+
+
+def test_run_time_specialisation_builds_on_cpu():
+    """Codecs that are not compiled in (p <= 8, k <= 32) get bit-sliced kernels
+    built by hiprtc at run time, requested by the first chunk-sized call or by
+    kernel_kind(wait=True); the build is host-only, so it runs here without a
+    GPU.  Compiled-in codecs and ineligible ones report so."""
+    assert R.galois_8.ReedSolomon(10, 4).kernel_kind() == "bitslice-compiled"
+    assert R.galois_16.ReedSolomon(20, 8).kernel_kind() == "bitslice-compiled"
+    assert R.galois_8.ReedSolomon(50, 20).kernel_kind() == "table"   # p > 8
+    assert R.galois_8.ReedSolomon(33, 4).kernel_kind() == "table"    # k > 32
+    built = L.rse_get_option(10)
+    r = R.galois_8.ReedSolomon(12, 4)
+    assert r.kernel_kind(wait=True) == "bitslice-specialised"
+    assert L.rse_get_option(10) >= built + 2  # encode module + reconstruct module
+    assert R.galois_8.ReedSolomon(12, 4).kernel_kind() == "bitslice-specialised"  # cached
+    old = L.rse_get_option(9)
+    try:
+        assert L.rse_set_option(9, 0) == 0  # off: new codecs stay on the table kernels
+        assert R.galois_8.ReedSolomon(7, 2).kernel_kind(wait=True) == "table"
+    finally:
+        L.rse_set_option(9, old)

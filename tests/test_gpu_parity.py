@@ -636,6 +636,79 @@ def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
             assert (got[s_, i] == full[i]).all(), (s_, i)
 
 
+JIT_CODECS = [(8, 12, 4), (8, 6, 3), (8, 4, 2), (8, 32, 8), (8, 1, 1), (8, 17, 5),
+              (16, 10, 4), (16, 4, 2), (16, 6, 7)]
+
+
+@pytest.mark.parametrize("field,k,p", JIT_CODECS)
+def test_run_time_specialised_bitslice(R, field, k, p):
+    """Codecs without compiled-in bit-sliced kernels get them specialised at
+    run time (hiprtc, rse_jit.cpp).  With RSE_OPT_JIT 2 the first launch waits
+    for the build, so every call below runs the specialised kernels (checked
+    with the bit-sliced launch counter): encode, verify (clean and corrupted),
+    reconstruct / reconstruct_data at every erasure count 1..p, and flat
+    multi-stripe encode, all against the oracle."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 2 * 16384 + 48 * es
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(field * 1000 + k * 10 + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    old = lib.rse_get_option(9)
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        r = R.core.ReedSolomon(k, p, field)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        t = [dev(x).reshape(shape) for x in full[:k]] + \
+            [torch.full(shape, 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        n0 = lib.rse_get_option(6)
+        r.encode(t)
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(6) - n0 == 1
+        for i in range(p):
+            assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
+        assert r.verify(t)
+        t[k + p - 1].view(-1)[nbytes - 1] ^= 1  # in the table-coded tail
+        assert not r.verify(t)
+        t[k + p - 1].view(-1)[nbytes - 1] ^= 1
+        t[0].view(-1)[100] ^= 0x80  # in a bit-sliced chunk
+        assert not r.verify(t)
+        t[0].view(-1)[100] ^= 0x80
+        patterns = [sorted(rng.choice(k + p, ne, replace=False).tolist()) for ne in range(1, p + 1)]
+        patterns += [list(range(min(p, k))), list(range(k, k + p))]
+        for erased in patterns:
+            present = [i not in erased for i in range(k + p)]
+            for data_only in (False, True):
+                tb = [dev(x).reshape(shape) for x in full]
+                for e in erased:
+                    tb[e].fill_(0x33)
+                n0 = lib.rse_get_option(6)
+                (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+                torch.cuda.synchronize()
+                if not (data_only and all(e >= k for e in erased)):
+                    assert lib.rse_get_option(6) - n0 == 1, (erased, data_only)
+                for i in range(k + p):
+                    got = host(tb[i]).reshape(-1)
+                    if data_only and i >= k and i in erased:
+                        assert (got == 0x33).all()
+                    else:
+                        assert (got == full[i]).all(), (erased, data_only, i)
+        stripes = 3
+        buf = np.concatenate([np.concatenate(full)] * stripes)
+        d = dev(buf)
+        d.view(stripes, k + p, nbytes)[:, k:].fill_(0)
+        n0 = lib.rse_get_option(6)
+        r.encode_flat(d, n_elems, stripes)
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(6) - n0 == 1
+        assert (host(d) == buf).all()
+    finally:
+        lib.rse_set_option(9, old)
+
+
 def test_encode_host_matches_device(R):
     rng = np.random.default_rng(23)
     k, p = 10, 4

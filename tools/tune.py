@@ -46,6 +46,9 @@ def main():
         for i in range(k):
             fill_splitmix(v[s, i], 1, (s << 8) | i)
     r = R.core.ReedSolomon(k, p, args.field)
+    # codecs without compiled-in bit-sliced kernels: let the run-time
+    # specialisation (rse_jit.cpp) finish before timing
+    print(f"kernels: {r.kernel_kind(wait=True)}", flush=True)
     elems = L // (args.field // 8)
     erased = [int(x) for x in args.erase.split(",")]
     present = [i not in erased for i in range(k + p)]
