@@ -312,6 +312,11 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
+def R_lib():
+    import reed_solomon_erasure as R
+    return R._lib.load()
+
+
 def extra_legs(r, v, k, p, L, n_stripes, stream):
     """Reconstruct (data shards 0 and 1 erased, BASELINE config 3) and the
     pinned-host end-to-end encode (PCIe-inclusive; never `value`)."""
@@ -330,9 +335,32 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
     rb = n_stripes * (k + 2) * L
-    out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased",
+    out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased, first uses of the "
+                                  "pattern (bit-sliced syndrome kernel)",
                           "stripes": n_stripes, "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
                           "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
+    # a repeated pattern: its decode rows get their own specialised kernel
+    # (rse_jit.cpp), like the reference's decode-matrix cache (core.rs:697-731);
+    # RSE_OPT_JIT 2 waits for that build before timing
+    lib = R_lib()
+    old = lib.rse_get_option(9)
+    lib.rse_set_option(9, 2)
+    p0 = lib.rse_get_option(12)
+    r.reconstruct_data_flat(flat, L, n_stripes, present)
+    torch.cuda.synchronize()
+    a.record(stream)
+    for _ in range(reps):
+        r.reconstruct_data_flat(flat, L, n_stripes, present)
+    b.record(stream)
+    torch.cuda.synchronize()
+    lib.rse_set_option(9, old)
+    ms = a.elapsed_time(b) / reps
+    out["reconstruct_cached_pattern"] = {
+        "what": "reconstruct_data, data shards 0,1 erased, repeated pattern (decode-pattern "
+                "kernel specialised at run time)", "stripes": n_stripes,
+        "pattern_kernel": lib.rse_get_option(12) - p0 == reps + 1,
+        "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
+        "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
     # verify (check mode: k+p reads, no writes), stripe by stripe as the API is
     shards = [[v[s_, i] for i in range(k + p)] for s_ in range(n_stripes)]
     assert all(r.verify(sh) for sh in shards[:2])

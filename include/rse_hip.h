@@ -194,6 +194,10 @@ int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len
 #define RSE_OPT_JIT 9               /* run-time specialised kernels: 0 off, 1 used once built
                                        (default), 2 the first launch waits for the build */
 #define RSE_OPT_JIT_MODULES 10      /* read-only: specialised modules built in this process */
+#define RSE_OPT_JIT_PATTERNS 11     /* 1: decode patterns used twice get their own specialised
+                                       kernel (reconstruct at encode speed); 0 off */
+#define RSE_OPT_PATTERN_LAUNCHES 12 /* read-only, per thread: reconstructs that ran on a
+                                       decode-pattern kernel */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

@@ -154,6 +154,12 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
   bitslice_body<C, NT, SB, XC>(a, chunks_per_stripe);
 }
 
+template <class C, int D>
+__global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_deep_kernel(
+    const CodeArgs a, uint64_t chunks_per_stripe) {
+  bitslice_body_deep<C, true, D>(a, chunks_per_stripe);
+}
+
 // ----------------------------------------------- LDS-DMA input ring variant
 // The same kernel with the shard loads issued as global_load_lds_dwordx4
 // (LDS-DMA, no VGPR destination) into a per-wave ring of D input slots, D - 1
@@ -274,8 +280,9 @@ struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
-  BsFn fn[5][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
-                      // prefetch, 3/4 LDS-DMA input ring of 3/2 slots (nt only)
+  BsFn fn[7][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
+                      // prefetch, 3/4 LDS-DMA input ring of 3/2 slots, 5/6 two/three
+                      // inputs in flight in VGPRs (3-6: nt only)
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
 };
 
@@ -291,7 +298,9 @@ constexpr BsRecFn rec_fn() {
     {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false>},                 \
     {nullptr, bitslice_kernel<Code<F, K, P>, true, true, true>},                  \
     {nullptr, bitslice_dma_kernel<Code<F, K, P>, 3>},                             \
-    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 2>}},                            \
+    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 2>},                             \
+    {nullptr, bitslice_deep_kernel<Code<F, K, P>, 2>},                            \
+    {nullptr, bitslice_deep_kernel<Code<F, K, P>, 3>}},                           \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
@@ -314,12 +323,13 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
   for (const BsShape& sh : kBsShapes) {
     if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
-    for (uint32_t o = 0; o < sh.p; ++o)
-      for (uint32_t i = 0; i < sh.k; ++i)
-        if (a.coef[o][i] != sh.m[o * sh.k + i]) return hipSuccess;
+    bool same = true;  // other rows of this shape (a decode pattern) may be specialised
+    for (uint32_t o = 0; o < sh.p && same; ++o)
+      for (uint32_t i = 0; i < sh.k && same; ++i) same = a.coef[o][i] == sh.m[o * sh.k + i];
+    if (!same) break;
     // RSE_OPT_KERNEL_VARIANT picks a bit-sliced variant too (-1: default)
     const int64_t vopt = get_option(4);
-    int v = (vopt >= 0 && vopt < 5) ? (int)vopt : kBsDefaultVariant;
+    int v = (vopt >= 0 && vopt < 7) ? (int)vopt : kBsDefaultVariant;
     BsFn fn = sh.fn[v][nt ? 1 : 0];
     if (!fn) fn = sh.fn[v][1];
     hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);

@@ -250,6 +250,45 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }
 
+// Inputs I.. of one chunk with D inputs in flight: input I + D is loaded
+// before input I is coded (buf is a ring of D + 1 input slots, indexed at
+// compile time so it stays in VGPRs).
+template <class C, bool NT, int D, int I>
+__device__ __forceinline__ void code_inputs_deep(uint32_t (&acc)[C::p * 16],
+                                                 u32x4 (&buf)[D + 1][4], const CodeArgs& a,
+                                                 uint64_t off) {
+  if constexpr (I < C::k) {
+    if constexpr (I + D < C::k) load4<NT>(buf[(I + D) % (D + 1)], a.in[I + D] + off);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t pl[16];
+    slice<typename C::Field>(buf[I % (D + 1)], pl);
+    mac_input<C, I>(acc, pl, make_int_seq<C::p * 16>{});
+#pragma unroll
+    for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+    code_inputs_deep<C, NT, D, I + 1>(acc, buf, a, off);
+  }
+}
+
+// bitslice_body with D inputs in flight per lane instead of one.
+template <class C, bool NT, int D>
+__device__ __forceinline__ void bitslice_body_deep(const CodeArgs& a, uint64_t chunks_per_stripe) {
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint32_t mode = a.mode;
+  bool diff = false;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+    uint32_t acc[C::p * 16];
+    u32x4 buf[D + 1][4];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (j < C::k) load4<NT>(buf[j], a.in[j] + off);
+    code_inputs_deep<C, NT, D, 0>(acc, buf, a, off);
+    store_outputs<C, NT>(acc, a, off, mode, diff);
+  }
+  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+}
+
 // ------------------------------------------------------------ reconstruct
 // Bit-sliced syndrome reconstruct (BsReconArgs in rse_kernels.hpp).  The input
 // sequence is the present data shards, then the syndrome parity shards; the

@@ -63,7 +63,11 @@ struct rse_codec {
   rse::Matrix<rse::Gf16Field> m16;  // field == 16
   // decode-matrix LRU keyed by invalid indices (core.rs:697-731)
   mutable std::mutex mu;
-  mutable std::list<std::pair<std::vector<size_t>, std::vector<uint16_t>>> lru;
+  struct Cached {
+    std::vector<uint16_t> dec;  // k x k inverse of the valid rows
+    uint32_t uses = 0;          // reconstructs that used this pattern (run-time kernels)
+  };
+  mutable std::list<std::pair<std::vector<size_t>, Cached>> lru;
   mutable std::map<std::vector<size_t>, decltype(lru)::iterator> index;
   // run-time specialisation requested (rse_jit.cpp; see want_bitslice)
   mutable std::atomic<bool> jit_requested{false};
@@ -267,7 +271,7 @@ void want_bitslice(const rse_codec* c, size_t len_bytes) {
       c->p > rse::kJitMaxOut)
     return;
   const Rows rows = parity_rows(c);
-  rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data());
+  rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), true);
 }
 
 Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, core.rs:492-509
@@ -280,17 +284,21 @@ Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, c
 }
 
 // core.rs:697-731: k x k inverse of the valid rows, cached by invalid indices.
+// *uses: how many reconstructs (this one included) used the pattern while cached.
 int decode_matrix(const rse_codec* c, const std::vector<size_t>& valid,
-                  const std::vector<size_t>& invalid, std::vector<uint16_t>& out) {
+                  const std::vector<size_t>& invalid, std::vector<uint16_t>& out,
+                  uint32_t* uses) {
   {
     std::lock_guard<std::mutex> g(c->mu);
     auto it = c->index.find(invalid);
     if (it != c->index.end()) {
       c->lru.splice(c->lru.begin(), c->lru, it->second);
-      out = it->second->second;
+      out = it->second->second.dec;
+      *uses = ++it->second->second.uses;
       return RSE_OK;
     }
   }
+  *uses = 1;
   const size_t k = c->k;
   bool ok;
   if (c->field == 16) {
@@ -309,7 +317,7 @@ int decode_matrix(const rse_codec* c, const std::vector<size_t>& valid,
   if (!ok) return RSE_ERR_SINGULAR_MATRIX;  // unreachable for an MDS code
   std::lock_guard<std::mutex> g(c->mu);
   if (c->index.find(invalid) == c->index.end()) {
-    c->lru.emplace_front(invalid, out);
+    c->lru.emplace_front(invalid, rse_codec::Cached{out, 1});
     c->index[invalid] = c->lru.begin();
     if (c->lru.size() > kCacheCapacity) {
       c->index.erase(c->lru.back().first);
@@ -327,6 +335,7 @@ struct ReconPlan {
   Rows rows;
   size_t len = 0;  // elements
   bool nothing_to_do = false;
+  uint32_t pattern_uses = 0;  // decode_matrix *uses
 };
 
 int plan_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens,
@@ -375,7 +384,7 @@ int plan_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens
     if (!shards[v]) return RSE_ERR_INVALID_ARGUMENT;
 
   std::vector<uint16_t> dec;
-  rc = decode_matrix(c, valid, invalid, dec);
+  rc = decode_matrix(c, valid, invalid, dec, &plan.pattern_uses);
   if (rc) return rc;
 
   // Coefficients that rebuild data shard j from the k valid inputs:
@@ -532,6 +541,25 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
   return RSE_OK;
 }
 
+thread_local int64_t g_pattern_launches = 0;  // RSE_OPT_PATTERN_LAUNCHES
+
+// Decode patterns used more than once (the decode-matrix LRU of
+// core.rs:697-731 counts them) get a bit-sliced kernel built at run time for
+// the plan's composed rows (rse_jit.cpp): the encode kernel over the k valid
+// inputs, one pass at encode speed with no run-time mixing.  Until it is ready
+// the syndrome kernel serves the pattern.  RSE_OPT_JIT 2 builds (and waits
+// for) it on first use.  True if the pattern kernel is ready for this plan.
+bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes) {
+  const int64_t mode = rse::get_option(RSE_OPT_JIT);
+  if (mode == 0 || !rse::get_option(RSE_OPT_JIT_PATTERNS) || !rse::get_option(RSE_OPT_BITSLICE) ||
+      len_bytes < rse::bitslice_chunk_bytes() || plan.rows.n_out > rse::kJitMaxOut ||
+      c->k > (size_t)kMaxIn || (mode < 2 && plan.pattern_uses < 2))
+    return false;
+  const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
+  if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), false)) return false;
+  return rse::jit_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+}
+
 // Codes plan.rows over [off, len) of every shard (the table kernels).
 int run_plan_tail(const rse_codec* c, const ReconPlan& plan, size_t off, uint64_t stripe_stride,
                   size_t n_stripes, hipStream_t s) {
@@ -552,6 +580,10 @@ int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens
   ReconPlan plan;
   int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  if (pattern_kernel(c, plan, plan.len * c->esize())) {
+    ++g_pattern_launches;
+    return run_plan_tail(c, plan, 0, 0, 1, s);  // launch_code finds the pattern's kernel
+  }
   size_t done = 0;
   rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(shards), present, data_only,
                             plan.len * c->esize(), 0, 1, s, &done);
@@ -699,7 +731,8 @@ int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes());
-  switch (rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, wait != 0)) {
+  const Rows rows = parity_rows(c);
+  switch (rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), wait != 0)) {
     case 2: return RSE_KERNELS_SPECIALISED;
     case 1: return RSE_KERNELS_SPECIALISING;
     case -1: return RSE_KERNELS_SPECIALISE_FAILED;
@@ -814,6 +847,10 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
   ReconPlan plan;
   int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, true, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  if (pattern_kernel(c, plan, sb)) {
+    ++g_pattern_launches;
+    return run_plan_tail(c, plan, 0, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream);
+  }
   size_t done = 0;
   rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(ptrs.data()), present, true,
                             sb, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream, &done);
@@ -1043,7 +1080,9 @@ int rse_set_option(int key, int64_t value) {
   return rse::set_option(key, value) == 0 ? RSE_OK : RSE_ERR_INVALID_ARGUMENT;
 }
 
-int64_t rse_get_option(int key) { return rse::get_option(key); }
+int64_t rse_get_option(int key) {
+  return key == RSE_OPT_PATTERN_LAUNCHES ? g_pattern_launches : rse::get_option(key);
+}
 
 int rse_fill_splitmix(void* dst, size_t nbytes, uint64_t seed, uint64_t shard_id,
                       rse_stream_t stream) {

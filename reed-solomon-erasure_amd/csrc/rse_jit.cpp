@@ -58,7 +58,8 @@ enum Stage { kEnc = 0, kRec = 1 };
 struct Entry {
   int field = 0;
   uint32_t k = 0, p = 0;
-  std::vector<uint16_t> rows;  // p x k parity rows
+  std::vector<uint16_t> rows;  // p x k: a codec's parity rows, or a decode pattern's rows
+  int stages = 2;              // kEnc only (decode pattern) or kEnc + kRec (codec)
   std::promise<std::shared_ptr<const Compiled>> promise[2];
   std::shared_future<std::shared_ptr<const Compiled>> built[2];
   std::mutex mu;  // guards loaded
@@ -74,17 +75,32 @@ std::mutex g_mu;  // guards the registry and the job queues
 std::condition_variable g_cv;
 std::deque<Entry*> g_jobs[2];  // per stage; every encode job runs before any reconstruct job
 std::atomic<int64_t> g_built{0};
+int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
+constexpr int kMaxPatterns = 64;
+constexpr size_t kMaxPendingPatternJobs = 8;
 
 std::vector<std::unique_ptr<Entry>>& registry() {
   static std::vector<std::unique_ptr<Entry>> v;
   return v;
 }
 
-Entry* find_entry(int field, uint32_t k, uint32_t p) {
-  std::lock_guard<std::mutex> g(g_mu);
+bool same_rows(const Entry& e, const uint16_t* rows, size_t stride) {
+  for (uint32_t o = 0; o < e.p; ++o)
+    for (uint32_t i = 0; i < e.k; ++i)
+      if (rows[o * stride + i] != e.rows[o * e.k + i]) return false;
+  return true;
+}
+
+// Caller holds g_mu.
+Entry* find_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride) {
   for (auto& e : registry())
-    if (e->field == field && e->k == k && e->p == p) return e.get();
+    if (e->field == field && e->k == k && e->p == p && same_rows(*e, rows, stride)) return e.get();
   return nullptr;
+}
+
+Entry* find_entry(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return find_locked(field, k, p, rows, stride);
 }
 
 // Sigma-row counts of the reconstruct kernels: 1, 2, 4, 8 up to p, and p.
@@ -192,8 +208,8 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
   out->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (const char* dir = std::getenv("RSE_JIT_DUMP")) {  // debugging aid
     char path[1024];
-    std::snprintf(path, sizeof path, "%s/rse_jit_gf%d_%u_%u_%s.hip", dir, e.field, e.k, e.p,
-                  stage == kEnc ? "encode" : "reconstruct");
+    std::snprintf(path, sizeof path, "%s/rse_jit_gf%d_%u_%u_%s_%p.hip", dir, e.field, e.k, e.p,
+                  stage == kEnc ? "encode" : "reconstruct", (const void*)&e);
     if (FILE* f = std::fopen(path, "w")) {
       std::fputs(src.c_str(), f);
       std::fprintf(f, "\n/* %s, %.0f ms\n%s\n*/\n", out->ok ? "ok" : "FAILED", out->ms,
@@ -251,38 +267,44 @@ Worker& worker() {
 
 }  // namespace
 
-int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool with_recon) {
   if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || k > (uint32_t)kMaxIn ||
-      p == 0 || p > kJitMaxOut || bitslice_compiled(field, k, p))
+      p == 0 || p > kJitMaxOut || (with_recon && bitslice_compiled(field, k, p)))
     return 0;
   registry();
   Worker& w = worker();
   std::lock_guard<std::mutex> g(g_mu);
-  for (auto& e : registry())
-    if (e->field == field && e->k == k && e->p == p) return 1;
+  if (find_locked(field, k, p, rows, k)) return 1;
+  if (!with_recon &&
+      (g_patterns >= kMaxPatterns || g_jobs[kEnc].size() >= kMaxPendingPatternJobs))
+    return 0;  // decode patterns are an optimisation: never queue without bound
   auto e = std::make_unique<Entry>();
   e->field = field;
   e->k = k;
   e->p = p;
+  e->stages = with_recon ? 2 : 1;
   e->rows.assign(rows, rows + (size_t)k * p);
-  for (int st = 0; st < 2; ++st) {
+  for (int st = 0; st < e->stages; ++st) {
     e->built[st] = e->promise[st].get_future().share();
     g_jobs[st].push_back(e.get());
   }
+  if (!with_recon) ++g_patterns;
   registry().push_back(std::move(e));
   w.start();
   g_cv.notify_all();
   return 1;
 }
 
-int jit_status(int field, uint32_t k, uint32_t p, bool wait) {
-  Entry* e = find_entry(field, k, p);
+int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
+  Entry* e = find_entry(field, k, p, rows, k);
   if (!e) return 0;
-  for (auto& b : e->built) {
-    if (wait) b.wait();
-    else if (b.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 1;
+  for (int st = 0; st < e->stages; ++st) {
+    if (wait) e->built[st].wait();
+    else if (e->built[st].wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 1;
   }
-  return e->built[kEnc].get()->ok && e->built[kRec].get()->ok ? 2 : -1;
+  for (int st = 0; st < e->stages; ++st)
+    if (!e->built[st].get()->ok) return -1;
+  return 2;
 }
 
 bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
@@ -290,11 +312,8 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
   *err = hipSuccess;
   const int64_t mode = get_option(9);
   if (mode == 0 || p > kJitMaxOut) return false;
-  Entry* e = find_entry(field, k, p);
-  if (!e) return false;
-  for (uint32_t o = 0; o < p; ++o)
-    for (uint32_t i = 0; i < k; ++i)
-      if (rows[o * stride + i] != e->rows[o * k + i]) return false;
+  Entry* e = find_entry(field, k, p, rows, stride);
+  if (!e || stage >= e->stages) return false;
   auto& b = e->built[stage];
   if (mode >= 2) b.wait();
   else if (b.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;

@@ -753,6 +753,7 @@ struct Options {
   int64_t host_chunk_kib = 4096;  // host pipeline chunk per shard (rse_encode_host*)
   int64_t host_h2d_streams = 2;   // host pipeline H2D streams (tools/host_e2e.py)
   int64_t jit = 1;                // run-time specialised bit-sliced kernels (rse_jit.cpp)
+  int64_t jit_patterns = 1;       // ... also for repeated decode patterns
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1081,6 +1082,7 @@ int set_option(int key, int64_t value) {
     case 7: g_opt.host_chunk_kib = value < 64 ? 64 : value; return 0;
     case 8: g_opt.host_h2d_streams = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 9: g_opt.jit = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
+    case 11: g_opt.jit_patterns = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1099,6 +1101,7 @@ int64_t get_option(int key) {
     case 8: return g_opt.host_h2d_streams;
     case 9: return g_opt.jit;
     case 10: return jit_modules_built();
+    case 11: return g_opt.jit_patterns;
     default: return -1;
   }
 }

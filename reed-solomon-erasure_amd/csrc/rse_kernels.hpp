@@ -113,12 +113,16 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
 // with hiprtc (host CPU only; no device work), then loaded per device on first
 // use.  Results never depend on which kernel runs.
 constexpr uint32_t kJitMaxOut = 8;  // p' <= 8: 16 x p' accumulator VGPRs
-// Registers the rows and starts the compile on a background thread (no-op if
-// already registered or not eligible).  Returns 1 if eligible.
-int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows);
-// 2 ready, 1 compiling, 0 not registered / not eligible, -1 compile failed.
-// wait != 0 blocks until the compile has finished.
-int jit_status(int field, uint32_t k, uint32_t p, bool wait);
+// Registers p x k rows (row-major) and queues their build on the background
+// thread.  with_recon: a codec's parity rows, built with the syndrome
+// reconstruct kernels too; otherwise a decode pattern (the composed rows of a
+// reconstruct, core.rs:697-731), encode kernel only, capped in number and
+// queue length.  Returns 1 if registered (now or before), 0 if not eligible
+// or refused.
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool with_recon);
+// 2 ready, 1 building, 0 not registered, -1 build failed; wait != 0 blocks
+// until the build has finished.
+int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 struct JitFns {
   hipFunction_t enc = nullptr;  // bitslice encode/verify (CodeArgs, chunks per stripe)
   int n_rec = 0;

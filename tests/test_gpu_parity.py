@@ -550,7 +550,7 @@ def test_bitslice_kernel_variants(R, field, k, p):
     base = np.concatenate([np.concatenate(full)] * stripes)
     r = R.core.ReedSolomon(k, p, field)
     try:
-        for var in (0, 1, 2, 3, 4):
+        for var in (0, 1, 2, 3, 4, 5, 6):
             for nt in (0, 1):
                 for gx in (1, 7, 4096):
                     lib.rse_set_option(4, var)
@@ -660,6 +660,7 @@ def test_run_time_specialised_bitslice(R, field, k, p):
     old = lib.rse_get_option(9)
     try:
         assert lib.rse_set_option(9, 2) == 0
+        assert lib.rse_set_option(11, 0) == 0  # the syndrome kernels, not decode-pattern ones
         r = R.core.ReedSolomon(k, p, field)
         assert r.kernel_kind(wait=True) == "bitslice-specialised"
         t = [dev(x).reshape(shape) for x in full[:k]] + \
@@ -705,6 +706,79 @@ def test_run_time_specialised_bitslice(R, field, k, p):
         torch.cuda.synchronize()
         assert lib.rse_get_option(6) - n0 == 1
         assert (host(d) == buf).all()
+    finally:
+        lib.rse_set_option(9, old)
+        lib.rse_set_option(11, 1)
+
+
+@pytest.mark.parametrize("field,k,p,erasures", [
+    (8, 10, 4, [[0, 1], [3], [2, 11], [0, 5, 9, 13], [10, 12]]),
+    (16, 20, 8, [[0, 1, 2, 3, 4, 5, 6, 7], [19, 20]]),
+    (8, 12, 4, [[1, 2, 3], [0, 15]]),
+    (8, 32, 8, [[0, 8, 16, 24, 32, 33, 39]]),
+])
+def test_decode_pattern_kernels(R, field, k, p, erasures):
+    """Repeated erasure patterns get their composed decode rows specialised
+    into a bit-sliced kernel at run time (RSE_OPT_JIT 2: built on first use
+    and waited for).  reconstruct, reconstruct_data and the flat many-stripe
+    form on the pattern kernels (RSE_OPT_PATTERN_LAUNCHES counts them) must
+    give the oracle's bytes; in the default mode a pattern's first use runs
+    the syndrome kernel instead."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 2 * 16384 + 40 * es
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(field + k + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    r = R.core.ReedSolomon(k, p, field)
+    old = lib.rse_get_option(9)
+    try:
+        # default mode: a fresh pattern's first use is not a pattern launch
+        lib.rse_set_option(9, 1)
+        fresh = [i for i in range(k + p) if i not in erasures[0]][:1]
+        tb = [dev(x).reshape(shape) for x in full]
+        n0 = lib.rse_get_option(12)
+        r.reconstruct([(x, i not in fresh) for i, x in enumerate(tb)])
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(12) == n0
+        assert lib.rse_set_option(9, 2) == 0
+        for erased in erasures:
+            present = [i not in erased for i in range(k + p)]
+            for data_only in (False, True):
+                if data_only and all(e >= k for e in erased):
+                    continue
+                tb = [dev(x).reshape(shape) for x in full]
+                for e in erased:
+                    tb[e].fill_(0x77)
+                n0 = lib.rse_get_option(12)
+                (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+                torch.cuda.synchronize()
+                assert lib.rse_get_option(12) - n0 == 1, (erased, data_only)
+                for i in range(k + p):
+                    got = host(tb[i]).reshape(-1)
+                    if data_only and i >= k and i in erased:
+                        assert (got == 0x77).all()
+                    else:
+                        assert (got == full[i]).all(), (erased, data_only, i)
+        # flat: several stripes, first pattern
+        erased = erasures[0]
+        stripes = 3
+        buf = np.concatenate([np.concatenate(full)] * stripes)
+        d = dev(buf)
+        v = d.view(stripes, k + p, nbytes)
+        for e in erased:
+            v[:, e].fill_(0)
+        n0 = lib.rse_get_option(12)
+        r.reconstruct_data_flat(d, n_elems, stripes, [i not in erased for i in range(k + p)])
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(12) - n0 == 1
+        got = host(d).reshape(stripes, k + p, nbytes)
+        for s_ in range(stripes):
+            for i in range(k):
+                assert (got[s_, i] == full[i]).all(), (s_, i)
     finally:
         lib.rse_set_option(9, old)
 

@@ -37,8 +37,12 @@ def main():
     ap.add_argument("--shapes", default="", help="gx:gy,gx:gy,... (default: built-in list)")
     ap.add_argument("--erase", default="0,1", help="reconstruct: erased shard indices")
     ap.add_argument("--nt-only", action="store_true", help="only non-temporal configurations")
+    ap.add_argument("--patterns", default="1",
+                    help="reconstruct: comma list of RSE_OPT_JIT_PATTERNS values (decode-pattern "
+                         "kernels; the run-time builds are waited for)")
     args = ap.parse_args()
     lib = R._lib.load()
+    lib.rse_set_option(9, 2)  # time run-time specialised kernels, not their build
     k, p, L, S = args.k, args.p, args.shard_mib * MiB, args.stripes
     buf = torch.empty(S * (k + p) * L, dtype=torch.uint8, device="cuda")
     v = buf.view(S, k + p, L)
@@ -64,16 +68,18 @@ def main():
     if args.shapes:
         shapes = [tuple(int(x) for x in s.split(":")) for s in args.shapes.split(",")]
     bss = [int(x) for x in args.bitslice.split(",")]
+    pats = [int(x) for x in args.patterns.split(",")] if args.op == "reconstruct" else [1]
     nts = (0, 1) if not args.nt_only else (1,)
-    configs = [(nt, gx, gy, var, bs) for bs in bss for var in range(args.variants)
-               for nt in nts for gx, gy in shapes]
+    configs = [(nt, gx, gy, var, bs, pat) for pat in pats for bs in bss
+               for var in range(args.variants) for nt in nts for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for c in configs:
-            nt, gx, gy, var, bs = c
+            nt, gx, gy, var, bs, pat = c
+            lib.rse_set_option(11, pat)
             lib.rse_set_option(5, bs)
             lib.rse_set_option(1, nt)
             lib.rse_set_option(2, gx)
@@ -89,9 +95,9 @@ def main():
     rows = sorted(((statistics.median(x), min(x), max(x), c) for c, x in res.items()), reverse=True)
     what = f" erased {erased}" if args.op == "reconstruct" else ""
     print(f"{args.op} GF(2^{args.field}) {k}+{p} x {args.shard_mib} MiB, {S} stripes{what}; GB/s (1e9)")
-    for med, lo, hi, (nt, gx, gy, var, bs) in rows:
-        print(f"  bitslice={bs} variant={var} nt={nt} grid_x={gx:<5} stripes_in_flight={gy:<3}  median "
-              f"{med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
+    for med, lo, hi, (nt, gx, gy, var, bs, pat) in rows:
+        print(f"  bitslice={bs} patterns={pat} variant={var} nt={nt} grid_x={gx:<5} "
+              f"stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
     print(json.dumps({"best": {"bitslice": b[4], "variant": b[3], "nt": b[0], "grid_x": b[1],
                                "stripes_in_flight": b[2], "GBps": round(rows[0][0], 1)}}))
