@@ -273,7 +273,154 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_kerne
   bitslice_recon_body<C, NT, NS>(a, chunks_per_stripe);
 }
 
+template <class C, bool NT, int NS>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_kernel(
+    const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
+  bitslice_recon_desc_body<C, NT, NS>(descs, chunks_per_stripe, n_stripes);
+}
+
+// ------------------------------------------------- batched reconstruct planner
+// One lane per stripe of rse_reconstruct_batch: the syndrome plan of
+// rse_codec.cpp bitslice_reconstruct on the device.  The valid/invalid
+// partition of core.rs:801-841 gives S (missing data), R (the first |S|
+// present parity rows -- the parity rows of the reference's `valid` set) and
+// M (missing parity, unless data_only); A = P[R][S] is inverted by
+// Gauss-Jordan (the unique inverse: any k rows of the systematic MDS matrix
+// are independent, so A is invertible) and the stripe's BsReconArgs written.
+struct GfDev {
+  const uint8_t* lg;
+  const uint8_t* ex;
+  int field;
+  __device__ uint32_t m8(uint32_t a, uint32_t b) const {
+    return (a && b) ? ex[lg[a] + lg[b]] : 0u;
+  }
+  __device__ uint32_t mul(uint32_t a, uint32_t b) const {  // galois_16.rs:146-162
+    if (field == 8) return m8(a, b);
+    const uint32_t a1 = a >> 8, a0 = a & 0xFFu, b1 = b >> 8, b0 = b & 0xFFu;
+    const uint32_t hh = m8(a1, b1);
+    const uint32_t x = m8(a1, b0) ^ m8(a0, b1) ^ m8(2u, hh);
+    const uint32_t c = m8(a0, b0) ^ m8(128u, hh);
+    return (x << 8) | c;
+  }
+  __device__ uint32_t inv(uint32_t a) const {  // a != 0
+    if (field == 8) return ex[255 - lg[a]];
+    uint32_t r = 1, b = a;
+    for (uint32_t n = 65534u; n; n >>= 1) {
+      if (n & 1u) r = mul(r, b);
+      b = mul(b, b);
+    }
+    return r;
+  }
+};
+
+constexpr int kPlanBlock = 64;
+
+__global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
+    int field, const uint16_t* __restrict__ rows, const uint8_t* __restrict__ present, uint32_t k,
+    uint32_t p, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
+    BsReconArgs* descs) {
+  __shared__ uint8_t lg[256], ex[512];
+  if (threadIdx.x == 0) {  // generator 2 modulo 0x11D (build.rs:13-43)
+    uint32_t b = 1;
+    for (uint32_t l = 0; l < 255; ++l) {
+      lg[b] = (uint8_t)l;
+      ex[l] = ex[l + 255] = (uint8_t)b;
+      b <<= 1;
+      if (b & 0x100u) b ^= 0x11Du;
+    }
+    lg[0] = 0;
+    ex[510] = ex[511] = 0;
+  }
+  __syncthreads();
+  const uint32_t s = blockIdx.x * kPlanBlock + threadIdx.x;
+  if (s >= n_stripes) return;
+  const GfDev gf{lg, ex, field};
+  const uint32_t total = k + p;
+  const uint8_t* pr = present + (uint64_t)s * total;
+  uint8_t* sb = base + (uint64_t)s * total * shard_bytes;
+  BsReconArgs& d = descs[s];
+  uint32_t S[kMaxOut], R[kMaxOut], M[kMaxOut];
+  uint32_t ne = 0, nr = 0, nm = 0, pmask = 0;
+  bool fits = true;
+  for (uint32_t j = 0; j < k; ++j) {
+    d.data[j] = pr[j] ? sb + (uint64_t)j * shard_bytes : nullptr;
+    if (pr[j]) pmask |= 1u << j;
+    else if (ne < (uint32_t)kMaxOut) S[ne++] = j;
+    else fits = false;
+  }
+  for (uint32_t r = 0; r < p; ++r) {
+    if (pr[k + r]) {
+      if (nr < ne) R[nr++] = r;
+    } else if (!data_only) {
+      M[nm++] = r;
+    }
+  }
+  for (uint32_t r = 0; r < (uint32_t)kMaxOut; ++r) {
+    d.par[r] = nullptr;
+    d.out[r] = nullptr;
+    d.out_sigma[r] = -1;
+    for (uint32_t q = 0; q < (uint32_t)kMaxOut; ++q) d.w[r][q] = 0;
+  }
+  d.stripe_stride = 0;
+  d.n_stripes = 1;
+  d.present = pmask;
+  d.sigma = d.synd = 0;
+  d.n_out = 0;  // nothing to do unless completed below
+  if (!fits || nr != ne || ne + nm == 0 || ne + nm > (uint32_t)kMaxOut) return;
+  // [A | I], A = P[R][S], Gauss-Jordan
+  uint16_t w[kMaxOut][2 * kMaxOut];
+  for (uint32_t t = 0; t < ne; ++t)
+    for (uint32_t u = 0; u < ne; ++u) {
+      w[t][u] = rows[R[t] * k + S[u]];
+      w[t][ne + u] = t == u ? 1 : 0;
+    }
+  for (uint32_t col = 0; col < ne; ++col) {
+    uint32_t piv = col;
+    while (piv < ne && w[piv][col] == 0) ++piv;
+    if (piv == ne) return;  // singular: impossible for this code; stripe untouched
+    if (piv != col)
+      for (uint32_t x = 0; x < 2 * ne; ++x) {
+        const uint16_t t0 = w[col][x];
+        w[col][x] = w[piv][x];
+        w[piv][x] = t0;
+      }
+    const uint32_t sc = gf.inv(w[col][col]);
+    for (uint32_t x = 0; x < 2 * ne; ++x) w[col][x] = (uint16_t)gf.mul(sc, w[col][x]);
+    for (uint32_t r = 0; r < ne; ++r) {
+      const uint32_t f = w[r][col];
+      if (r == col || !f) continue;
+      for (uint32_t x = 0; x < 2 * ne; ++x) w[r][x] ^= (uint16_t)gf.mul(f, w[col][x]);
+    }
+  }
+  uint32_t o = 0;
+  for (uint32_t u = 0; u < ne; ++u, ++o) {  // missing data S[u] = sum_t Ainv[u][t] s_t
+    d.out[o] = sb + (uint64_t)S[u] * shard_bytes;
+    for (uint32_t t = 0; t < ne; ++t) d.w[o][R[t]] = w[u][ne + t];
+  }
+  for (uint32_t m = 0; m < nm; ++m, ++o) {  // missing parity r = sigma_r ^ sum_t (P[r][S] Ainv)[t] s_t
+    const uint32_t r = M[m];
+    d.out[o] = sb + (uint64_t)(k + r) * shard_bytes;
+    d.out_sigma[o] = (int32_t)r;
+    for (uint32_t t = 0; t < ne; ++t) {
+      uint32_t v = 0;
+      for (uint32_t u = 0; u < ne; ++u) v ^= gf.mul(rows[r * k + S[u]], w[u][ne + t]);
+      d.w[o][R[t]] = (uint16_t)v;
+    }
+  }
+  uint32_t synd = 0, sigma = 0;
+  for (uint32_t t = 0; t < ne; ++t) {
+    synd |= 1u << R[t];
+    d.par[R[t]] = sb + (uint64_t)(k + R[t]) * shard_bytes;
+  }
+  sigma = synd;
+  for (uint32_t m = 0; m < nm; ++m) sigma |= 1u << M[m];
+  d.synd = synd;
+  d.sigma = sigma;
+  d.n_out = o;
+}
+
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
+using BsDescFn = void (*)(const BsReconArgs*, uint64_t, uint64_t);
 
 using BsFn = void (*)(const CodeArgs, uint64_t);
 struct BsShape {
@@ -284,11 +431,17 @@ struct BsShape {
                       // prefetch, 3/4 LDS-DMA input ring of 3/2 slots, 5/6 two/three
                       // inputs in flight in VGPRs (3-6: nt only)
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
+  BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
 
 template <class C, int NS>
 constexpr BsRecFn rec_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS>;
+  else return nullptr;
+}
+template <class C, int NS>
+constexpr BsDescFn rec_desc_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_desc_kernel<C, true, NS>;
   else return nullptr;
 }
 #define BS(F, FIELD, K, P)                                                      \
@@ -302,7 +455,9 @@ constexpr BsRecFn rec_fn() {
     {nullptr, bitslice_deep_kernel<Code<F, K, P>, 2>},                            \
     {nullptr, bitslice_deep_kernel<Code<F, K, P>, 3>}},                           \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
-    rec_fn<Code<F, K, P>, 8>()}}
+    rec_fn<Code<F, K, P>, 8>()},                                                   \
+   {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
+    rec_desc_fn<Code<F, K, P>, 4>(), rec_desc_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
     BS(CF8, 8, 10, 4),    // BASELINE headline: galois_8 10+4
     BS(CF8, 8, 10, 2),    // benches/bandwidth.rs 10+2
@@ -391,6 +546,62 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
   void* args[] = {const_cast<BsReconArgs*>(&a), &cps_arg};
   e = hipModuleLaunchKernel(jf.rec[slot], (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args,
                             nullptr);
+  if (e != hipSuccess) return e;
+  count_bitslice_launch();
+  *handled = true;
+  return hipSuccess;
+}
+
+hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
+                                       const uint16_t* parity_rows, const uint16_t* d_rows,
+                                       const uint8_t* d_present, uint32_t data_only,
+                                       uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
+                                       uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
+                                       bool* handled) {
+  *handled = false;
+  if (!get_option(5) || shard_bytes < kBsChunk || k == 0 || k > (uint32_t)kMaxIn ||
+      p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0)
+    return hipSuccess;
+  BsDescFn sfn = nullptr;
+  hipFunction_t jfn = nullptr;
+  bool compiled = false;
+  for (const BsShape& sh : kBsShapes) {
+    if (sh.field != field || sh.k != k || sh.p != p) continue;
+    compiled = true;
+    for (uint32_t i = 0; i < k * p; ++i)
+      if (parity_rows[i] != sh.m[i]) return hipSuccess;
+    for (int q = 0; q < 4 && !sfn; ++q)
+      if (sh.rec_desc[q] && (1u << q) >= need) sfn = sh.rec_desc[q];
+    if (!sfn) return hipSuccess;
+  }
+  if (!compiled) {
+    JitFns jf;
+    hipError_t e = hipSuccess;
+    if (!jit_find(field, k, p, parity_rows, k, 1, &jf, &e)) return e;
+    for (int q = 0; q < jf.n_rec && !jfn; ++q)
+      if ((uint32_t)jf.rec_ns[q] >= need) jfn = jf.rec_desc[q];
+    if (!jfn) return hipSuccess;
+  }
+  hipLaunchKernelGGL(bs_recon_plan_kernel, dim3((n_stripes + kPlanBlock - 1) / kPlanBlock),
+                     dim3(kPlanBlock), 0, stream, field, d_rows, d_present, k, p, data_only, base,
+                     shard_bytes, n_stripes, d_descs);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
+  const uint64_t total = cps * ns;
+  const int64_t grid = get_option(2);
+  uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;
+  if (gx > total) gx = total;
+  if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+  if (sfn) {
+    hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
+                       (const BsReconArgs*)d_descs, cps, ns);
+    e = hipGetLastError();
+  } else {
+    const BsReconArgs* dp = d_descs;
+    void* args[] = {&dp, &cps, &ns};
+    e = hipModuleLaunchKernel(jfn, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args, nullptr);
+  }
   if (e != hipSuccess) return e;
   count_bitslice_launch();
   *handled = true;

@@ -360,18 +360,15 @@ __device__ __forceinline__ void mac_vectors(u32x4 (&o)[4], const uint32_t* v, co
   }
 }
 
-// Reconstruct body.  Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
-template <class C, bool NT, int NS>
-__device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
-                                                    uint64_t chunks_per_stripe) {
+// The per-(output, syndrome row) GF(2^8) tables of the run-time mixing, for
+// one set of reconstruct arguments (all lanes; the caller synchronises).
+template <class C, int NS>
+__device__ __forceinline__ void recon_tables(const BsReconArgs& a, uint4* tq, uint32_t* tt2) {
   using F = typename C::Field;
-  constexpr int TPC = F::kPlanes == 16 ? 4 : 1;  // GF(2^8) tables per coefficient
-  __shared__ uint4 tq[kMaxOut * NS * TPC];
-  __shared__ uint32_t tt2[kMaxOut * NS * TPC];
   const uint32_t n_out = a.n_out;
   for (uint32_t t = threadIdx.x; t < n_out * NS; t += kBsBlock) {
     const uint32_t c = a.w[t / NS][t % NS];
-    if constexpr (TPC == 1) {
+    if constexpr (F::kPlanes == 8) {
       write_tab(tq, tt2, t, make_gf8_tab(c));
     } else {
       uint32_t sub[4];
@@ -380,61 +377,113 @@ __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
       for (int q = 0; q < 4; ++q) write_tab(tq, tt2, t * 4 + q, make_gf8_tab(sub[q]));
     }
   }
-  __syncthreads();
+}
+
+// One 16 KiB chunk of one stripe: off is the lane's byte offset from the
+// argument block's shard pointers.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* tq,
+                                            const uint32_t* tt2, uint64_t off) {
+  using F = typename C::Field;
+  const uint32_t n_out = a.n_out;
   const uint64_t mask = recon_mask(a, C::k);
-  const int first = __builtin_ctzll(mask);  // host guarantees mask != 0
+  const int first = __builtin_ctzll(mask);  // host / planner guarantee mask != 0
+  uint32_t acc[NS * 16];
+#pragma unroll
+  for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
+  u32x4 cur[4];
+  load4<NT>(cur, recon_ptr(a, C::k, first) + off);
+  recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
+  // back to element order, in place
+#pragma unroll
+  for (int r = 0; r < NS; ++r) {
+    if (!((a.sigma >> r) & 1u)) continue;
+    uint32_t pl[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pl[q] = acc[r * 16 + q];
+    u32x4 v[4];
+    unslice<F>(pl, v);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[r * 16 + q] = v[q >> 2][q & 3];
+  }
+#pragma unroll 1
+  for (uint32_t o = 0; o < n_out; ++o) {
+    // opaque per output: otherwise LICM hoists every row's byte-plane split
+    // and selectors out of this loop (hundreds of VGPRs -> scratch)
+#pragma unroll
+    for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (u32x4){0u, 0u, 0u, 0u};
+    const int os = a.out_sigma[o];
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      if (os == r) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] ^= acc[r * 16 + q];
+      }
+      // one row's tables at a time: the opaque offset (ordered after the
+      // previous row's pins) keeps hipcc from loading every row's tables
+      // up front, which spills
+      const uint32_t lb = opaque_zero();
+      if (((a.synd >> r) & 1u) && a.w[o][r] != 0)
+        mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * NS + r));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(v[j][w]));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stv<NT>(a.out[o] + off + j * (kBsBlock * 16), v[j]);
+  }
+}
+
+template <int NS, class F>
+struct ReconLds {
+  static constexpr int kTabs = kMaxOut * NS * (F::kPlanes == 16 ? 4 : 1);
+};
+
+// Reconstruct body: one argument block for every stripe of the launch.
+// Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
+                                                    uint64_t chunks_per_stripe) {
+  constexpr int T = ReconLds<NS, typename C::Field>::kTabs;
+  __shared__ uint4 tq[T];
+  __shared__ uint32_t tt2[T];
+  recon_tables<C, NS>(a, tq, tt2);
+  __syncthreads();
   const uint64_t total = chunks_per_stripe * a.n_stripes;
   for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    const uint64_t off = stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
-    uint32_t acc[NS * 16];
-#pragma unroll
-    for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
-    u32x4 cur[4];
-    load4<NT>(cur, recon_ptr(a, C::k, first) + off);
-    recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
-    // back to element order, in place
-#pragma unroll
-    for (int r = 0; r < NS; ++r) {
-      if (!((a.sigma >> r) & 1u)) continue;
-      uint32_t pl[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) pl[q] = acc[r * 16 + q];
-      u32x4 v[4];
-      unslice<F>(pl, v);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[r * 16 + q] = v[q >> 2][q & 3];
+    recon_chunk<C, NT, NS>(a, tq, tt2,
+                           stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
+  }
+}
+
+// Reconstruct body over per-stripe argument blocks (descs[s], written by the
+// device planner of rse_reconstruct_batch: every stripe its own erasure
+// pattern).  A workgroup rebuilds its mixing tables when its stripe changes.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __restrict__ descs,
+                                                         uint64_t chunks_per_stripe,
+                                                         uint64_t n_stripes) {
+  constexpr int T = ReconLds<NS, typename C::Field>::kTabs;
+  __shared__ uint4 tq[T];
+  __shared__ uint32_t tt2[T];
+  uint64_t built = ~0ull;
+  const uint64_t total = chunks_per_stripe * n_stripes;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const BsReconArgs& a = descs[stripe];
+    if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
+    if (stripe != built) {
+      __syncthreads();  // every lane is done with the previous stripe's tables
+      recon_tables<C, NS>(a, tq, tt2);
+      __syncthreads();
+      built = stripe;
     }
-#pragma unroll 1
-    for (uint32_t o = 0; o < n_out; ++o) {
-      // opaque per output: otherwise LICM hoists every row's byte-plane split
-      // and selectors out of this loop (hundreds of VGPRs -> scratch)
-#pragma unroll
-      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
-      u32x4 v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (u32x4){0u, 0u, 0u, 0u};
-      const int os = a.out_sigma[o];
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        if (os == r) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] ^= acc[r * 16 + q];
-        }
-        // one row's tables at a time: the opaque offset (ordered after the
-        // previous row's pins) keeps hipcc from loading every row's tables
-        // up front, which spills
-        const uint32_t lb = opaque_zero();
-        if (((a.synd >> r) & 1u) && a.w[o][r] != 0)
-          mac_vectors<F>(v, &acc[r * 16], tq, tt2, (int)(lb + o * NS + r));
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(v[j][w]));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) stv<NT>(a.out[o] + off + j * (kBsBlock * 16), v[j]);
-    }
+    recon_chunk<C, NT, NS>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
   }
 }
 

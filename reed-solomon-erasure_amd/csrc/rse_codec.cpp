@@ -869,41 +869,85 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
                           const uint8_t* present, int data_only, rse_stream_t stream) {
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
-  const size_t T = c->total, sb = shard_len * c->esize();
+  const size_t k = c->k, p = c->p, T = c->total, sb = shard_len * c->esize();
   for (size_t s = 0; s < n_stripes; ++s) {  // core.rs:747-772, stripe by stripe
     size_t np = 0;
     for (size_t i = 0; i < T; ++i) np += present[s * T + i] ? 1 : 0;
     if (np && shard_len == 0) return RSE_EMPTY_SHARD;
-    if (np < c->k) return RSE_TOO_FEW_SHARDS_PRESENT;
+    if (np < k) return RSE_TOO_FEW_SHARDS_PRESENT;
   }
   uint8_t* base = static_cast<uint8_t*>(stripes);
   hipStream_t st = (hipStream_t)stream;
-  if (c->field != RSE_FIELD_GF8 || c->k > (size_t)kMaxIn || c->p > (size_t)kMaxOut ||
-      n_stripes > 0xffffffffu) {
-    std::vector<void*> ptrs(T);
-    std::vector<size_t> lens(T, shard_len);
+  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
+  size_t done = 0;  // bytes of every shard coded so far
+  // 1. whole 16 KiB chunks on the bit-sliced syndrome kernels (compiled or
+  //    run-time specialised codecs), planned per stripe on the device
+  if (fits && sb >= rse::bitslice_chunk_bytes() && sb % 16u == 0 && aligned16(base) &&
+      rse::get_option(RSE_OPT_BITSLICE)) {
+    want_bitslice(c, sb);
+    uint32_t need = 0;  // sigma rows any stripe uses: its R and missing parity rows
     for (size_t s = 0; s < n_stripes; ++s) {
-      for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb;
+      const uint8_t* pr = present + s * T;
+      size_t ne = 0, nr = 0;
+      for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0 : 1;
+      for (size_t r = 0; r < p; ++r) {
+        const bool syn = pr[k + r] && nr < ne;
+        nr += syn ? 1 : 0;
+        if (syn || (!pr[k + r] && !data_only)) need = std::max<uint32_t>(need, (uint32_t)r + 1);
+      }
+    }
+    if (need > 0) {
+      const Rows rows = parity_rows(c);
+      const size_t rows_bytes = rows.c.size() * 2, pres_off = (rows_bytes + 255) & ~size_t(255);
+      const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
+      uint8_t* ws = nullptr;
+      RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + n_stripes * sizeof(rse::BsReconArgs), st));
+      hipError_t e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
+      bool handled = false;
+      if (e == hipSuccess)
+        e = rse::launch_bitslice_recon_batch(
+            c->field, (uint32_t)k, (uint32_t)p, rows.c.data(), reinterpret_cast<uint16_t*>(ws),
+            ws + pres_off, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
+            reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &handled);
+      hipError_t f = hipFreeAsync(ws, st);
+      if (e == hipSuccess) e = f;
+      if (e == hipSuccess) e = hipStreamSynchronize(st);  // `rows` dies here
+      if (e != hipSuccess) return dev_fail(e);
+      if (handled) done = (sb / rse::bitslice_chunk_bytes()) * rse::bitslice_chunk_bytes();
+    } else {
+      return RSE_OK;  // nothing missing that this call rebuilds, in any stripe
+    }
+  }
+  if (done == sb) return RSE_OK;
+  // 2. the rest of every shard (all of it if step 1 did not apply)
+  if (c->field != RSE_FIELD_GF8 || !fits) {  // host planner, stripe by stripe
+    std::vector<void*> ptrs(T);
+    std::vector<size_t> lens(T, (sb - done) / c->esize());
+    for (size_t s = 0; s < n_stripes; ++s) {
+      for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb + done;
       int rc = reconstruct_impl(c, ptrs.data(), lens.data(), present + s * T, T, data_only != 0, st);
       if (rc) return rc;
     }
     return RSE_OK;
   }
-  const size_t mat_bytes = T * c->k, pres_off = (mat_bytes + 255) & ~size_t(255);
+  // device planner (k x k inverse per stripe) + table kernels
+  const size_t mat_bytes = T * k, pres_off = (mat_bytes + 255) & ~size_t(255);
   const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
   const size_t ws_bytes = desc_off + n_stripes * sizeof(CodeArgs);
   std::vector<uint8_t> mat(mat_bytes);
   for (size_t r = 0; r < T; ++r)
-    for (size_t j = 0; j < c->k; ++j) mat[r * c->k + j] = (uint8_t)c->mat(r, j);
+    for (size_t j = 0; j < k; ++j) mat[r * k + j] = (uint8_t)c->mat(r, j);
   uint8_t* ws = nullptr;
   RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), ws_bytes, st));
   hipError_t e = hipMemcpyAsync(ws, mat.data(), mat_bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
-    e = rse::launch_recon_batch(ws, ws + pres_off, (uint32_t)c->k, (uint32_t)T,
-                                data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes,
-                                reinterpret_cast<CodeArgs*>(ws + desc_off), st);
+    e = rse::launch_recon_batch(ws, ws + pres_off, (uint32_t)k, (uint32_t)T,
+                                data_only ? 1u : 0u, base, sb, done, sb - done,
+                                (uint32_t)n_stripes, reinterpret_cast<CodeArgs*>(ws + desc_off), st);
   hipError_t f = hipFreeAsync(ws, st);
   if (e != hipSuccess) return dev_fail(e);
   if (f != hipSuccess) return dev_fail(f);

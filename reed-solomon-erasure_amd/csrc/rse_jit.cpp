@@ -179,6 +179,12 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   "  rse::bitslice_recon_body<rse::JitCode, true, %d>(a, cps);\n}\n",
                   ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
     s += buf;
+    std::snprintf(buf, sizeof buf,
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
+                  "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+                  "  rse::bitslice_recon_desc_body<rse::JitCode, true, %d>(d, cps, n);\n}\n",
+                  ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
+    s += buf;
   }
   return s;
 }
@@ -346,6 +352,9 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
         char name[32];
         std::snprintf(name, sizeof name, "rse_jit_recon%d", f.rec_ns[q]);
         he = hipModuleGetFunction(&f.rec[q], m, name);
+        if (he != hipSuccess) break;
+        std::snprintf(name, sizeof name, "rse_jit_recon_desc%d", f.rec_ns[q]);
+        he = hipModuleGetFunction(&f.rec_desc[q], m, name);
       }
     }
     if (he != hipSuccess) {

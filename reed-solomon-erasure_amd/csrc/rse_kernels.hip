@@ -874,8 +874,8 @@ __global__ __launch_bounds__(1024) void gf8_invert_kernel(const uint8_t* in, uin
 // stripe's CodeArgs for gf8_code_desc_kernel.  k <= kMaxIn, p <= kMaxOut.
 __global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
     const uint8_t* __restrict__ matrix, const uint8_t* __restrict__ present, uint32_t k,
-    uint32_t total, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint64_t n_vec,
-    CodeArgs* descs) {
+    uint32_t total, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint64_t off,
+    uint64_t len, uint64_t n_vec, CodeArgs* descs) {
   __shared__ uint8_t lg[256], ex[512];
   __shared__ uint8_t valid[kMaxIn], miss[kMaxIn + kMaxOut];
   __shared__ uint8_t w[kMaxIn][2 * kMaxIn];
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
     d.n_stripes = 1;
     d.stripe_stride = 0;
     d.n_vec = n_vec;
-    d.len = shard_bytes;
+    d.len = len;
     d.mismatch = nullptr;
     d.mode = kStore;
     d.accumulate = 0;
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
   __syncthreads();
   const uint32_t n_out = (uint32_t)s_nout;
   if (n_out == 0) return;  // uniform
-  const uint8_t* sbase = base + (uint64_t)s * total * shard_bytes;
+  const uint8_t* sbase = base + (uint64_t)s * total * shard_bytes + off;
   for (uint32_t i = tid; i < k; i += nt) d.in[i] = sbase + (uint64_t)valid[i] * shard_bytes;
   for (uint32_t o = tid; o < n_out; o += nt) {
     d.out[o] = const_cast<uint8_t*>(sbase) + (uint64_t)miss[o] * shard_bytes;
@@ -1045,17 +1045,18 @@ hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream) {
 
 hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
                               uint32_t total, uint32_t data_only, uint8_t* base,
-                              uint64_t shard_bytes, uint32_t n_stripes, CodeArgs* d_descs,
-                              hipStream_t stream) {
-  if (k == 0 || k > (uint32_t)kMaxIn || total - k > (uint32_t)kMaxOut || n_stripes == 0)
+                              uint64_t shard_bytes, uint64_t off, uint64_t len,
+                              uint32_t n_stripes, CodeArgs* d_descs, hipStream_t stream) {
+  if (k == 0 || k > (uint32_t)kMaxIn || total - k > (uint32_t)kMaxOut || n_stripes == 0 ||
+      off + len > shard_bytes || len == 0)
     return hipErrorInvalidValue;
-  const bool al = (reinterpret_cast<uintptr_t>(base) % 16u) == 0 && shard_bytes % 16u == 0;
-  const uint64_t n_vec = al ? shard_bytes / 16u : 0;
+  const bool al = (reinterpret_cast<uintptr_t>(base + off) % 16u) == 0 && shard_bytes % 16u == 0;
+  const uint64_t n_vec = al ? len / 16u : 0;
   hipLaunchKernelGGL(gf8_recon_plan_kernel, dim3(n_stripes), dim3(256), 0, stream, d_matrix,
-                     d_present, k, total, data_only, base, shard_bytes, n_vec, d_descs);
+                     d_present, k, total, data_only, base, shard_bytes, off, len, n_vec, d_descs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint64_t units = n_vec ? n_vec : shard_bytes + 1;
+  const uint64_t units = n_vec ? n_vec : len + 1;
   uint64_t gx = (2048u + n_stripes - 1) / n_stripes;
   const uint64_t want = (units + kBlock - 1) / kBlock;
   if (gx > want) gx = want;

@@ -82,10 +82,12 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
 // on the device, then code every stripe from its descriptor.  `base` holds
 // n_stripes flat stripes of `total` shards of shard_bytes each; d_present is
 // n_stripes x total flags; d_matrix the (total x k) encoding matrix.
+// Only bytes [off, off + len) of every shard are coded (the bit-sliced batch
+// path codes the whole chunks before).
 hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
                               uint32_t total, uint32_t data_only, uint8_t* base,
-                              uint64_t shard_bytes, uint32_t n_stripes, CodeArgs* d_descs,
-                              hipStream_t stream);
+                              uint64_t shard_bytes, uint64_t off, uint64_t len,
+                              uint32_t n_stripes, CodeArgs* d_descs, hipStream_t stream);
 
 // Table kernels only (launch_code minus the bit-sliced dispatch).
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
@@ -106,6 +108,19 @@ int bitslice_compiled(int field, uint32_t k, uint32_t p);
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
                                  bool* handled);
+
+// rse_reconstruct_batch on the bit-sliced kernels: a device planner writes one
+// BsReconArgs per stripe (its own erasure pattern: partition, e x e syndrome
+// inverse, mixing rows), then the syndrome kernel codes the whole 16 KiB
+// chunks of every stripe from them.  d_rows: the p x k parity rows on the
+// device (parity_rows: the same on the host, to select the kernels); need:
+// sigma rows any stripe uses (max row + 1).  *handled unset = nothing queued.
+hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
+                                       const uint16_t* parity_rows, const uint16_t* d_rows,
+                                       const uint8_t* d_present, uint32_t data_only,
+                                       uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
+                                       uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
+                                       bool* handled);
 
 // ---- run-time specialisation (rse_jit.cpp) ----------------------------------
 // Bit-sliced kernels for codecs not compiled into the library: the XOR networks
@@ -128,6 +143,7 @@ struct JitFns {
   int n_rec = 0;
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
+  hipFunction_t rec_desc[5] = {};  // ... over per-stripe BsReconArgs (descs, cps, n_stripes)
 };
 // Kernels of `stage` (0: encode/verify, 1: reconstruct) for a launch whose
 // coefficients rows[o * stride + i] equal a registered codec's parity rows,

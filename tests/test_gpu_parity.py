@@ -401,19 +401,31 @@ def test_encode_flat_many_stripes(R):
     assert torch.equal(v[:, :k], ref[:, :k])
 
 
-@pytest.mark.parametrize("field,k,p,n,stripes", [
-    (8, 10, 4, 4096 + 16, 33),     # device planner, aligned
-    (8, 10, 4, 1037, 9),           # device planner, byte path
-    (8, 32, 16, 256, 5),           # device planner at its limits
-    (8, 1, 1, 64, 3),
-    (8, 40, 20, 512, 3),           # host-planner fallback (k > 32)
-    (16, 20, 8, 300, 4),           # host-planner fallback (GF(2^16))
+@pytest.mark.parametrize("field,k,p,n,stripes,bs", [
+    (8, 10, 4, 4096 + 16, 33, 0),     # device planner, aligned
+    (8, 10, 4, 1037, 9, 0),           # device planner, byte path
+    (8, 32, 16, 256, 5, 0),           # device planner at its limits
+    (8, 1, 1, 64, 3, 0),
+    (8, 40, 20, 512, 3, 0),           # host-planner fallback (k > 32)
+    (16, 20, 8, 300, 4, 0),           # host-planner fallback (GF(2^16))
+    (8, 10, 4, 2 * 16384 + 48, 9, 1),   # bit-sliced syndrome batch + table-planner tail
+    (8, 10, 2, 16384, 5, 1),            # bit-sliced only
+    (16, 20, 8, 16384 + 8, 5, 1),       # GF(2^16) device planner + host-planner tail
+    (8, 12, 4, 2 * 16384, 7, 1),        # run-time specialised codec
+    (16, 6, 3, 8192 * 3, 4, 1),         # run-time specialised GF(2^16) codec
 ])
-def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes):
+def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs):
     """rse_reconstruct_batch: every stripe with its own erasure pattern, against
-    the oracle's reconstruct of each stripe (core.rs:680/690 semantics)."""
+    the oracle's reconstruct of each stripe (core.rs:680/690 semantics).  bs:
+    the whole 16 KiB chunks run on the bit-sliced syndrome kernels from
+    per-stripe descriptors planned on the device (one launch, counted)."""
     rng = np.random.default_rng(field * 1000 + k * 31 + p)
+    lib = R._lib.load()
+    old_jit = lib.rse_get_option(9)
+    lib.rse_set_option(9, 2)  # run-time specialised kernels: wait for the build
     r = R.core.ReedSolomon(k, p, field)
+    if bs:
+        assert r.kernel_kind(wait=True).startswith("bitslice")
     oc = O.Codec(field, k, p)
     es = field // 8
     T = k + p
@@ -438,14 +450,17 @@ def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes):
             oc.reconstruct(ob, present[s].tolist(), data_only=data_only)
             want[s] = np.stack(ob)
         d = dev(buf)
+        n0 = lib.rse_get_option(6)
         r.reconstruct_batch(d, n, stripes, present, data_only=data_only)
         got = host(d).reshape(stripes, T, n * es)
+        assert lib.rse_get_option(6) - n0 == bs, data_only
         assert (got == want).all(), data_only
         # every data shard is back; parity back unless data_only
         for s in range(stripes):
             for i in range(T):
                 if i < k or not data_only:
                     assert (got[s, i] == full[s][i]).all(), (s, i, data_only)
+    lib.rse_set_option(9, old_jit)
 
 
 def test_reconstruct_batch_many_stripes_and_errors(R):

@@ -31,7 +31,9 @@ def main():
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--field", type=int, default=8)
     ap.add_argument("--shard-mib", type=int, default=16)
-    ap.add_argument("--op", default="encode", choices=["encode", "reconstruct"])
+    ap.add_argument("--op", default="encode", choices=["encode", "reconstruct", "batch"],
+                    help="batch: rse_reconstruct_batch, every stripe its own random pattern "
+                         "of len(--erase) erased shards")
     ap.add_argument("--variants", type=int, default=1)
     ap.add_argument("--bitslice", default="1", help="comma list of RSE_OPT_BITSLICE values")
     ap.add_argument("--shapes", default="", help="gx:gy,gx:gy,... (default: built-in list)")
@@ -57,18 +59,30 @@ def main():
     erased = [int(x) for x in args.erase.split(",")]
     present = [i not in erased for i in range(k + p)]
 
+    import numpy as np
+    rng = np.random.default_rng(5)
+    batch_present = np.ones((S, k + p), bool)
+    for s_ in range(S):
+        batch_present[s_, rng.choice(k + p, len(erased), replace=False)] = False
+
     def op():
         if args.op == "encode":
             r.encode_flat(buf, elems, S)
+        elif args.op == "batch":
+            r.reconstruct_batch(buf, elems, S, batch_present, data_only=True)
         else:
             r.reconstruct_data_flat(buf, elems, S, present)
 
-    nbytes = S * ((k + p) if args.op == "encode" else (k + len(erased))) * L
+    if args.op == "batch":  # per stripe with missing data: k reads + the missing data written
+        miss = (~batch_present[:, :k]).sum(axis=1)
+        nbytes = int((miss > 0).sum() * k + miss.sum()) * L
+    else:
+        nbytes = S * ((k + p) if args.op == "encode" else (k + len(erased))) * L
     shapes = [(512, 1), (1024, 1), (2048, 1), (4096, 1), (8, 0), (16, 0)]
     if args.shapes:
         shapes = [tuple(int(x) for x in s.split(":")) for s in args.shapes.split(",")]
     bss = [int(x) for x in args.bitslice.split(",")]
-    pats = [int(x) for x in args.patterns.split(",")] if args.op == "reconstruct" else [1]
+    pats = [int(x) for x in args.patterns.split(",")] if args.op != "encode" else [1]
     nts = (0, 1) if not args.nt_only else (1,)
     configs = [(nt, gx, gy, var, bs, pat) for pat in pats for bs in bss
                for var in range(args.variants) for nt in nts for gx, gy in shapes]
