@@ -143,9 +143,13 @@ int rse_reconstruct_data_flat(const rse_codec *codec, void *stripes, size_t shar
  * decode-matrix inversion, composed parity rows) done by a HIP kernel: two
  * launches for the whole batch.  Errors (TooFewShardsPresent / EmptyShard for
  * the first offending stripe) are detected before any stripe is modified.
- * GF(2^8) with k <= 32 and p <= 16 runs on the device planner; other codecs
- * fall back to the host planner stripe by stripe (same results).  Returns after
- * the work is queued and the host inputs have been consumed. */
+ * Whole 16 KiB chunks of codecs with bit-sliced kernels (compiled in or run-time
+ * specialised, either field) are planned per stripe on the device (e x e
+ * syndrome inverse) and coded by the bit-sliced syndrome kernel; the rest of
+ * every shard, and other GF(2^8) codecs with k <= 32 and p <= 16, use the
+ * device planner with k x k inverses and the table kernels; anything else
+ * falls back to the host planner stripe by stripe (same results).  Returns
+ * after the work is queued and the host inputs have been consumed. */
 int rse_reconstruct_batch(const rse_codec *codec, void *stripes, size_t shard_len,
                           size_t n_stripes, const uint8_t *present, int data_only,
                           rse_stream_t stream);
