@@ -370,6 +370,17 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     dt = time.perf_counter() - t0
     out["verify"] = {"what": f"verify, {n_stripes} stripes, one call each (synchronous)",
                      "all_ok": ok, "algorithmic_GB_per_s": round(n_stripes * (k + p) * L / dt / 1e9, 1)}
+    # the same check over every stripe in one pass (rse_verify_flat)
+    assert r.verify_flat(flat, L, n_stripes).all()
+    a.record(stream)
+    for _ in range(reps):
+        oks = r.verify_flat(flat, L, n_stripes)
+    b.record(stream)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    out["verify_flat"] = {"what": f"verify_flat, {n_stripes} stripes in one pass (reads k+p shards)",
+                          "all_ok": bool(oks.all()),
+                          "algorithmic_GB_per_s": round(n_stripes * (k + p) * L / (ms * 1e-3) / 1e9, 1)}
     # end to end from pinned host memory: one stripe, H2D data, D2H parity
     hs = [v[0, i].cpu().pin_memory() for i in range(k)] + \
          [torch.empty(L, dtype=torch.uint8).pin_memory() for _ in range(p)]

@@ -132,6 +132,12 @@ int rse_reconstruct_data(const rse_codec *codec, void *const *shards, const size
  * shard_len elements laid end to end (the wasm encode() layout).  One launch. */
 int rse_encode_flat(const rse_codec *codec, void *stripes, size_t shard_len,
                     size_t n_stripes, rse_stream_t stream);
+/* verify (core.rs:637-651) of every stripe in one pass: ok[s] = 1 iff stripe
+ * s's parity matches.  Reads each shard once, writes nothing.  Synchronises
+ * `stream`.  (No reference counterpart: the crate verifies one stripe per
+ * call; this is the batched form of the same check for scrubbing.) */
+int rse_verify_flat(const rse_codec *codec, const void *stripes, size_t shard_len,
+                    size_t n_stripes, uint8_t *ok, rse_stream_t stream);
 /* Same layout; every stripe has the same erasure pattern `present[k+p]`
  * (wasm reconstruct(): reconstruct_data semantics). */
 int rse_reconstruct_data_flat(const rse_codec *codec, void *stripes, size_t shard_len,

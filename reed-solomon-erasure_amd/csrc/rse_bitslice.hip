@@ -262,6 +262,10 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_dma_kerne
     uint32_t acc[C::p * 16];
     dma_inputs<C, D, 0>(acc, ring, ring_ptr, c * C::k, c > 0, s_ops);
     store_outputs<C, true>(acc, a, off, mode, diff);
+    if (a.per_stripe && diff) {
+      atomicOr(a.mismatch + (blockIdx.x + c * gridDim.x) / chunks_per_stripe, 1u);
+      diff = false;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);

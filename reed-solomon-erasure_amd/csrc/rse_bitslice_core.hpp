@@ -246,6 +246,10 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
     if (!XC) load4<NT>(cur, a.in[0] + off);
     code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
     store_outputs<C, NT>(acc, a, off, mode, diff);
+    if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
+      atomicOr(a.mismatch + idx / chunks_per_stripe, 1u);
+      diff = false;
+    }
   }
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }
@@ -285,6 +289,10 @@ __device__ __forceinline__ void bitslice_body_deep(const CodeArgs& a, uint64_t c
       if (j < C::k) load4<NT>(buf[j], a.in[j] + off);
     code_inputs_deep<C, NT, D, 0>(acc, buf, a, off);
     store_outputs<C, NT>(acc, a, off, mode, diff);
+    if (a.per_stripe && diff) {
+      atomicOr(a.mismatch + stripe, 1u);
+      diff = false;
+    }
   }
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }

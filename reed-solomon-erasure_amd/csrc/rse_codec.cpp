@@ -117,6 +117,7 @@ struct Job {
   uint32_t* mismatch;
   uint64_t stripe_stride;
   size_t n_stripes;
+  bool per_stripe = false;  // CHECK modes: one mismatch word per stripe (verify_flat)
 };
 
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mismatch,
@@ -146,6 +147,7 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
   a.n_out = (uint32_t)no;
   a.mode = mode;
   a.accumulate = acc ? 1u : 0u;
+  a.per_stripe = j.per_stripe ? 1u : 0u;
   a.n_stripes = 0;
   hipError_t e = hipSuccess;
   for (size_t done = 0; done < j.n_stripes && e == hipSuccess;) {
@@ -154,6 +156,7 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
     e = rse::launch_code(j.field, a, s);
     done += batch;
     const uint64_t adv = (uint64_t)batch * j.stripe_stride;  // next batch's stripe 0
+    if (a.per_stripe) a.mismatch += batch;
     for (size_t i = 0; i < ni; ++i) a.in[i] += adv;
     for (size_t r = 0; r < no; ++r) {
       if (a.out[r]) a.out[r] += adv;
@@ -205,7 +208,8 @@ int run_job(const Job& j, hipStream_t s) {
   for (size_t r = 0; rc == RSE_OK && r < n_out; ++r)
     for (size_t sidx = 0; sidx < j.n_stripes && rc == RSE_OK; ++sidx) {
       const size_t off = sidx * j.stripe_stride;
-      hipError_t e = launch_compare(dst[r] + off, j.cmp[r] + off, j.len_bytes, j.mismatch, s);
+      hipError_t e = launch_compare(dst[r] + off, j.cmp[r] + off, j.len_bytes,
+                                    j.mismatch + (j.per_stripe ? sidx : 0), s);
       if (e != hipSuccess) rc = dev_fail(e);
     }
   for (void* q : owned) (void)hipFreeAsync(q, s);
@@ -227,25 +231,28 @@ hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32
   return hipGetLastError();
 }
 
-// Runs `j` in a check mode and returns the verdict (synchronises the stream).
+// Runs `j` in a check mode and returns the verdict (synchronises the stream):
+// ok[0], or ok[s] for every stripe when j.per_stripe.
 int run_check(Job j, hipStream_t s, int* ok) {
+  const size_t words = j.per_stripe ? j.n_stripes : 1;
   uint32_t* flag = nullptr;
-  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(uint32_t), s));
-  hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), s);
+  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), words * sizeof(uint32_t), s));
+  hipError_t e = hipMemsetAsync(flag, 0, words * sizeof(uint32_t), s);
   if (e != hipSuccess) {
     (void)hipFreeAsync(flag, s);
     return dev_fail(e);
   }
   j.mismatch = flag;
   int rc = run_job(j, s);
-  uint32_t h = 0;
+  std::vector<uint32_t> h(words, 0);
   if (rc == RSE_OK) {
-    e = hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s);
+    e = hipMemcpyAsync(h.data(), flag, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) rc = dev_fail(e);
   }
   (void)hipFreeAsync(flag, s);
-  if (rc == RSE_OK) *ok = h == 0 ? 1 : 0;
+  if (rc == RSE_OK)
+    for (size_t w = 0; w < words; ++w) ok[w] = h[w] == 0 ? 1 : 0;
   return rc;
 }
 
@@ -833,6 +840,32 @@ int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t 
   Job j{c->field, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
         (uint64_t)c->total * sb, n_stripes};
   return run_job(j, (hipStream_t)stream);
+}
+
+int rse_verify_flat(const rse_codec* c, const void* stripes, size_t shard_len, size_t n_stripes,
+                    uint8_t* ok, rse_stream_t stream) {
+  if (!c || !stripes || !ok) return RSE_ERR_INVALID_ARGUMENT;
+  if (shard_len == 0) return RSE_EMPTY_SHARD;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t sb = shard_len * c->esize();
+  const uint8_t* base = static_cast<const uint8_t*>(stripes);
+  std::vector<const uint8_t*> in(c->k), cmp(c->p);
+  for (size_t i = 0; i < c->k; ++i) in[i] = base + i * sb;
+  for (size_t r = 0; r < c->p; ++r) cmp[r] = base + (c->k + r) * sb;
+  want_bitslice(c, sb);
+  const Rows rows = parity_rows(c);
+  Job j{c->field, &rows, in.data(), nullptr, cmp.data(), sb, rse::kCheck, false, nullptr,
+        (uint64_t)c->total * sb, n_stripes, true};
+  std::vector<int> res;
+  try {
+    res.resize(n_stripes);
+  } catch (const std::bad_alloc&) {
+    return RSE_ERR_NO_MEMORY;
+  }
+  const int rc = run_check(j, (hipStream_t)stream, res.data());
+  if (rc == RSE_OK)
+    for (size_t s = 0; s < n_stripes; ++s) ok[s] = (uint8_t)res[s];
+  return rc;
 }
 
 int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_len,

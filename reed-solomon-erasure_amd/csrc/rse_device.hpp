@@ -128,10 +128,16 @@ __device__ __forceinline__ bool ne4(uint4 a, uint4 b) {
   return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u;
 }
 
-__device__ __forceinline__ void flag_mismatch(bool diff, uint32_t* word) {
+// The mismatch word of the stripe at byte offset soff (CodeArgs::per_stripe).
+__device__ __forceinline__ uint32_t* mismatch_word(const CodeArgs& a, uint64_t soff) {
+  return a.mismatch + ((a.per_stripe && a.stripe_stride) ? soff / a.stripe_stride : 0u);
+}
+
+// One atomic per wave that saw a difference, on the word of stripe offset soff.
+__device__ __forceinline__ void flag_mismatch(bool diff, const CodeArgs& a, uint64_t soff) {
   const unsigned long long m = __ballot(diff);
   if (m != 0ull && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
-    atomicOr(word, 1u);
+    atomicOr(mismatch_word(a, soff), 1u);
 }
 
 __device__ __forceinline__ uint32_t opaque_zero() {

@@ -116,7 +116,7 @@ __device__ __forceinline__ void gf8_span(const CodeArgs& a, const uint4* tq, con
       if (NOGUARD || (uint32_t)r < n_out)
 #pragma unroll
         for (int q = 0; q < VPL; ++q) diff |= ne4(acc[r][q], ld16<NT>(a.cmp[r] + off[q]));
-    flag_mismatch(diff, a.mismatch);
+    flag_mismatch(diff, a, soff);
   }
 }
 
@@ -178,7 +178,7 @@ __device__ __forceinline__ void gf8_code_impl(const CodeArgs& a, uint32_t stripe
       if (mode != kCheck) a.out[r][off] = (uint8_t)acc[r];
       if (mode != kStore) diff |= (uint8_t)acc[r] != a.cmp[r][off];
     }
-    if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+    if (mode != kStore && diff) atomicOr(mismatch_word(a, soff), 1u);
   }
   }  // stripe loop
 }
@@ -441,7 +441,7 @@ __device__ __forceinline__ void gf16_span(const CodeArgs& a, const uint4* tq, co
       if (mode != kStore) diff |= ne4(ov, ld16<NT>(a.cmp[r] + off[q]));
     }
   }
-  if (mode != kStore) flag_mismatch(diff, a.mismatch);
+  if (mode != kStore) flag_mismatch(diff, a, soff);
 }
 
 template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
       if (mode != kStore)
         diff |= ((uint8_t)oh[r] != a.cmp[r][off]) || ((uint8_t)ol[r] != a.cmp[r][off + 1]);
     }
-    if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+    if (mode != kStore && diff) atomicOr(mismatch_word(a, soff), 1u);
   }
   }  // stripe loop
 }
@@ -912,6 +912,7 @@ __global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
     d.mismatch = nullptr;
     d.mode = kStore;
     d.accumulate = 0;
+    d.per_stripe = 0;
   }
   __syncthreads();
   const uint32_t n_out = (uint32_t)s_nout;

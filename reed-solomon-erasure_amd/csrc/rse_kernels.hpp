@@ -45,6 +45,8 @@ struct CodeArgs {
   uint32_t n_in, n_out;
   uint32_t mode;
   uint32_t accumulate;     // 1: out[r] ^= ... (ShardByShard / chunked inputs)
+  uint32_t per_stripe;     // CHECK modes: 1 = mismatch[stripe] per stripe (verify_flat),
+                           // 0 = one mismatch word for the launch
   // GF(2^8): coef[r][i] & 0xff.  GF(2^16): (coef_of_x << 8) | constant.
   uint16_t coef[kMaxOut][kMaxIn];
 };

@@ -19,7 +19,7 @@ EXPORTS = (
     "rse_codec_total_shard_count", "rse_codec_matrix", "rse_codec_kernel_kind",
     "rse_encode", "rse_encode_sep", "rse_encode_single", "rse_encode_single_sep",
     "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
-    "rse_encode_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
+    "rse_encode_flat", "rse_verify_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
     "rse_code_shards",
     "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_encode_host_flat", "rse_fill_splitmix",
     "rse_set_option", "rse_get_option",
@@ -53,6 +53,7 @@ _SIGS = {
     "rse_reconstruct": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
     "rse_reconstruct_data": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
     "rse_encode_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _vp]),
+    "rse_verify_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
     "rse_reconstruct_data_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
     "rse_reconstruct_batch": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _c.c_int, _vp]),
     "rse_encode_host_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _vp]),

@@ -125,9 +125,9 @@ class ReedSolomon:
     def kernel_kind(self, wait: bool = False) -> str:
         """Which kernels code this codec (results are identical either way):
         bit-sliced kernels compiled into the library, bit-sliced kernels
-        specialised for this codec at run time (hiprtc, started by the
-        constructor; ``wait`` blocks until that build has finished), or the
-        table kernels."""
+        specialised for this codec at run time (hiprtc; the build starts at the
+        first call that codes a whole 16 KiB chunk, or here with ``wait``, which
+        blocks until it has finished), or the table kernels."""
         return self.KERNELS[_lib.rse_codec_kernel_kind(self._h, 1 if wait else 0)]
 
     def matrix(self) -> "list":
@@ -262,6 +262,16 @@ class ReedSolomon:
         _check_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
         _raise(_lib.rse_encode_flat(self._h, _dev(stripes), shard_len, n_stripes,
                                     _stream(stripes)))
+
+    def verify_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int = 1) -> np.ndarray:
+        """verify() (core.rs:637-651) of every stripe of the flat layout in one
+        pass; returns one bool per stripe.  Synchronous, like verify()."""
+        _check_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
+        ok = np.zeros(max(1, n_stripes), np.uint8)
+        _raise(_lib.rse_verify_flat(self._h, _dev(stripes), shard_len, n_stripes,
+                                    ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                    _stream(stripes)))
+        return ok[:n_stripes].astype(bool)
 
     def reconstruct_data_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int,
                               present: Sequence[bool]) -> None:

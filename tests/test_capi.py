@@ -136,6 +136,15 @@ def test_reconstruct_batch_validation():  # core.rs:747-772 per stripe, before a
         r.reconstruct_batch(None, 10, 2, [[True] * 5])
 
 
+def test_verify_flat_validation():  # before any device access
+    r = R.galois_8.ReedSolomon(3, 2)
+    ok = (ctypes.c_uint8 * 4)()
+    assert L.rse_verify_flat(r._h, FAKE, 0, 4, ok, None) == Error.EmptyShard
+    assert L.rse_verify_flat(r._h, FAKE, 10, 0, ok, None) == 0
+    assert L.rse_verify_flat(None, FAKE, 10, 4, ok, None) == 100
+    assert L.rse_verify_flat(r._h, FAKE, 10, 4, None, None) == 100
+
+
 def test_buffer_and_sep_validation():  # tests/mod.rs:905-964, 2304-2619
     r = R.galois_8.ReedSolomon(3, 2)
     ok = ctypes.c_int()

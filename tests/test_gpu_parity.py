@@ -798,6 +798,56 @@ def test_decode_pattern_kernels(R, field, k, p, erasures):
         lib.rse_set_option(9, old)
 
 
+@pytest.mark.parametrize("field,k,p,n", [
+    (8, 10, 4, 2 * 16384 + 48),   # bit-sliced chunks + table tail
+    (16, 20, 8, 16384 + 8),       # GF(2^16) bit-sliced + tail
+    (8, 12, 4, 16384),            # run-time specialised codec
+    (8, 3, 2, 1000),              # table kernels (exact shape)
+    (8, 7, 3, 777),               # table kernels, byte path (stride not 16-aligned)
+    (8, 40, 20, 300),             # k > 32: sums materialised, then compared per stripe
+])
+def test_verify_flat_per_stripe(R, field, k, p, n):
+    """rse_verify_flat: one pass over many stripes, one verdict per stripe
+    (core.rs:637-651 applied stripe by stripe), with corruptions in data and
+    parity shards, in bit-sliced chunks and in tails, and clean stripes."""
+    lib = R._lib.load()
+    es = field // 8
+    nb = n * es
+    T = k + p
+    stripes = 11
+    rng = np.random.default_rng(field * 100 + k + p + n)
+    oc = O.Codec(field, k, p)
+    buf = []
+    for _ in range(stripes):
+        st = rand_shards(rng, k, nb) + [np.zeros(nb, np.uint8) for _ in range(p)]
+        oc.encode(st)
+        buf.append(np.concatenate(st))
+    buf = np.concatenate(buf)
+    want = np.ones(stripes, bool)
+    v = buf.reshape(stripes, T, nb)
+    for s_ in (1, 4, 5, 9):
+        i = int(rng.integers(0, T))
+        pos = int(rng.integers(0, nb)) if s_ != 9 else nb - 1
+        v[s_, i, pos] ^= 1 + int(rng.integers(0, 255))
+        want[s_] = False
+    old = lib.rse_get_option(9)
+    try:
+        lib.rse_set_option(9, 2)
+        r = R.core.ReedSolomon(k, p, field)
+        d = dev(buf)
+        got = r.verify_flat(d, n, stripes)
+        assert (got == want).all(), (got, want)
+        # the same verdicts as verify() stripe by stripe
+        dv = d.view(stripes, T, nb)
+        shape = (n,) if field == 8 else (n, 2)
+        for s_ in range(stripes):
+            assert r.verify([dv[s_, i].view(*shape) for i in range(T)]) == want[s_]
+        # nothing was written
+        assert (host(d) == buf).all()
+    finally:
+        lib.rse_set_option(9, old)
+
+
 def test_encode_host_matches_device(R):
     rng = np.random.default_rng(23)
     k, p = 10, 4
