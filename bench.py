@@ -272,7 +272,9 @@ def main(argv=None):
 
     extras = {}
     if rank == 0 and not args.no_extras:
-        extras = extra_legs(r, v, k, p, L, min(pool, 64), stream)
+        extras = extra_legs(r, v, k, p, L, min(pool, 256), stream)
+        if (k, p, L) == (10, 4, 16 * MiB):
+            extras["other_configs"] = other_configs(stream)
 
     if rank == 0:
         launches = -(-n_local // pool)
@@ -312,6 +314,69 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
+def timed_gbps(fn, nbytes, stream, reps=5):
+    """Algorithmic GB/s (1e9) of fn() over `reps` back-to-back calls, HIP
+    events on the launch stream, after one untimed call."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(reps):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return round(nbytes / (a.elapsed_time(b) / reps * 1e-3) / 1e9, 1)
+
+
+def other_configs(stream):
+    """BASELINE.json configs[1] (galois_8 10+2 x 1 MiB) and configs[4]
+    (galois_16 20+8 x 4 MiB encode/reconstruct) on this GPU, each with stripe
+    0's parity checked against the reference digests of tests/golden."""
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix
+    lib = R_lib()
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
+    out = {}
+    for field, k, p, nbytes, stripes in ((8, 10, 2, MiB, 512), (16, 20, 8, 4 * MiB, 256)):
+        T = k + p
+        buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
+        v = buf.view(stripes, T, nbytes)
+        for s_ in range(stripes):
+            for i in range(k):
+                fill_splitmix(v[s_, i], SEED, shard_id(s_, i))
+        r = R.core.ReedSolomon(k, p, field)
+        elems = nbytes // (field // 8)
+        enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream)
+        want = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]["parity_sha256"]
+        got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
+        d = {"workload": f"gf{field} {k}+{p} x {nbytes // MiB} MiB, {stripes} stripes/launch",
+             "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
+             "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),
+             "parity_check_vs_reference": got == want}
+        if field == 16:
+            erased = [0, 1, 2, 3]
+            present = [i not in erased for i in range(T)]
+            rb = stripes * (k + len(erased)) * nbytes
+            lib.rse_set_option(11, 0)
+            d["reconstruct_4_erased_syndrome_GB_per_s"] = timed_gbps(
+                lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
+            lib.rse_set_option(11, 1)
+            old = lib.rse_get_option(9)
+            lib.rse_set_option(9, 2)
+            d["reconstruct_4_erased_cached_pattern_GB_per_s"] = timed_gbps(
+                lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
+            lib.rse_set_option(9, old)
+            ok = [hashlib.sha256(v[0, i].cpu().numpy().tobytes()).hexdigest() for i in erased]
+            d["reconstruct_check_vs_reference"] = ok == g["full_size"][f"gf16_20_8_{nbytes}"][
+                "data_sha256"][:len(erased)]
+        out[f"gf{field}_{k}_{p}"] = d
+        del buf, v
+        torch.cuda.empty_cache()
+    return out
+
+
 def R_lib():
     import reed_solomon_erasure as R
     return R._lib.load()
@@ -325,6 +390,8 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     present = [i not in (0, 1) for i in range(k + p)]
     flat = v[:n_stripes].reshape(-1)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lib = R_lib()
+    lib.rse_set_option(11, 0)  # decode-pattern kernels off: the syndrome kernel
     r.reconstruct_data_flat(flat, L, n_stripes, present)
     torch.cuda.synchronize()
     reps = 5
@@ -333,6 +400,7 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
         r.reconstruct_data_flat(flat, L, n_stripes, present)
     b.record(stream)
     torch.cuda.synchronize()
+    lib.rse_set_option(11, 1)
     ms = a.elapsed_time(b) / reps
     rb = n_stripes * (k + 2) * L
     out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased, first uses of the "
@@ -342,7 +410,6 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
     # a repeated pattern: its decode rows get their own specialised kernel
     # (rse_jit.cpp), like the reference's decode-matrix cache (core.rs:697-731);
     # RSE_OPT_JIT 2 waits for that build before timing
-    lib = R_lib()
     old = lib.rse_get_option(9)
     lib.rse_set_option(9, 2)
     p0 = lib.rse_get_option(12)
@@ -362,6 +429,8 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
         "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
         "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
     # verify (check mode: k+p reads, no writes), stripe by stripe as the API is
+    n_stripes = min(n_stripes, 64)
+    flat = v[:n_stripes].reshape(-1)
     shards = [[v[s_, i] for i in range(k + p)] for s_ in range(n_stripes)]
     assert all(r.verify(sh) for sh in shards[:2])
     torch.cuda.synchronize()
