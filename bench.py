@@ -339,7 +339,7 @@ def other_configs(stream):
     lib = R_lib()
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
     out = {}
-    for field, k, p, nbytes, stripes in ((8, 10, 2, MiB, 512), (16, 20, 8, 4 * MiB, 256)):
+    for field, k, p, nbytes, stripes in ((8, 10, 2, MiB, 2048), (16, 20, 8, 4 * MiB, 256)):
         T = k + p
         buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
         v = buf.view(stripes, T, nbytes)
