@@ -227,9 +227,15 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 // chunks of all stripes are one flat index space walked grid-stride.  a.n_vec
 // counts whole chunks' vectors only (the host codes the remainder with the
 // table kernels).  Launch bounds: kBsBlock lanes, C::p > 4 ? 2 : 3 waves/SIMD.
-template <class C, bool NT, bool SB, bool XC>
+//  XM: XCD-aware order -- workgroups are dispatched round-robin over the 8
+//      XCDs, so workgroup b (on XCD b % 8) takes slot (b % 8) * (G / 8) + b / 8
+//      and each XCD walks its own contiguous run of chunks.
+template <class C, bool NT, bool SB, bool XC, bool XM = false>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint32_t G = gridDim.x;
+  const uint32_t wg = (XM && G % 8u == 0) ? (blockIdx.x % 8u) * (G / 8u) + blockIdx.x / 8u
+                                           : blockIdx.x;
   const uint32_t mode = a.mode;
   bool diff = false;
   auto chunk_off = [&](uint64_t idx) {
@@ -237,10 +243,10 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
     return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
   };
   u32x4 cur[4];
-  if (XC && blockIdx.x < total) load4<NT>(cur, a.in[0] + chunk_off(blockIdx.x));
-  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+  if (XC && wg < total) load4<NT>(cur, a.in[0] + chunk_off(wg));
+  for (uint64_t idx = wg; idx < total; idx += G) {
     const uint64_t off = chunk_off(idx);
-    const uint64_t nidx = idx + gridDim.x;
+    const uint64_t nidx = idx + G;
     const uint64_t next_off = (XC && nidx < total) ? chunk_off(nidx) : ~0ull;
     uint32_t acc[C::p * 16];
     if (!XC) load4<NT>(cur, a.in[0] + off);
