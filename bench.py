@@ -474,11 +474,22 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
         r.encode_host_flat(hflat, L, ns)
     dt = (time.perf_counter() - t0) / reps
     ok = torch.equal(hflat.view(ns, k + p, L)[:, k:], v[:ns, k:].cpu())
+    # the PCIe ceiling in this process: one plain pinned H2D copy of the same bytes
+    dbuf = torch.empty_like(hflat, device="cuda")
+    dbuf.copy_(hflat, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dbuf.copy_(hflat, non_blocking=True)
+    torch.cuda.synchronize()
+    raw_h2d = hflat.numel() / ((time.perf_counter() - t0) / reps) / 1e9
+    del dbuf
     out["end_to_end_pinned_host_flat"] = {
         "what": f"rse_encode_host_flat, {ns} stripes from pinned host memory, one "
                 "H2D/kernel/D2H pipeline",
         "MB_per_s": round(ns * (k + p) * L / dt / MiB, 1),
-        "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1), "parity_matches_device": ok}
+        "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1),
+        "raw_pinned_h2d_copy_GB_per_s": round(raw_h2d, 1), "parity_matches_device": ok}
     return out
 
 
