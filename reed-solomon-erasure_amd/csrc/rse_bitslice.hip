@@ -148,10 +148,10 @@ struct Code {
   static constexpr Planes<F, K, P> planes{};
 };
 
-template <class C, bool NT, bool SB, bool XC, bool XM = false>
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
-  bitslice_body<C, NT, SB, XC, XM>(a, chunks_per_stripe);
+  bitslice_body<C, NT, SB, XC, XM, WT>(a, chunks_per_stripe);
 }
 
 template <class C, int D>
@@ -431,9 +431,10 @@ struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
-  BsFn fn[8][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
+  BsFn fn[9][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
                       // prefetch, 3/4 LDS-DMA input ring of 3/2 slots, 5/6 two/three
-                      // inputs in flight in VGPRs, 7 = 1 in XCD-aware order (3-7: nt only)
+                      // inputs in flight in VGPRs, 7 = 1 in XCD-aware order, 8 = 1 with
+                      // write-through (sc1) stores; [8][0] sc1, [8][1] sc1 nt
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
@@ -458,7 +459,9 @@ constexpr BsDescFn rec_desc_fn() {
     {nullptr, bitslice_dma_kernel<Code<F, K, P>, 2>},                             \
     {nullptr, bitslice_deep_kernel<Code<F, K, P>, 2>},                            \
     {nullptr, bitslice_deep_kernel<Code<F, K, P>, 3>},                            \
-    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false, true>}},          \
+    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false, true>},           \
+    {bitslice_kernel<Code<F, K, P>, false, true, false, false, true>,             \
+     bitslice_kernel<Code<F, K, P>, true, true, false, false, true>}},            \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()},                                                   \
    {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
@@ -490,7 +493,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     if (!same) break;
     // RSE_OPT_KERNEL_VARIANT picks a bit-sliced variant too (-1: default)
     const int64_t vopt = get_option(4);
-    int v = (vopt >= 0 && vopt < 8) ? (int)vopt : kBsDefaultVariant;
+    int v = (vopt >= 0 && vopt < 9) ? (int)vopt : kBsDefaultVariant;
     BsFn fn = sh.fn[v][nt ? 1 : 0];
     if (!fn) fn = sh.fn[v][1];
     hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);

@@ -143,6 +143,20 @@ __device__ __forceinline__ void stv(uint8_t* p, u32x4 v) {
   else *q = v;
 }
 
+// 16-byte store with an explicit cache policy: WT = write-through (sc1: the
+// line leaves the XCD's L2 at once instead of waiting there for eviction).
+template <bool NT, bool WT>
+__device__ __forceinline__ void stv_policy(uint8_t* p, u32x4 v) {
+  if constexpr (WT) {
+    if constexpr (NT)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    stv<NT>(p, v);
+  }
+}
+
 template <bool NT>
 __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 #pragma unroll
@@ -165,7 +179,7 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&i
 
 // Output phase of one chunk: un-slice every output's planes and store them
 // (kStore), compare them with the stored parity (kCheck), or both.
-template <class C, bool NT>
+template <class C, bool NT, bool WT = false>
 __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const CodeArgs& a,
                                               uint64_t off, uint32_t mode, bool& diff) {
 #pragma unroll
@@ -178,7 +192,7 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t o16 = off + j * (kBsBlock * 16);
-      if (mode != kCheck) stv<NT>(a.out[o] + o16, v[j]);
+      if (mode != kCheck) stv_policy<NT, WT>(a.out[o] + o16, v[j]);
       if (mode != kStore) {
         const u32x4 w = ldv<NT>(a.cmp[o] + o16);
         diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
@@ -230,7 +244,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 //  XM: XCD-aware order -- workgroups are dispatched round-robin over the 8
 //      XCDs, so workgroup b (on XCD b % 8) takes slot (b % 8) * (G / 8) + b / 8
 //      and each XCD walks its own contiguous run of chunks.
-template <class C, bool NT, bool SB, bool XC, bool XM = false>
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
   const uint32_t G = gridDim.x;
@@ -251,7 +265,7 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
     uint32_t acc[C::p * 16];
     if (!XC) load4<NT>(cur, a.in[0] + off);
     code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
-    store_outputs<C, NT>(acc, a, off, mode, diff);
+    store_outputs<C, NT, WT>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
       atomicOr(a.mismatch + idx / chunks_per_stripe, 1u);
       diff = false;
