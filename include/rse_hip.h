@@ -208,6 +208,8 @@ int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len
                                        kernel (reconstruct at encode speed); 0 off */
 #define RSE_OPT_PATTERN_LAUNCHES 12 /* read-only, per thread: reconstructs that ran on a
                                        decode-pattern kernel */
+#define RSE_OPT_JIT_CSE 13          /* GF(2^16) specialised XOR networks: up to this many shared
+                                       subexpressions per input (0..16), for modules built after */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

@@ -20,7 +20,9 @@
 namespace rse {
 namespace {
 
-constexpr int kBsDefaultVariant = 1;  // bitslice_kernel variant (tools/tune.py sweeps)
+// bitslice_kernel variant (tools/tune.py sweeps): GF(2^8) 1 (scheduling
+// barrier); GF(2^16), VALU-heavier, 0 (the scheduler's own interleaving)
+constexpr int kBsDefaultVariant8 = 1, kBsDefaultVariant16 = 0;
 
 // ----------------------------------------------------------- constexpr GF
 // GF(2^8), generating polynomial 0x11D (build.rs:11), log/exp built the way
@@ -124,28 +126,66 @@ struct Parity {
 // sel[o][i][p] = the input planes whose XOR is output plane p of the product
 // by coefficient (o, i): column q of the bit matrix is c * (element with only
 // plane q's bit set).
-template <class F, int K, int P>
+template <class F, int K, int P, bool CSE = true>
 struct Planes {
+  // GF(2^16): an input's p x 16 output planes share one group of 16 sources,
+  // so common pairs become per-input temporaries (rse_jit.cpp:
+  // eliminate_common_pairs, the same greedy rule); GF(2^8) networks are small
+  static constexpr int kTemps = (CSE && F::kPlanes == 16) ? 16 : 0;
   Parity<F, K, P> par{};
-  uint16_t sel[P][K][F::kPlanes] = {};
+  uint32_t sel[P][K][F::kPlanes] = {};
+  uint8_t ntmp[K] = {};
+  uint8_t tmp[K][kTemps > 0 ? kTemps : 1][2] = {};
   constexpr Planes() {
     for (int o = 0; o < P; ++o)
       for (int i = 0; i < K; ++i)
         for (int q = 0; q < F::kPlanes; ++q) {
           const uint16_t col = F::mul(par.m[o][i], (uint16_t)(1u << F::bit(q)));
           for (int p = 0; p < F::kPlanes; ++p)
-            if ((col >> F::bit(p)) & 1u) sel[o][i][p] |= (uint16_t)(1u << q);
+            if ((col >> F::bit(p)) & 1u) sel[o][i][p] |= 1u << q;
         }
+    for (int i = 0; i < K && kTemps > 0; ++i) {
+      int n = 0;
+      while (n < kTemps) {
+        // pair counts over the rows' set bits: cnt[a][b], a < b < 16 + n
+        uint16_t cnt[32][32] = {};
+        for (int o = 0; o < P; ++o)
+          for (int q = 0; q < F::kPlanes; ++q)
+            for (uint32_t m = sel[o][i][q]; m; m &= m - 1) {
+              const int a = __builtin_ctz(m);
+              for (uint32_t r = m & (m - 1); r; r &= r - 1) ++cnt[a][__builtin_ctz(r)];
+            }
+        int best = 0, ba = 0, bb = 0;
+        for (int a = 0; a < 16 + n; ++a)
+          for (int b = a + 1; b < 16 + n; ++b)
+            if (cnt[a][b] > best) {
+              best = cnt[a][b];
+              ba = a;
+              bb = b;
+            }
+        if (best < 3) break;
+        const uint32_t pm = (1u << ba) | (1u << bb);
+        for (int o = 0; o < P; ++o)
+          for (int q = 0; q < F::kPlanes; ++q)
+            if ((sel[o][i][q] & pm) == pm) sel[o][i][q] = (sel[o][i][q] & ~pm) | (1u << (16 + n));
+        tmp[i][n][0] = (uint8_t)ba;
+        tmp[i][n][1] = (uint8_t)bb;
+        ++n;
+      }
+      ntmp[i] = (uint8_t)n;
+    }
   }
 };
 
 // A compiled codec: NP planes per group, NG groups per lane-chunk (16 dwords).
-template <class F, int K, int P>
+// CSE = false: the plain networks (kernel variant 9, for A/B).
+template <class F, int K, int P, bool CSE = true>
 struct Code {
   using Field = F;
   static constexpr int k = K, p = P;
   static constexpr int NP = F::kPlanes, NG = 16 / F::kPlanes;
-  static constexpr Planes<F, K, P> planes{};
+  static constexpr int kTemps = Planes<F, K, P, CSE>::kTemps;
+  static constexpr Planes<F, K, P, CSE> planes{};
 };
 
 template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false>
@@ -431,10 +471,11 @@ struct BsShape {
   int field;
   uint32_t k, p;
   const uint16_t* m;  // P x K parity rows compiled into the kernel
-  BsFn fn[9][2];      // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
+  BsFn fn[10][2];     // [variant][nt]: 0 plain, 1 +sched barrier, 2 +cross-chunk
                       // prefetch, 3/4 LDS-DMA input ring of 3/2 slots, 5/6 two/three
                       // inputs in flight in VGPRs, 7 = 1 in XCD-aware order, 8 = 1 with
-                      // write-through (sc1) stores; [8][0] sc1, [8][1] sc1 nt
+                      // write-through (sc1) stores ([8][0] sc1, [8][1] sc1 nt), 9 = 1
+                      // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
@@ -461,7 +502,8 @@ constexpr BsDescFn rec_desc_fn() {
     {nullptr, bitslice_deep_kernel<Code<F, K, P>, 3>},                            \
     {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false, true>},           \
     {bitslice_kernel<Code<F, K, P>, false, true, false, false, true>,             \
-     bitslice_kernel<Code<F, K, P>, true, true, false, false, true>}},            \
+     bitslice_kernel<Code<F, K, P>, true, true, false, false, true>},             \
+    {nullptr, bitslice_kernel<Code<F, K, P, false>, true, true, false>}},         \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()},                                                   \
    {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
@@ -493,7 +535,8 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     if (!same) break;
     // RSE_OPT_KERNEL_VARIANT picks a bit-sliced variant too (-1: default)
     const int64_t vopt = get_option(4);
-    int v = (vopt >= 0 && vopt < 9) ? (int)vopt : kBsDefaultVariant;
+    int v = (vopt >= 0 && vopt < 10) ? (int)vopt
+                                     : (field == 16 ? kBsDefaultVariant16 : kBsDefaultVariant8);
     BsFn fn = sh.fn[v][nt ? 1 : 0];
     if (!fn) fn = sh.fn[v][1];
     hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);

@@ -10,9 +10,13 @@
 // matrix selects, three at a time in gfx950's v_bitop3_b32: no tables, no
 // v_perm in the network.  A codec type C supplies the matrices as constants:
 //   using Field = BitsF8 | BitsF16 (planes per group and their bit order);
-//   static constexpr int k, p, NP;
-//   static constexpr ... planes.sel[o][i][q]: bit j set iff input plane j
-//     contributes to output plane q of coefficient (o, i).
+//   static constexpr int k, p, NP, kTemps;
+//   static constexpr ... planes.sel[o][i][q]: bit j set iff source j
+//     contributes to output plane q of coefficient (o, i).  Sources 0..15 are
+//     the input's planes; with kTemps > 0, sources 16 + t are common
+//     subexpressions of that input's network, planes.tmp[i][t] = {a, b}:
+//     source a ^ source b, t < planes.ntmp[i] (computed once per input,
+//     shared by every output plane that uses them).
 //
 // Lane layout: a workgroup of 256 lanes codes a 16 KiB chunk of every shard.
 // Lane t loads the 16-byte vectors t, t+256, t+512, t+768 of the chunk (each
@@ -166,8 +170,17 @@ __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 // acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
 // every output o, group g and plane p.
 template <class C, int I, int N, int... OP>
-__device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&in)[16],
+__device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&pl)[16],
                                           int_seq<int, OP...>) {
+  uint32_t in[16 + C::kTemps];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) in[q] = pl[q];
+  if constexpr (C::kTemps > 0) {
+#pragma unroll
+    for (int t = 0; t < C::kTemps; ++t)
+      if (t < C::planes.ntmp[I])
+        in[16 + t] = in[C::planes.tmp[I][t][0]] ^ in[C::planes.tmp[I][t][1]];
+  }
   if constexpr (I == 0)
     ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),
      ...);

@@ -112,6 +112,43 @@ int recon_ns(uint32_t p, int* ns) {
   return n;
 }
 
+// Greedy common-subexpression elimination over one input's XOR network.
+// rows: the source mask of every output plane (bit j: source j, planes 0..15).
+// Repeatedly the pair of sources that occurs together in the most rows (at
+// least 3: a temporary costs one v_bitop3 and saves about half of one per row
+// that uses it, the rows absorbing two sources per op) becomes a new source
+// 16 + t, up to `budget` temporaries.
+struct Cse {
+  int n = 0;
+  uint8_t tmp[16][2] = {};
+};
+Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget) {
+  Cse c;
+  while (c.n < budget && c.n < 16) {
+    const int ns = 16 + c.n;
+    int best = 0, ba = -1, bb = -1;
+    for (int a = 0; a < ns; ++a)
+      for (int b = a + 1; b < ns; ++b) {
+        const uint32_t m = (1u << a) | (1u << b);
+        int cnt = 0;
+        for (uint32_t r : rows) cnt += (r & m) == m;
+        if (cnt > best) {
+          best = cnt;
+          ba = a;
+          bb = b;
+        }
+      }
+    if (best < 3) break;
+    const uint32_t m = (1u << ba) | (1u << bb);
+    for (uint32_t& r : rows)
+      if ((r & m) == m) r = (r & ~m) | (1u << ns);
+    c.tmp[c.n][0] = (uint8_t)ba;
+    c.tmp[c.n][1] = (uint8_t)bb;
+    ++c.n;
+  }
+  return c;
+}
+
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
@@ -130,33 +167,66 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
        "using __hip_internal::uint32_t;\nusing __hip_internal::uint64_t;\n"
        "using __hip_internal::int32_t;\n";
   s += kJitSource;
-  char buf[512];
-  std::snprintf(buf, sizeof buf,
-                "\nnamespace rse {\nnamespace {\n"
-                "struct JitPlanes {\n  uint16_t sel[%u][%u][%d];\n};\n"
-                "struct JitCode {\n  using Field = %s;\n"
-                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d;\n"
-                "  static constexpr JitPlanes planes = {{",
-                p, k, np, field == 16 ? "BitsF16" : "BitsF8", k, p, np, 16 / np);
-  s += buf;
   // sel[o][i][q]: bit j set iff input plane j feeds output plane q -- column j
   // of the bit matrix of rows[o][i] is rows[o][i] * (the element with only
   // plane j's bit set)
-  for (uint32_t o = 0; o < p; ++o) {
-    s += "{";
-    for (uint32_t i = 0; i < k; ++i) {
-      uint16_t sel[16] = {};
+  std::vector<uint32_t> sel((size_t)p * k * np, 0);
+  auto at = [&](uint32_t o, uint32_t i, int q) -> uint32_t& { return sel[((size_t)o * k + i) * np + q]; };
+  for (uint32_t o = 0; o < p; ++o)
+    for (uint32_t i = 0; i < k; ++i)
       for (int j = 0; j < np; ++j) {
         const uint16_t col = mul(rows[o * k + i], (uint16_t)(1u << bit(j)));
         for (int q = 0; q < np; ++q)
-          if ((col >> bit(q)) & 1u) sel[q] |= (uint16_t)(1u << j);
+          if ((col >> bit(q)) & 1u) at(o, i, q) |= 1u << j;
       }
+  // GF(2^16): one 16-plane group per input, so an input's p x 16 rows share
+  // their sources -- common pairs become temporaries (RSE_OPT_JIT_CSE)
+  const int budget = field == 16 ? (int)get_option(13) : 0;
+  std::vector<Cse> cse(k);
+  if (budget > 0)
+    for (uint32_t i = 0; i < k; ++i) {
+      std::vector<uint32_t> r;
+      for (uint32_t o = 0; o < p; ++o)
+        for (int q = 0; q < np; ++q) r.push_back(at(o, i, q));
+      cse[i] = eliminate_common_pairs(r, budget);
+      size_t n = 0;
+      for (uint32_t o = 0; o < p; ++o)
+        for (int q = 0; q < np; ++q) at(o, i, q) = r[n++];
+    }
+  char buf[512];
+  std::snprintf(buf, sizeof buf,
+                "\nnamespace rse {\nnamespace {\n"
+                "struct JitPlanes {\n  uint32_t sel[%u][%u][%d];\n  uint8_t ntmp[%u];\n"
+                "  uint8_t tmp[%u][%d][2];\n};\n"
+                "struct JitCode {\n  using Field = %s;\n"
+                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d;\n"
+                "  static constexpr JitPlanes planes = {{",
+                p, k, np, k, k, budget > 0 ? budget : 1, field == 16 ? "BitsF16" : "BitsF8", k, p,
+                np, 16 / np, budget > 0 ? budget : 0);
+  s += buf;
+  for (uint32_t o = 0; o < p; ++o) {
+    s += "{";
+    for (uint32_t i = 0; i < k; ++i) {
       s += "{";
       for (int q = 0; q < np; ++q) {
-        std::snprintf(buf, sizeof buf, "%u,", (unsigned)sel[q]);
+        std::snprintf(buf, sizeof buf, "%uu,", (unsigned)at(o, i, q));
         s += buf;
       }
       s += "},";
+    }
+    s += "},";
+  }
+  s += "}, {";
+  for (uint32_t i = 0; i < k; ++i) {
+    std::snprintf(buf, sizeof buf, "%d,", cse[i].n);
+    s += buf;
+  }
+  s += "}, {";
+  for (uint32_t i = 0; i < k; ++i) {
+    s += "{";
+    for (int t = 0; t < (budget > 0 ? budget : 1); ++t) {
+      std::snprintf(buf, sizeof buf, "{%d,%d},", cse[i].tmp[t][0], cse[i].tmp[t][1]);
+      s += buf;
     }
     s += "},";
   }

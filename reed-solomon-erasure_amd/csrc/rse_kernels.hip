@@ -754,6 +754,7 @@ struct Options {
   int64_t host_h2d_streams = 2;   // host pipeline H2D streams (tools/host_e2e.py)
   int64_t jit = 1;                // run-time specialised bit-sliced kernels (rse_jit.cpp)
   int64_t jit_patterns = 1;       // ... also for repeated decode patterns
+  int64_t jit_cse = 16;           // GF(2^16) specialised networks: temporaries per input
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1085,6 +1086,7 @@ int set_option(int key, int64_t value) {
     case 8: g_opt.host_h2d_streams = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 9: g_opt.jit = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case 11: g_opt.jit_patterns = value ? 1 : 0; return 0;
+    case 13: g_opt.jit_cse = value < 0 ? 0 : value > 16 ? 16 : value; return 0;
     default: return -1;
   }
 }
@@ -1104,6 +1106,7 @@ int64_t get_option(int key) {
     case 9: return g_opt.jit;
     case 10: return jit_modules_built();
     case 11: return g_opt.jit_patterns;
+    case 13: return g_opt.jit_cse;
     default: return -1;
   }
 }

@@ -565,7 +565,7 @@ def test_bitslice_kernel_variants(R, field, k, p):
     base = np.concatenate([np.concatenate(full)] * stripes)
     r = R.core.ReedSolomon(k, p, field)
     try:
-        for var in (0, 1, 2, 3, 4, 5, 6, 7, 8):
+        for var in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
             for nt in (0, 1):
                 for gx in (1, 7, 4096):
                     lib.rse_set_option(4, var)

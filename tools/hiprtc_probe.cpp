@@ -67,5 +67,9 @@ int main(int argc, char** argv) {
   const double ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::printf("ok: %zu-byte code object in %.0f ms\n", n, ms);
+  if (argc > 2) {  // write the code object (llvm-objdump -d --mcpu=gfx950 / readelf --notes)
+    std::ofstream o(argv[2], std::ios::binary);
+    o.write(code.data(), (std::streamsize)n);
+  }
   return 0;
 }

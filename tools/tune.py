@@ -42,9 +42,13 @@ def main():
     ap.add_argument("--patterns", default="1",
                     help="reconstruct: comma list of RSE_OPT_JIT_PATTERNS values (decode-pattern "
                          "kernels; the run-time builds are waited for)")
+    ap.add_argument("--jit-cse", type=int, default=-1,
+                    help="RSE_OPT_JIT_CSE for run-time specialised GF(2^16) modules (-1: default)")
     args = ap.parse_args()
     lib = R._lib.load()
     lib.rse_set_option(9, 2)  # time run-time specialised kernels, not their build
+    if args.jit_cse >= 0:
+        lib.rse_set_option(13, args.jit_cse)
     k, p, L, S = args.k, args.p, args.shard_mib * MiB, args.stripes
     buf = torch.empty(S * (k + p) * L, dtype=torch.uint8, device="cuda")
     v = buf.view(S, k + p, L)
