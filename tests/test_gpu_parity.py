@@ -947,6 +947,48 @@ def test_random_round_trips(R):  # tests/mod.rs:355-478, tests/galois_16.rs:36-1
         assert r.verify(s)
 
 
+def test_random_round_trips_bitsliced(R):
+    """Quickcheck-style round trips (tests/mod.rs:355-478) at chunk-sized
+    lengths, so that the bit-sliced kernels run: random codecs of both fields
+    with k <= 32, p <= 8 (compiled in or specialised at run time, waited for),
+    random lengths with ragged tails, random erasures rebuilt by the syndrome
+    kernels and by decode-pattern kernels; every shard against the oracle."""
+    lib = R._lib.load()
+    rng = np.random.default_rng(4242)
+    old = lib.rse_get_option(9)
+    try:
+        lib.rse_set_option(9, 2)
+        for trial in range(3):  # each codec costs a few seconds of hiprtc
+            field = 16 if trial % 2 else 8
+            k, p = int(rng.integers(1, 25)), int(rng.integers(1, 9))
+            es = field // 8
+            n = int(rng.integers(16384, 3 * 16384)) // es  # elements
+            shape = (n,) if field == 8 else (n, 2)
+            oc = O.Codec(field, k, p)
+            full = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+            oc.encode(full)
+            r = R.core.ReedSolomon(k, p, field)
+            assert r.kernel_kind(wait=True).startswith("bitslice"), (field, k, p)
+            t = [dev(x).reshape(shape) for x in full[:k]] + \
+                [torch.zeros(shape, dtype=torch.uint8, device="cuda") for _ in range(p)]
+            r.encode(t)
+            for i in range(p):
+                assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), (field, k, p, n, i)
+            assert r.verify(t)
+            for patterns in (0, 1):
+                lib.rse_set_option(11, patterns)
+                erased = rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False).tolist()
+                s_ = [x.clone() for x in t]
+                for e in erased:
+                    s_[e].random_(0, 256)
+                r.reconstruct([(x, i not in erased) for i, x in enumerate(s_)])
+                for i in range(k + p):
+                    assert torch.equal(s_[i], t[i]), (field, k, p, n, erased, patterns, i)
+    finally:
+        lib.rse_set_option(9, old)
+        lib.rse_set_option(11, 1)
+
+
 # ------------------------------------------------ every compiled variant
 @pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 10, 2), (16, 20, 8), (8, 3, 2), (8, 12, 6)])
 def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
