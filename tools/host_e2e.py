@@ -37,7 +37,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--hog-gib", type=int, default=0,
+                    help="allocate this much extra device memory first (the bench holds 112 GiB)")
+    ap.add_argument("--chunks", default="1024,2048,4096,8192,16384")
     args = ap.parse_args()
+    hog = torch.empty(args.hog_gib << 30, dtype=torch.uint8, device="cuda") if args.hog_gib else None
+    if os.environ.get("RSE_E2E_JIT_FIRST"):  # a hiprtc build in this process beforehand
+        print("jit:", R.galois_8.ReedSolomon(12, 4).kernel_kind(wait=True))
     lib = R._lib.load()
     k, p, L, S = 10, 4, 16 * MiB, args.stripes
     d = torch.empty(S * (k + p) * L, dtype=torch.uint8, device="cuda")
@@ -67,7 +73,7 @@ def main():
     t = timed(both, args.reps)
     print(f"raw H2D+D2H concurrent {2 * n / t / 1e9:6.1f} GB/s total")
     best = None
-    for chunk in (1024, 2048, 4096, 8192, 16384):
+    for chunk in [int(x) for x in args.chunks.split(",")]:
         for nh in (1, 2, 3):
             lib.rse_set_option(7, chunk)
             lib.rse_set_option(8, nh)
@@ -82,6 +88,7 @@ def main():
     print(f"best: chunk={best[1]} KiB h2d_streams={best[2]} {best[0] / 1e9:.1f} GB/s")
     lib.rse_set_option(7, 4096)
     lib.rse_set_option(8, 2)
+    del hog
 
 
 if __name__ == "__main__":
