@@ -747,7 +747,7 @@ const Variant* pick(int field, const CodeArgs& a, int64_t variant) {
 struct Options {
   int64_t nontemporal = 1;        // streaming hint on shard loads/stores
   int64_t grid_x = 0;             // blocks per stripe row (0 = auto)
-  int64_t stripes_in_flight = 1;  // gridDim.y (0 = all stripes at once)
+  int64_t stripes_in_flight = 0;  // gridDim.y (0 = all stripes at once)
   int64_t variant = -1;           // kernel variant of a tuned shape (-1 = default)
   int64_t bitslice = 1;           // bit-sliced kernels where compiled (rse_bitslice.hip)
   int64_t host_chunk_kib = 4096;  // host pipeline chunk per shard (rse_encode_host*)
@@ -1033,12 +1033,10 @@ hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream) {
   if (var->pipe) gy = 1;
   const uint64_t units = args.n_vec ? args.n_vec : (args.len + 1u);
   const uint64_t want = (units + kBlock - 1) / kBlock;
-  uint64_t gx;
-  if (g_opt.grid_x > 0) {
-    gx = (uint64_t)g_opt.grid_x;
-  } else {  // ~2048 workgroups over the chip in total, see Options
-    gx = (2048u + gy - 1) / gy;
-  }
+  // ~2048 workgroups over the chip in total, never more per stripe row than
+  // the row has vectors for (idle workgroups still build their LDS tables:
+  // 16 per row at 1 KiB shards ran 13x slower than 1, tools/small_session.sh)
+  uint64_t gx = g_opt.grid_x > 0 ? (uint64_t)g_opt.grid_x : (2048u + gy - 1) / gy;
   if (gx > want) gx = want;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(fn, dim3((uint32_t)gx, (uint32_t)gy, 1), dim3(kBlock, 1, 1), 0, stream, args);
