@@ -401,6 +401,40 @@ def test_encode_flat_many_stripes(R):
     assert torch.equal(v[:, :k], ref[:, :k])
 
 
+@pytest.mark.parametrize("field,k,p,n,stripes", [
+    (8, 10, 4, 1024, 70_000),    # > 65535 stripes in flight: the kernels' stripe loop
+    (8, 3, 2, 48, 5_000),        # tiny aligned shards
+    (8, 5, 3, 37, 3_000),        # unaligned stride: byte path
+    (16, 6, 3, 1024, 3_000),     # GF(2^16) small shards
+])
+def test_flat_small_shards_many_stripes(R, field, k, p, n, stripes):
+    """Flat encode / verify_flat / reconstruct_data_flat over many small
+    stripes (all stripes in flight on the table kernels), against the
+    oracle's encode of a sample of stripes and against stripe-by-stripe calls."""
+    rng = np.random.default_rng(field + k + n + stripes)
+    es = field // 8
+    T = k + p
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    host_buf = rng.integers(0, 256, stripes * T * n * es, dtype=np.uint8)
+    d = dev(host_buf)
+    r.encode_flat(d, n, stripes)
+    got = host(d).reshape(stripes, T, n * es)
+    for s_ in list(range(0, stripes, max(1, stripes // 40))) + [stripes - 1]:
+        want = [got[s_, i].copy() for i in range(k)] + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(want)
+        for i in range(p):
+            assert (got[s_, k + i] == want[k + i]).all(), (s_, i)
+    assert r.verify_flat(d, n, stripes).all()
+    erased = [0, k]  # a data and a parity shard of every stripe
+    v = d.view(stripes, T, n * es)
+    for e in erased:
+        v[:, e].fill_(0)
+    r.reconstruct_data_flat(d, n, stripes, [i not in erased for i in range(T)])
+    back = host(d).reshape(stripes, T, n * es)
+    assert (back[:, :k] == got[:, :k]).all()
+
+
 @pytest.mark.parametrize("field,k,p,n,stripes,bs", [
     (8, 10, 4, 4096 + 16, 33, 0),     # device planner, aligned
     (8, 10, 4, 1037, 9, 0),           # device planner, byte path
