@@ -271,7 +271,7 @@ def main(argv=None):
     value = job_throughput(args.steps, n_local, world, stripe_bytes, elapsed)
 
     extras = {}
-    if rank == 0 and not args.no_extras:
+    if rank == 0 and not args.no_extras and world == 1:  # single-GPU legs
         extras = extra_legs(r, v, k, p, L, min(pool, 256), stream)
         if (k, p, L) == (10, 4, 16 * MiB):
             extras["other_configs"] = other_configs(stream)
