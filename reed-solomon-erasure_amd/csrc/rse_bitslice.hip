@@ -188,10 +188,10 @@ struct Code {
   static constexpr Planes<F, K, P, CSE> planes{};
 };
 
-template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false>
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
-  bitslice_body<C, NT, SB, XC, XM, WT>(a, chunks_per_stripe);
+  bitslice_body<C, NT, SB, XC, XM, WT, W4>(a, chunks_per_stripe);
 }
 
 template <class C, int D>
@@ -476,6 +476,7 @@ struct BsShape {
                       // inputs in flight in VGPRs, 7 = 1 in XCD-aware order, 8 = 1 with
                       // write-through (sc1) stores ([8][0] sc1, [8][1] sc1 nt), 9 = 1
                       // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
+  BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
@@ -504,6 +505,7 @@ constexpr BsDescFn rec_desc_fn() {
     {bitslice_kernel<Code<F, K, P>, false, true, false, false, true>,             \
      bitslice_kernel<Code<F, K, P>, true, true, false, false, true>},             \
     {nullptr, bitslice_kernel<Code<F, K, P, false>, true, true, false>}},         \
+   bitslice_kernel<Code<F, K, P>, true, true, false, false, false, true>,          \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()},                                                   \
    {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
@@ -518,15 +520,15 @@ static const BsShape kBsShapes[] = {
 }  // namespace
 
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
-                           hipStream_t stream, bool* handled) {
+                           hipStream_t stream, bool* handled, uint64_t* done) {
   *handled = false;
-  if (a.accumulate || a.n_vec < kBsChunk / 16) return hipSuccess;
-  const uint64_t cps = a.n_vec / (kBsChunk / 16);
-  const uint64_t total = cps * a.n_stripes;
-  // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
-  uint64_t gx = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);
-  if (gx > total) gx = total;
-  if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+  *done = 0;
+  constexpr uint64_t kV16 = kBsChunk / 16, kV4 = 4096 / 16;  // vectors per chunk
+  if (a.accumulate || a.n_vec < kV4) return hipSuccess;
+  // the kernels for these coefficients: compiled in, or specialised at run time
+  BsFn f16 = nullptr, f4 = nullptr;
+  hipFunction_t j16 = nullptr, j4 = nullptr;
+  bool compiled = false;
   for (const BsShape& sh : kBsShapes) {
     if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
     bool same = true;  // other rows of this shape (a decode pattern) may be specialised
@@ -537,23 +539,56 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     const int64_t vopt = get_option(4);
     int v = (vopt >= 0 && vopt < 10) ? (int)vopt
                                      : (field == 16 ? kBsDefaultVariant16 : kBsDefaultVariant8);
-    BsFn fn = sh.fn[v][nt ? 1 : 0];
-    if (!fn) fn = sh.fn[v][1];
-    hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    *handled = true;
-    return hipSuccess;
+    f16 = sh.fn[v][nt ? 1 : 0];
+    if (!f16) f16 = sh.fn[v][1];
+    f4 = sh.w4;
+    compiled = true;
+    break;
   }
-  // a codec specialised at run time (rse_jit.cpp): the default variant, nt
-  JitFns jf;
-  hipError_t e = hipSuccess;
-  if (!jit_find(field, a.n_in, a.n_out, &a.coef[0][0], kMaxIn, 0, &jf, &e)) return e;
-  uint64_t cps_arg = cps;
-  void* args[] = {const_cast<CodeArgs*>(&a), &cps_arg};
-  e = hipModuleLaunchKernel(jf.enc, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args, nullptr);
-  if (e != hipSuccess) return e;
-  *handled = true;
+  if (!compiled) {  // run-time specialised (rse_jit.cpp): the default scheme, nt
+    JitFns jf;
+    hipError_t e = hipSuccess;
+    if (!jit_find(field, a.n_in, a.n_out, &a.coef[0][0], kMaxIn, 0, &jf, &e)) return e;
+    j16 = jf.enc;
+    j4 = jf.enc4;
+  }
+  // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
+  const uint64_t g0 = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);
+  auto clamp = [&](uint64_t steps) {
+    uint64_t gx = g0 < steps ? g0 : steps;
+    return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
+  };
+  auto launch = [&](BsFn f, hipFunction_t j, const CodeArgs& args, uint64_t cps, uint64_t steps) {
+    const uint64_t gx = clamp(steps);
+    if (f) {
+      hipLaunchKernelGGL(f, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, args, cps);
+      return hipGetLastError();
+    }
+    uint64_t cps_arg = cps;
+    void* argv[] = {const_cast<CodeArgs*>(&args), &cps_arg};
+    return hipModuleLaunchKernel(j, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, argv, nullptr);
+  };
+  // whole 16 KiB chunks, then whole 4 KiB chunks of the rest (one per wave)
+  const uint64_t cps16 = a.n_vec / kV16, cps4 = (a.n_vec - cps16 * kV16) / kV4;
+  if (cps16) {
+    const hipError_t e = launch(f16, j16, a, cps16, cps16 * a.n_stripes);
+    if (e != hipSuccess) return e;
+    *done = cps16 * kBsChunk;
+  }
+  if (cps4 && (f4 || j4)) {
+    CodeArgs b = a;
+    for (uint32_t i = 0; i < b.n_in; ++i) b.in[i] += *done;
+    for (uint32_t o = 0; o < b.n_out; ++o) {
+      if (b.out[o]) b.out[o] += *done;
+      if (b.cmp[o]) b.cmp[o] += *done;
+    }
+    b.n_vec -= *done / 16;
+    b.len -= *done;
+    const hipError_t e = launch(f4, j4, b, cps4, (cps4 * a.n_stripes + 3) / 4);
+    if (e != hipSuccess) return e;
+    *done += cps4 * 4096;
+  }
+  *handled = *done > 0;
   return hipSuccess;
 }
 

@@ -161,10 +161,12 @@ __device__ __forceinline__ void stv_policy(uint8_t* p, u32x4 v) {
   }
 }
 
-template <bool NT>
+// A lane's 4 vectors of one shard, S bytes apart (4 KiB: the workgroup's 256
+// lanes cover a 16 KiB chunk; 1 KiB: each wave covers its own 4 KiB chunk).
+template <bool NT, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = ldv<NT>(p + j * (kBsBlock * 16));
+  for (int j = 0; j < 4; ++j) v[j] = ldv<NT>(p + j * S);
 }
 
 // acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
@@ -192,7 +194,7 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
 
 // Output phase of one chunk: un-slice every output's planes and store them
 // (kStore), compare them with the stored parity (kCheck), or both.
-template <class C, bool NT, bool WT = false>
+template <class C, bool NT, bool WT = false, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const CodeArgs& a,
                                               uint64_t off, uint32_t mode, bool& diff) {
 #pragma unroll
@@ -204,7 +206,7 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
     unslice<typename C::Field>(pl, v);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t o16 = off + j * (kBsBlock * 16);
+      const uint64_t o16 = off + j * S;
       if (mode != kCheck) stv_policy<NT, WT>(a.out[o] + o16, v[j]);
       if (mode != kStore) {
         const u32x4 w = ldv<NT>(a.cmp[o] + o16);
@@ -221,14 +223,14 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 //      pressure heuristics), which serialises HBM latency and compute.
 //  XC: the last input prefetches input 0 of the workgroup's next chunk
 //      (next_off, ~0 if none) into cur, so the output phase overlaps it too.
-template <class C, bool NT, bool SB, bool XC, int I>
+template <class C, bool NT, bool SB, bool XC, int I, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
                                             const CodeArgs& a, uint64_t off, uint64_t next_off) {
   u32x4 nxt[4];
   if constexpr (I + 1 < C::k) {
-    load4<NT>(nxt, a.in[I + 1] + off);
+    load4<NT, S>(nxt, a.in[I + 1] + off);
   } else if constexpr (XC) {
-    if (next_off != ~0ull) load4<NT>(nxt, a.in[0] + next_off);
+    if (next_off != ~0ull) load4<NT, S>(nxt, a.in[0] + next_off);
   }
   if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   uint32_t pl[16];
@@ -241,7 +243,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   if constexpr (I + 1 < C::k) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    code_inputs<C, NT, SB, XC, I + 1>(acc, cur, a, off, next_off);
+    code_inputs<C, NT, SB, XC, I + 1, S>(acc, cur, a, off, next_off);
   } else if constexpr (XC) {
     if (next_off != ~0ull) {
 #pragma unroll
@@ -257,30 +259,42 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 //  XM: XCD-aware order -- workgroups are dispatched round-robin over the 8
 //      XCDs, so workgroup b (on XCD b % 8) takes slot (b % 8) * (G / 8) + b / 8
 //      and each XCD walks its own contiguous run of chunks.
-template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false>
+//  W4: 4 KiB chunks, one per wave (lane l loads vectors l, l+64, l+128,
+//      l+192 of its wave's chunk; each load instruction still 1 KiB
+//      contiguous), for shards -- or the rest of shards -- shorter than
+//      16 KiB; chunks_per_stripe then counts 4 KiB chunks.
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
+  static_assert(!(XC && W4), "cross-chunk prefetch is for 16 KiB chunks");
+  constexpr uint32_t S = W4 ? 1024u : kBsBlock * 16u;
+  constexpr uint64_t CH = W4 ? 4096u : kBsChunk;
   const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint64_t steps = W4 ? (total + 3) / 4 : total;
+  const uint32_t sub = W4 ? threadIdx.x >> 6 : 0u;  // wave-uniform
+  const uint32_t lane_off = (W4 ? (threadIdx.x & 63u) : threadIdx.x) * 16u;
   const uint32_t G = gridDim.x;
   const uint32_t wg = (XM && G % 8u == 0) ? (blockIdx.x % 8u) * (G / 8u) + blockIdx.x / 8u
                                            : blockIdx.x;
   const uint32_t mode = a.mode;
   bool diff = false;
-  auto chunk_off = [&](uint64_t idx) {
-    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+  auto chunk_off = [&](uint64_t c) {
+    const uint64_t stripe = c / chunks_per_stripe, chunk = c - stripe * chunks_per_stripe;
+    return stripe * a.stripe_stride + chunk * CH + lane_off;
   };
   u32x4 cur[4];
-  if (XC && wg < total) load4<NT>(cur, a.in[0] + chunk_off(wg));
-  for (uint64_t idx = wg; idx < total; idx += G) {
-    const uint64_t off = chunk_off(idx);
+  if (XC && wg < total) load4<NT, S>(cur, a.in[0] + chunk_off(wg));
+  for (uint64_t idx = wg; idx < steps; idx += G) {
+    const uint64_t c = W4 ? idx * 4 + sub : idx;
+    if (W4 && c >= total) continue;  // the last step's spare waves
+    const uint64_t off = chunk_off(c);
     const uint64_t nidx = idx + G;
     const uint64_t next_off = (XC && nidx < total) ? chunk_off(nidx) : ~0ull;
     uint32_t acc[C::p * 16];
-    if (!XC) load4<NT>(cur, a.in[0] + off);
-    code_inputs<C, NT, SB, XC, 0>(acc, cur, a, off, next_off);
-    store_outputs<C, NT, WT>(acc, a, off, mode, diff);
+    if (!XC) load4<NT, S>(cur, a.in[0] + off);
+    code_inputs<C, NT, SB, XC, 0, S>(acc, cur, a, off, next_off);
+    store_outputs<C, NT, WT, S>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
-      atomicOr(a.mismatch + idx / chunks_per_stripe, 1u);
+      atomicOr(a.mismatch + c / chunks_per_stripe, 1u);
       diff = false;
     }
   }

@@ -238,6 +238,13 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   "  rse::bitslice_body<rse::JitCode, true, true, false>(a, cps);\n}\n",
                   p > 4 ? 2 : 3);
     s += buf;
+    std::snprintf(buf, sizeof buf,
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode4(\n"
+                  "    const rse::CodeArgs a, uint64_t cps) {\n"
+                  "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, true>(a, cps);"
+                  "\n}\n",
+                  p > 4 ? 2 : 3);
+    s += buf;
     return s;
   }
   int ns[5];
@@ -416,6 +423,7 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
     JitFns f = l->fns;
     if (stage == kEnc) {
       if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
+      if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4, m, "rse_jit_encode4");
     } else {
       f.n_rec = recon_ns(p, f.rec_ns);
       for (int q = 0; q < f.n_rec && he == hipSuccess; ++q) {

@@ -1001,14 +1001,13 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
     return hipErrorInvalidValue;
   if (g_opt.bitslice) {
     bool handled = false;
+    uint64_t done = 0;
     hipError_t e = launch_bitslice(field, args, g_opt.nontemporal != 0, g_opt.grid_x, stream,
-                                   &handled);
+                                   &handled, &done);
     if (e != hipSuccess) return e;
     if (handled) {
       ++g_bs_launches;
-      // the bit-sliced kernel codes whole chunks; the rest goes to the table kernels
-      const uint64_t cb = bitslice_chunk_bytes();
-      const uint64_t done = (args.n_vec * 16u / cb) * cb;
+      // the bit-sliced kernels code whole chunks; the rest goes to the table kernels
       if (done == args.len) return hipSuccess;
       CodeArgs r = args;
       for (uint32_t i = 0; i < r.n_in; ++i) r.in[i] += done;

@@ -95,11 +95,12 @@ hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present,
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
 
 // Bit-sliced kernels (rse_bitslice.hip) for codecs whose parity rows are
-// compiled in or were specialised at run time (rse_jit.cpp): sets *handled when
-// it launched (whole 16 KiB chunks of every shard only -- the caller codes the
-// rest).
+// compiled in or were specialised at run time (rse_jit.cpp): the whole 16 KiB
+// chunks of every shard, then the whole 4 KiB chunks of the rest.  Sets
+// *handled when it launched and *done to the bytes of every shard coded (the
+// caller codes the rest).
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
-                           hipStream_t stream, bool* handled);
+                           hipStream_t stream, bool* handled, uint64_t* done);
 uint64_t bitslice_chunk_bytes();
 // 1 if (field, k, p) has bit-sliced kernels compiled into the library.
 int bitslice_compiled(int field, uint32_t k, uint32_t p);
@@ -142,6 +143,7 @@ int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool w
 int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 struct JitFns {
   hipFunction_t enc = nullptr;  // bitslice encode/verify (CodeArgs, chunks per stripe)
+  hipFunction_t enc4 = nullptr; // ... over 4 KiB chunks, one per wave
   int n_rec = 0;
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)

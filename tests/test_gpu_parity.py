@@ -527,7 +527,8 @@ def test_reconstruct_batch_many_stripes_and_errors(R):
 
 
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
-@pytest.mark.parametrize("chunks,extra", [(1, 0), (3, 16), (2, 2), (6, 1717)])
+@pytest.mark.parametrize("chunks,extra", [(1, 0), (3, 16), (2, 2), (6, 1717),
+                                          (0, 4096), (1, 12336), (2, 8194)])  # 4 KiB chunks
 def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra):
     """The bit-sliced kernels (compiled-in parity rows) against the table
     kernels and the oracle: encode (whole 16 KiB chunks bit-sliced, the rest
