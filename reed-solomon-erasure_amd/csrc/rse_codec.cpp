@@ -269,10 +269,10 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
 // Codecs without compiled-in bit-sliced kernels get them built for their
 // parity rows at run time (rse_jit.cpp: hiprtc on a background thread, host
 // CPU only).  The first call that codes at least one whole bit-sliced chunk
-// requests it, so codecs only ever used on short shards never pay for a build.
+// (4 KiB: the per-wave chunks) requests it, so codecs only ever used on short
+// shards never pay for a build.
 void want_bitslice(const rse_codec* c, size_t len_bytes) {
-  if (len_bytes < rse::bitslice_chunk_bytes() || c->jit_requested.load(std::memory_order_relaxed))
-    return;
+  if (len_bytes < 4096 || c->jit_requested.load(std::memory_order_relaxed)) return;
   c->jit_requested.store(true, std::memory_order_relaxed);
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p) || c->k > (size_t)kMaxIn ||
       c->p > rse::kJitMaxOut)
