@@ -80,7 +80,7 @@ size_t rse_codec_parity_shard_count(const rse_codec *codec); /* core.rs:473 */
 size_t rse_codec_total_shard_count(const rse_codec *codec);  /* core.rs:477 */
 /* Copy the (k+p) x k encoding matrix, row-major, elem bytes per element. */
 int rse_codec_matrix(const rse_codec *codec, uint8_t *out, size_t out_bytes);
-/* Which kernels code this codec's whole 16 KiB chunks (no reference counterpart;
+/* Which kernels code this codec's whole 16 KiB and 4 KiB chunks (no reference counterpart;
  * results are identical either way).  Codecs other than the compiled-in ones
  * with p <= 8 and k <= 32 get bit-sliced kernels specialised at run time:
  * rse_codec_new starts a hiprtc compile of the codec's parity rows on a

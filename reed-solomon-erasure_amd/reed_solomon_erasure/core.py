@@ -126,7 +126,7 @@ class ReedSolomon:
         """Which kernels code this codec (results are identical either way):
         bit-sliced kernels compiled into the library, bit-sliced kernels
         specialised for this codec at run time (hiprtc; the build starts at the
-        first call that codes a whole 16 KiB chunk, or here with ``wait``, which
+        first call that codes a whole 4 KiB chunk, or here with ``wait``, which
         blocks until it has finished), or the table kernels."""
         return self.KERNELS[_lib.rse_codec_kernel_kind(self._h, 1 if wait else 0)]
 
