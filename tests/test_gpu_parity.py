@@ -1024,6 +1024,53 @@ def test_random_round_trips_bitsliced(R):
         lib.rse_set_option(11, 1)
 
 
+def test_concurrent_threads_and_streams(R):
+    """ReedSolomon is Sync (core.rs:349: the decode-matrix cache is behind a
+    mutex): one codec shared by 4 host threads, each on its own HIP stream,
+    encoding and reconstructing its own stripes (ctypes drops the GIL for the
+    calls) -- every result the oracle's, and the run-time build of a codec
+    requested by all threads at once happens once."""
+    import threading
+    lib = R._lib.load()
+    k, p, n = 12, 4, 3 * 16384 + 4096 + 7
+    oc = O.Codec(8, k, p)
+    r = R.galois_8.ReedSolomon(k, p)
+    built0 = lib.rse_get_option(10)
+    errors = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(100 + t)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                for it in range(6):
+                    data = rand_shards(rng, k, n)
+                    want = data + [np.zeros(n, np.uint8) for _ in range(p)]
+                    oc.encode(want)
+                    sh = [dev(x) for x in data] + [torch.zeros(n, dtype=torch.uint8, device="cuda")
+                                                   for _ in range(p)]
+                    r.encode(sh)
+                    erased = rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False).tolist()
+                    for e in erased:
+                        sh[e].fill_(0)
+                    r.reconstruct([(x, i not in erased) for i, x in enumerate(sh)])
+                    st.synchronize()
+                    for i in range(k + p):
+                        if not (sh[i].cpu().numpy() == want[i]).all():
+                            errors.append((t, it, i))
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    r.kernel_kind(wait=True)
+    assert lib.rse_get_option(10) - built0 <= 2 + 8  # codec modules once (+ any patterns)
+
+
 # ------------------------------------------------ every compiled variant
 @pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 10, 2), (16, 20, 8), (8, 3, 2), (8, 12, 6)])
 def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
