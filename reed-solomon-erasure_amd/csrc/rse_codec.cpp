@@ -231,29 +231,57 @@ hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32
   return hipGetLastError();
 }
 
+// Per-thread, per-device verdict words for run_check: a device array the
+// kernels OR into and a pinned host copy, allocated once and grown on demand
+// (verify is synchronous, so a thread's buffers are free again when it
+// returns).  Deliberately never freed: a thread_local destructor could run
+// after the HIP runtime has shut down.
+struct CheckWords {
+  uint32_t* d = nullptr;
+  uint32_t* h = nullptr;
+  size_t words = 0;
+};
+
+hipError_t check_words(size_t words, CheckWords** out) {
+  constexpr int kMaxDev = 64;
+  thread_local CheckWords per_dev[kMaxDev];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+  CheckWords& w = per_dev[dev];
+  if (w.words < words) {
+    const size_t n = std::max<size_t>(words, 256);
+    uint32_t *d = nullptr, *h = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&d), n * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(reinterpret_cast<void**>(&h), n * sizeof(uint32_t), hipHostMallocDefault);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return e;
+    }
+    if (w.d) (void)hipFree(w.d);  // the previous call has synchronised
+    if (w.h) (void)hipHostFree(w.h);
+    w = CheckWords{d, h, n};
+  }
+  *out = &w;
+  return hipSuccess;
+}
+
 // Runs `j` in a check mode and returns the verdict (synchronises the stream):
 // ok[0], or ok[s] for every stripe when j.per_stripe.
 int run_check(Job j, hipStream_t s, int* ok) {
   const size_t words = j.per_stripe ? j.n_stripes : 1;
-  uint32_t* flag = nullptr;
-  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), words * sizeof(uint32_t), s));
-  hipError_t e = hipMemsetAsync(flag, 0, words * sizeof(uint32_t), s);
-  if (e != hipSuccess) {
-    (void)hipFreeAsync(flag, s);
-    return dev_fail(e);
-  }
-  j.mismatch = flag;
+  CheckWords* w = nullptr;
+  RSE_HIP(check_words(words, &w));
+  RSE_HIP(hipMemsetAsync(w->d, 0, words * sizeof(uint32_t), s));
+  j.mismatch = w->d;
   int rc = run_job(j, s);
-  std::vector<uint32_t> h(words, 0);
-  if (rc == RSE_OK) {
-    e = hipMemcpyAsync(h.data(), flag, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) rc = dev_fail(e);
-  }
-  (void)hipFreeAsync(flag, s);
-  if (rc == RSE_OK)
-    for (size_t w = 0; w < words; ++w) ok[w] = h[w] == 0 ? 1 : 0;
-  return rc;
+  if (rc != RSE_OK) return rc;
+  RSE_HIP(hipMemcpyAsync(w->h, w->d, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  RSE_HIP(hipStreamSynchronize(s));
+  for (size_t i = 0; i < words; ++i) ok[i] = w->h[i] == 0 ? 1 : 0;
+  return RSE_OK;
 }
 
 Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
