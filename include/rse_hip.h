@@ -81,10 +81,12 @@ size_t rse_codec_total_shard_count(const rse_codec *codec);  /* core.rs:477 */
 /* Copy the (k+p) x k encoding matrix, row-major, elem bytes per element. */
 int rse_codec_matrix(const rse_codec *codec, uint8_t *out, size_t out_bytes);
 /* Which kernels code this codec's whole 16 KiB and 4 KiB chunks (no reference counterpart;
- * results are identical either way).  Codecs other than the compiled-in ones
- * with p <= 8 and k <= 32 get bit-sliced kernels specialised at run time:
- * rse_codec_new starts a hiprtc compile of the codec's parity rows on a
- * background thread (host CPU only).  wait != 0 blocks until it has finished. */
+ * results are identical either way).  Codecs other than the compiled-in ones get
+ * bit-sliced kernels specialised at run time: the first call that codes at least
+ * 4 KiB per shard (or this call with wait != 0) starts a hiprtc compile of the
+ * codec's parity rows on a background thread (host CPU only) -- one module for
+ * p <= 8 and k <= 32, one per 8 x 32 block of the rows otherwise.  wait != 0
+ * blocks until every build has finished. */
 #define RSE_KERNELS_TABLE 0             /* table kernels (rse_kernels.hip) */
 #define RSE_KERNELS_COMPILED 1          /* bit-sliced, compiled into the library */
 #define RSE_KERNELS_SPECIALISED 2       /* bit-sliced, specialised at run time, ready */

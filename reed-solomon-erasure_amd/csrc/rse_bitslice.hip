@@ -275,7 +275,7 @@ __device__ __forceinline__ void dma_inputs(uint32_t (&acc)[C::p * 16], const Dma
     for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const u32x4*>(slot + j * 1024);
     uint32_t pl[16];
     slice<typename C::Field>(cur, pl);
-    mac_input<C, I>(acc, pl, make_int_seq<C::p * 16>{});
+    mac_input<C, I, false>(acc, pl, make_int_seq<C::p * 16>{});
 #pragma unroll
     for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
     dma_inputs<C, D, I + 1>(acc, ring, ring_ptr, g0, after_chunk, s_ops);
@@ -524,12 +524,14 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   *handled = false;
   *done = 0;
   constexpr uint64_t kV16 = kBsChunk / 16, kV4 = 4096 / 16;  // vectors per chunk
-  if (a.accumulate || a.n_vec < kV4) return hipSuccess;
+  // accumulate: store mode on a wide codec's block kernels (kJitBlock) only
+  if (a.n_vec < kV4 || (a.accumulate && a.mode != kStore)) return hipSuccess;
   // the kernels for these coefficients: compiled in, or specialised at run time
   BsFn f16 = nullptr, f4 = nullptr;
   hipFunction_t j16 = nullptr, j4 = nullptr;
   bool compiled = false;
   for (const BsShape& sh : kBsShapes) {
+    if (a.accumulate) break;
     if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
     bool same = true;  // other rows of this shape (a decode pattern) may be specialised
     for (uint32_t o = 0; o < sh.p && same; ++o)
@@ -548,9 +550,11 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   if (!compiled) {  // run-time specialised (rse_jit.cpp): the default scheme, nt
     JitFns jf;
     hipError_t e = hipSuccess;
-    if (!jit_find(field, a.n_in, a.n_out, &a.coef[0][0], kMaxIn, 0, &jf, &e)) return e;
-    j16 = jf.enc;
-    j4 = jf.enc4;
+    if (!jit_find(field, a.n_in, a.n_out, &a.coef[0][0], kMaxIn, 0, &jf, &e, a.accumulate != 0))
+      return e;
+    j16 = a.accumulate ? jf.enc_acc : jf.enc;
+    j4 = a.accumulate ? jf.enc4_acc : jf.enc4;
+    if (!j16) return hipSuccess;
   }
   // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
   const uint64_t g0 = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);

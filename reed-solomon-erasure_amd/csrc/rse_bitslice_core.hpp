@@ -171,7 +171,9 @@ __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 
 // acc[o*16 + g*NP + p] (^)= plane combination of group g of input I, for
 // every output o, group g and plane p.
-template <class C, int I, int N, int... OP>
+// ACC: the accumulators already hold a partial sum (accumulate mode), so
+// input 0 adds to them like every other input.
+template <class C, int I, bool ACC, int N, int... OP>
 __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&pl)[16],
                                           int_seq<int, OP...>) {
   uint32_t in[16 + C::kTemps];
@@ -183,7 +185,7 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
       if (t < C::planes.ntmp[I])
         in[16 + t] = in[C::planes.tmp[I][t][0]] ^ in[C::planes.tmp[I][t][1]];
   }
-  if constexpr (I == 0)
+  if constexpr (I == 0 && !ACC)
     ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),
      ...);
   else
@@ -223,7 +225,8 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 //      pressure heuristics), which serialises HBM latency and compute.
 //  XC: the last input prefetches input 0 of the workgroup's next chunk
 //      (next_off, ~0 if none) into cur, so the output phase overlaps it too.
-template <class C, bool NT, bool SB, bool XC, int I, uint32_t S = kBsBlock * 16>
+template <class C, bool NT, bool SB, bool XC, int I, uint32_t S = kBsBlock * 16,
+          bool ACC = false>
 __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
                                             const CodeArgs& a, uint64_t off, uint64_t next_off) {
   u32x4 nxt[4];
@@ -235,7 +238,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   uint32_t pl[16];
   slice<typename C::Field>(cur, pl);
-  mac_input<C, I>(acc, pl, make_int_seq<C::p * 16>{});
+  mac_input<C, I, ACC>(acc, pl, make_int_seq<C::p * 16>{});
   // keep each input's XORs together: without this the compiler reassociates
   // across inputs and keeps several inputs' planes live (spills)
 #pragma unroll
@@ -243,7 +246,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   if constexpr (I + 1 < C::k) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    code_inputs<C, NT, SB, XC, I + 1, S>(acc, cur, a, off, next_off);
+    code_inputs<C, NT, SB, XC, I + 1, S, ACC>(acc, cur, a, off, next_off);
   } else if constexpr (XC) {
     if (next_off != ~0ull) {
 #pragma unroll
@@ -263,9 +266,14 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 //      l+192 of its wave's chunk; each load instruction still 1 KiB
 //      contiguous), for shards -- or the rest of shards -- shorter than
 //      16 KiB; chunks_per_stripe then counts 4 KiB chunks.
-template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false>
+//  ACC: accumulate mode (a.accumulate): the outputs' current bytes are
+//      loaded and sliced into the accumulators first -- the blocks of a wide
+//      codec's parity matrix, input chunk after input chunk (rse_jit.cpp).
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false,
+          bool ACC = false>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
   static_assert(!(XC && W4), "cross-chunk prefetch is for 16 KiB chunks");
+  static_assert(!(XC && ACC), "cross-chunk prefetch is for store mode");
   constexpr uint32_t S = W4 ? 1024u : kBsBlock * 16u;
   constexpr uint64_t CH = W4 ? 4096u : kBsChunk;
   const uint64_t total = chunks_per_stripe * a.n_stripes;
@@ -291,7 +299,18 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
     const uint64_t next_off = (XC && nidx < total) ? chunk_off(nidx) : ~0ull;
     uint32_t acc[C::p * 16];
     if (!XC) load4<NT, S>(cur, a.in[0] + off);
-    code_inputs<C, NT, SB, XC, 0, S>(acc, cur, a, off, next_off);
+    if constexpr (ACC) {
+#pragma unroll
+      for (int o = 0; o < C::p; ++o) {
+        u32x4 t[4];
+        load4<NT, S>(t, a.out[o] + off);
+        uint32_t pl[16];
+        slice<typename C::Field>(t, pl);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[o * 16 + q] = pl[q];
+      }
+    }
+    code_inputs<C, NT, SB, XC, 0, S, ACC>(acc, cur, a, off, next_off);
     store_outputs<C, NT, WT, S>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
       atomicOr(a.mismatch + c / chunks_per_stripe, 1u);
@@ -313,7 +332,7 @@ __device__ __forceinline__ void code_inputs_deep(uint32_t (&acc)[C::p * 16],
     __builtin_amdgcn_sched_barrier(0);
     uint32_t pl[16];
     slice<typename C::Field>(buf[I % (D + 1)], pl);
-    mac_input<C, I>(acc, pl, make_int_seq<C::p * 16>{});
+    mac_input<C, I, false>(acc, pl, make_int_seq<C::p * 16>{});
 #pragma unroll
     for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
     code_inputs_deep<C, NT, D, I + 1>(acc, buf, a, off);
@@ -374,7 +393,7 @@ __device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&c
       if constexpr (I < C::k) {
         // every sigma row, needed or not: straight-line XOR networks (a
         // branch per row costs more in register pressure than the XORs)
-        mac_input<C, I>(acc, pl, make_int_seq<NS * 16>{});
+        mac_input<C, I, false>(acc, pl, make_int_seq<NS * 16>{});
       } else {  // syndrome: s_r = sigma_r ^ parity_r (slicing is linear)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[(I - C::k) * 16 + q] ^= pl[q];

@@ -173,8 +173,16 @@ int run_job(const Job& j, hipStream_t s) {
   if (n_out == 0 || j.len_bytes == 0) return RSE_OK;
   const bool single_in = n_in <= (size_t)kMaxIn;
   if (j.mode == rse::kStore || single_in) {
-    for (size_t o0 = 0; o0 < n_out; o0 += kMaxOut) {
-      const size_t no = std::min<size_t>(kMaxOut, n_out - o0);
+    // a wide codec's parity rows whose bit-sliced blocks are built (see
+    // want_bitslice): launch them block by block, 8 outputs at a time
+    size_t step = kMaxOut;
+    if ((n_in > (size_t)kMaxIn || n_out > rse::kJitMaxOut) && j.len_bytes >= 4096 &&
+        rse::get_option(5) != 0 &&
+        rse::jit_blocks_status(j.field, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data(),
+                               false) == 2)
+      step = rse::kJitMaxOut;
+    for (size_t o0 = 0; o0 < n_out; o0 += step) {
+      const size_t no = std::min<size_t>(step, n_out - o0);
       for (size_t i0 = 0; i0 < n_in; i0 += kMaxIn) {
         const size_t ni = std::min<size_t>(kMaxIn, n_in - i0);
         RSE_HIP(run_chunk(j, o0, no, i0, ni, j.mode, j.accumulate || i0 > 0, s));
@@ -298,15 +306,18 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
 // parity rows at run time (rse_jit.cpp: hiprtc on a background thread, host
 // CPU only).  The first call that codes at least one whole bit-sliced chunk
 // (4 KiB: the per-wave chunks) requests it, so codecs only ever used on short
-// shards never pay for a build.
+// shards never pay for a build.  Wide codecs (k > 32 or p > 8) get one
+// kernel pair per 8 x 32 block of their parity rows instead (store and
+// accumulate mode; run_job launches them block by block).
 void want_bitslice(const rse_codec* c, size_t len_bytes) {
   if (len_bytes < 4096 || c->jit_requested.load(std::memory_order_relaxed)) return;
   c->jit_requested.store(true, std::memory_order_relaxed);
-  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p) || c->k > (size_t)kMaxIn ||
-      c->p > rse::kJitMaxOut)
-    return;
+  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
-  rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), true);
+  if (c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut)
+    rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data());
+  else
+    rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
 }
 
 Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, core.rs:492-509
@@ -591,7 +602,7 @@ bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes)
       c->k > (size_t)kMaxIn || (mode < 2 && plan.pattern_uses < 2))
     return false;
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
-  if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), false)) return false;
+  if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), rse::kJitPattern)) return false;
   return rse::jit_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
 }
 
@@ -767,7 +778,11 @@ int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes());
   const Rows rows = parity_rows(c);
-  switch (rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), wait != 0)) {
+  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
+  switch (wide ? rse::jit_blocks_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
+                                        wait != 0)
+               : rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
+                                 wait != 0)) {
     case 2: return RSE_KERNELS_SPECIALISED;
     case 1: return RSE_KERNELS_SPECIALISING;
     case -1: return RSE_KERNELS_SPECIALISE_FAILED;

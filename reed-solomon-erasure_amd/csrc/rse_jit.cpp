@@ -59,7 +59,8 @@ struct Entry {
   int field = 0;
   uint32_t k = 0, p = 0;
   std::vector<uint16_t> rows;  // p x k: a codec's parity rows, or a decode pattern's rows
-  int stages = 2;              // kEnc only (decode pattern) or kEnc + kRec (codec)
+  JitKind kind = kJitCodec;
+  int stages = 2;              // kEnc only (decode pattern, block) or kEnc + kRec (codec)
   std::promise<std::shared_ptr<const Compiled>> promise[2];
   std::shared_future<std::shared_ptr<const Compiled>> built[2];
   std::mutex mu;  // guards loaded
@@ -77,6 +78,8 @@ std::deque<Entry*> g_jobs[2];  // per stage; every encode job runs before any re
 std::atomic<int64_t> g_built{0};
 int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
 constexpr int kMaxPatterns = 64;
+int g_blocks = 0;  // wide-codec block entries (capped: kMaxBlocks)
+constexpr int kMaxBlocks = 256;
 constexpr size_t kMaxPendingPatternJobs = 8;
 
 std::vector<std::unique_ptr<Entry>>& registry() {
@@ -91,16 +94,22 @@ bool same_rows(const Entry& e, const uint16_t* rows, size_t stride) {
   return true;
 }
 
-// Caller holds g_mu.
-Entry* find_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride) {
+// Caller holds g_mu.  want >= 0: only entries of that kind match; -2: any
+// but kJitBlockAcc (the kernels for store and check modes).
+Entry* find_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride,
+                   int want = -1) {
   for (auto& e : registry())
-    if (e->field == field && e->k == k && e->p == p && same_rows(*e, rows, stride)) return e.get();
+    if (e->field == field && e->k == k && e->p == p &&
+        (want == -1 || (want == -2 ? e->kind != kJitBlockAcc : e->kind == want)) &&
+        same_rows(*e, rows, stride))
+      return e.get();
   return nullptr;
 }
 
-Entry* find_entry(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride) {
+Entry* find_entry(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride,
+                  int want = -1) {
   std::lock_guard<std::mutex> g(g_mu);
-  return find_locked(field, k, p, rows, stride);
+  return find_locked(field, k, p, rows, stride, want);
 }
 
 // Sigma-row counts of the reconstruct kernels: 1, 2, 4, 8 up to p, and p.
@@ -152,7 +161,7 @@ Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget) {
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage) {
+                        int stage, JitKind kind) {
   const int np = field == 16 ? 16 : 8;
   auto bit = [&](int q) { return field == 16 ? (q ^ 8) : q; };
   auto mul = [&](uint16_t a, uint16_t b) {
@@ -232,19 +241,19 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   }
   s += "}};\n};\n}  // namespace\n}  // namespace rse\n";
   if (stage == kEnc) {
-    std::snprintf(buf, sizeof buf,
-                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode(\n"
-                  "    const rse::CodeArgs a, uint64_t cps) {\n"
-                  "  rse::bitslice_body<rse::JitCode, true, true, false>(a, cps);\n}\n",
-                  p > 4 ? 2 : 3);
-    s += buf;
-    std::snprintf(buf, sizeof buf,
-                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode4(\n"
-                  "    const rse::CodeArgs a, uint64_t cps) {\n"
-                  "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, true>(a, cps);"
-                  "\n}\n",
-                  p > 4 ? 2 : 3);
-    s += buf;
+    // encode/verify kernels (16 KiB and 4 KiB chunks); a later block of a wide
+    // codec: the same adding to the outputs' bytes instead
+    const bool acc = kind == kJitBlockAcc;
+    for (int w4 = 0; w4 < 2; ++w4) {
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode%s%s(\n"
+                    "    const rse::CodeArgs a, uint64_t cps) {\n"
+                    "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, %s, %s>"
+                    "(a, cps);\n}\n",
+                    p > 4 ? 2 : 3, w4 ? "4" : "", acc ? "_acc" : "", w4 ? "true" : "false",
+                    acc ? "true" : "false");
+      s += buf;
+    }
     return s;
   }
   int ns[5];
@@ -268,7 +277,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
 
 std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
   auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage);
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind);
   const auto t0 = std::chrono::steady_clock::now();
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "rse_jit.hip", 0, nullptr, nullptr) !=
@@ -292,7 +301,8 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
   if (const char* dir = std::getenv("RSE_JIT_DUMP")) {  // debugging aid
     char path[1024];
     std::snprintf(path, sizeof path, "%s/rse_jit_gf%d_%u_%u_%s_%p.hip", dir, e.field, e.k, e.p,
-                  stage == kEnc ? "encode" : "reconstruct", (const void*)&e);
+                  stage == kEnc ? (e.kind == kJitBlockAcc ? "block_acc" : "encode") : "reconstruct",
+                  (const void*)&e);
     if (FILE* f = std::fopen(path, "w")) {
       std::fputs(src.c_str(), f);
       std::fprintf(f, "\n/* %s, %.0f ms\n%s\n*/\n", out->ok ? "ok" : "FAILED", out->ms,
@@ -348,38 +358,38 @@ Worker& worker() {
   return w;
 }
 
-}  // namespace
-
-int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool with_recon) {
-  if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || k > (uint32_t)kMaxIn ||
-      p == 0 || p > kJitMaxOut || (with_recon && bitslice_compiled(field, k, p)))
-    return 0;
-  registry();
-  Worker& w = worker();
-  std::lock_guard<std::mutex> g(g_mu);
-  if (find_locked(field, k, p, rows, k)) return 1;
-  if (!with_recon &&
-      (g_patterns >= kMaxPatterns || g_jobs[kEnc].size() >= kMaxPendingPatternJobs))
-    return 0;  // decode patterns are an optimisation: never queue without bound
+// Caller holds g_mu; rows[o * stride + i].  Queues the entry's builds.
+void add_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride,
+                JitKind kind) {
   auto e = std::make_unique<Entry>();
   e->field = field;
   e->k = k;
   e->p = p;
-  e->stages = with_recon ? 2 : 1;
-  e->rows.assign(rows, rows + (size_t)k * p);
+  e->kind = kind;
+  e->stages = kind == kJitCodec ? 2 : 1;
+  e->rows.resize((size_t)k * p);
+  for (uint32_t o = 0; o < p; ++o)
+    for (uint32_t i = 0; i < k; ++i) e->rows[o * k + i] = rows[o * stride + i];
   for (int st = 0; st < e->stages; ++st) {
     e->built[st] = e->promise[st].get_future().share();
     g_jobs[st].push_back(e.get());
   }
-  if (!with_recon) ++g_patterns;
+  if (kind == kJitPattern) ++g_patterns;
+  if (kind == kJitBlock || kind == kJitBlockAcc) ++g_blocks;
   registry().push_back(std::move(e));
-  w.start();
-  g_cv.notify_all();
-  return 1;
 }
 
-int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
-  Entry* e = find_entry(field, k, p, rows, k);
+// The blocks of a wide p x k matrix and their kinds, in build order (output
+// block by output block, the way run_job launches them).
+template <class F>
+void for_each_block(uint32_t k, uint32_t p, F&& f) {
+  for (uint32_t o0 = 0; o0 < p; o0 += kJitMaxOut)
+    for (uint32_t i0 = 0; i0 < k; i0 += (uint32_t)kMaxIn)
+      f(o0, i0, std::min<uint32_t>(kJitMaxOut, p - o0), std::min<uint32_t>(kMaxIn, k - i0),
+        i0 == 0 ? kJitBlock : kJitBlockAcc);
+}
+
+int status_of(Entry* e, bool wait) {
   if (!e) return 0;
   for (int st = 0; st < e->stages; ++st) {
     if (wait) e->built[st].wait();
@@ -390,12 +400,66 @@ int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wai
   return 2;
 }
 
+}  // namespace
+
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKind kind) {
+  if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || k > (uint32_t)kMaxIn ||
+      p == 0 || p > kJitMaxOut || (kind == kJitCodec && bitslice_compiled(field, k, p)))
+    return 0;
+  registry();
+  Worker& w = worker();
+  std::lock_guard<std::mutex> g(g_mu);
+  if (find_locked(field, k, p, rows, k, kind)) return 1;
+  if (kind == kJitPattern &&
+      (g_patterns >= kMaxPatterns || g_jobs[kEnc].size() >= kMaxPendingPatternJobs))
+    return 0;  // decode patterns are an optimisation: never queue without bound
+  if ((kind == kJitBlock || kind == kJitBlockAcc) && g_blocks >= kMaxBlocks) return 0;
+  add_locked(field, k, p, rows, k, kind);
+  w.start();
+  g_cv.notify_all();
+  return 1;
+}
+
+int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
+  if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || p == 0) return 0;
+  registry();
+  Worker& w = worker();
+  std::lock_guard<std::mutex> g(g_mu);
+  int need = 0;
+  for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
+    need += !find_locked(field, ni, no, rows + (size_t)o0 * k + i0, k, kind);
+  });
+  if (need == 0) return 1;
+  if (g_blocks + need > kMaxBlocks) return 0;
+  for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
+    const uint16_t* r = rows + (size_t)o0 * k + i0;
+    if (!find_locked(field, ni, no, r, k, kind)) add_locked(field, ni, no, r, k, kind);
+  });
+  w.start();
+  g_cv.notify_all();
+  return 1;
+}
+
+int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
+  int worst = 2;
+  for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
+    if (worst <= 0) return;  // one block not registered: the rows are not a wide codec's
+    const int s = status_of(find_entry(field, ni, no, rows + (size_t)o0 * k + i0, k, kind), wait);
+    if (s < worst) worst = s;
+  });
+  return worst;
+}
+
+int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
+  return status_of(find_entry(field, k, p, rows, k), wait);
+}
+
 bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
-              JitFns* out, hipError_t* err) {
+              JitFns* out, hipError_t* err, bool acc) {
   *err = hipSuccess;
   const int64_t mode = get_option(9);
-  if (mode == 0 || p > kJitMaxOut) return false;
-  Entry* e = find_entry(field, k, p, rows, stride);
+  if (mode == 0 || p > kJitMaxOut || (acc && stage != kEnc)) return false;
+  Entry* e = find_entry(field, k, p, rows, stride, acc ? (int)kJitBlockAcc : -2);
   if (!e || stage >= e->stages) return false;
   auto& b = e->built[stage];
   if (mode >= 2) b.wait();
@@ -416,14 +480,19 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
     e->loaded.push_back(Entry::Loaded{dev});
     l = &e->loaded.back();
   }
-  const bool have = stage == kEnc ? l->fns.enc != nullptr : l->have_rec;
+  const bool have = stage == kEnc ? (acc ? l->fns.enc_acc : l->fns.enc) != nullptr : l->have_rec;
   if (!have) {  // load this stage's module on this device; it stays loaded
     hipModule_t m = nullptr;
     he = hipModuleLoadData(&m, c->code.data());
     JitFns f = l->fns;
     if (stage == kEnc) {
-      if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
-      if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4, m, "rse_jit_encode4");
+      if (acc) {
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.enc_acc, m, "rse_jit_encode_acc");
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4_acc, m, "rse_jit_encode4_acc");
+      } else {
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4, m, "rse_jit_encode4");
+      }
     } else {
       f.n_rec = recon_ns(p, f.rec_ns);
       for (int q = 0; q < f.n_rec && he == hipSuccess; ++q) {

@@ -131,19 +131,35 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
 // with hiprtc (host CPU only; no device work), then loaded per device on first
 // use.  Results never depend on which kernel runs.
 constexpr uint32_t kJitMaxOut = 8;  // p' <= 8: 16 x p' accumulator VGPRs
+// What a registered set of rows is:
+//  kJitCodec   a codec's parity rows, built with the syndrome reconstruct
+//              kernels too;
+//  kJitPattern a decode pattern (the composed rows of a reconstruct,
+//              core.rs:697-731), encode kernel only, capped in number and
+//              queue length;
+//  kJitBlock   one <= 8 x <= 32 block of a wide codec's parity rows (k > 32
+//              or p > 8) over its first 32 inputs: encode kernels
+//              (jit_register_blocks);
+//  kJitBlockAcc a block over later inputs: accumulate-mode encode kernels
+//              only (each kernel is seconds of hiprtc for 32 x 8 blocks).
+enum JitKind { kJitCodec = 0, kJitPattern = 1, kJitBlock = 2, kJitBlockAcc = 3 };
 // Registers p x k rows (row-major) and queues their build on the background
-// thread.  with_recon: a codec's parity rows, built with the syndrome
-// reconstruct kernels too; otherwise a decode pattern (the composed rows of a
-// reconstruct, core.rs:697-731), encode kernel only, capped in number and
-// queue length.  Returns 1 if registered (now or before), 0 if not eligible
-// or refused.
-int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool with_recon);
+// thread.  Returns 1 if registered (now or before), 0 if not eligible or
+// refused.
+int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKind kind);
+// Registers every kJitBlock block of a wide codec's p x k parity rows -- all of
+// them or, past the block cap, none.  Blocks: rows [o0, o0 + 8) x inputs
+// [i0, i0 + 32), the chunking of run_job (rse_codec.cpp).
+int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows);
+// jit_status over all of a wide codec's blocks (the least ready one).
+int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 // 2 ready, 1 building, 0 not registered, -1 build failed; wait != 0 blocks
 // until the build has finished.
 int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 struct JitFns {
   hipFunction_t enc = nullptr;  // bitslice encode/verify (CodeArgs, chunks per stripe)
   hipFunction_t enc4 = nullptr; // ... over 4 KiB chunks, one per wave
+  hipFunction_t enc_acc = nullptr, enc4_acc = nullptr;  // accumulate mode (kJitBlockAcc)
   int n_rec = 0;
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
@@ -153,9 +169,10 @@ struct JitFns {
 // coefficients rows[o * stride + i] equal a registered codec's parity rows,
 // loaded on the current device.  Returns false (and *err = hipSuccess) if there
 // are none (yet: RSE_OPT_JIT 1 does not wait for a compile in flight, 2 does);
-// *err is set on a module-load failure.
+// *err is set on a module-load failure.  acc: the accumulate-mode kernels of a
+// kJitBlockAcc entry (stage 0) instead.
 bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
-              JitFns* out, hipError_t* err);
+              JitFns* out, hipError_t* err, bool acc = false);
 int64_t jit_modules_built();  // RSE_OPT_JIT_MODULES
 
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).

@@ -206,3 +206,15 @@ def test_run_time_specialisation_builds_on_cpu():
         assert R.galois_8.ReedSolomon(7, 2).kernel_kind(wait=True) == "table"
     finally:
         L.rse_set_option(9, old)
+
+
+def test_wide_codec_blocks_build_on_cpu():
+    """Wide codecs (k > 32 or p > 8) are specialised per 8 x 32 block of their
+    parity rows: 6 + 10 has two blocks (rows 0..7 and 8..9), 34 + 1 a store
+    block over inputs 0..31 and an accumulate block over inputs 32..33."""
+    built = L.rse_get_option(10)
+    assert R.galois_8.ReedSolomon(6, 10).kernel_kind(wait=True) == "bitslice-specialised"
+    assert L.rse_get_option(10) >= built + 2
+    built = L.rse_get_option(10)
+    assert R.galois_8.ReedSolomon(34, 1).kernel_kind(wait=True) == "bitslice-specialised"
+    assert L.rse_get_option(10) >= built + 2

@@ -1132,3 +1132,63 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     assert d["n_gpus"] == 2 and d["config"]["global_stripes_per_step"] == 8
     assert d["config"]["parity_check_vs_reference"] is True
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
+
+
+WIDE_CODECS = [(8, 40, 2), (8, 6, 10), (16, 36, 3), (8, 33, 9)]
+
+
+@pytest.mark.parametrize("field,k,p", WIDE_CODECS)
+def test_wide_codec_blocks(R, field, k, p):
+    """Wide codecs (k > 32 or p > 8) get bit-sliced kernels per 8 x 32 block of
+    their parity rows (rse_jit.cpp kJitBlock / kJitBlockAcc): run_job launches
+    the blocks output block by output block, later input blocks accumulating
+    into the outputs.  Every block launch is bit-sliced (the launch counter
+    counts one per block), and encode, verify (through the materialised sums
+    of > 32 inputs) and flat multi-stripe encode match the oracle over 16 KiB
+    chunks, a 4 KiB chunk and a table-coded tail."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 2 * 16384 + 4096 + 48 * es
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(field * 1000 + k * 10 + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    blocks = -(-k // 32) * -(-p // 8)
+    old = lib.rse_get_option(9)
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        r = R.core.ReedSolomon(k, p, field)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        t = [dev(x).reshape(shape) for x in full[:k]] + \
+            [torch.full(shape, 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        n0 = lib.rse_get_option(6)
+        r.encode(t)
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(6) - n0 == blocks
+        for i in range(p):
+            assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
+        assert r.verify(t)
+        t[k + p - 1].view(-1)[20000] ^= 1  # in a bit-sliced chunk
+        assert not r.verify(t)
+        t[k + p - 1].view(-1)[20000] ^= 1
+        t[k - 1].view(-1)[nbytes - 1] ^= 0x80  # in the table-coded tail
+        assert not r.verify(t)
+        t[k - 1].view(-1)[nbytes - 1] ^= 0x80
+        stripes = 3
+        flat = torch.full((stripes, k + p, nbytes), 0xA5, dtype=torch.uint8, device="cuda")
+        for s_ in range(stripes):
+            for i in range(k):
+                flat[s_, i] = dev(np.roll(full[i], s_))
+        r.encode_flat(flat, n_elems, stripes)
+        torch.cuda.synchronize()
+        got = host(flat)
+        for s_ in range(stripes):
+            sh = [np.roll(full[i], s_) for i in range(k)] + \
+                 [np.zeros(nbytes, np.uint8) for _ in range(p)]
+            oc.encode(sh)
+            for i in range(p):
+                assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old)

@@ -5,7 +5,9 @@
 #include <hip/hiprtc.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <fstream>
+#include <thread>
 #include <sstream>
 #include <cstdio>
 #include <string>
@@ -33,8 +35,11 @@ extern "C" __global__ __launch_bounds__(256, 2) void probe(const uint8_t* in, ui
 }
 )";
 
+static int compile_once(int argc, char** argv, const std::string& file_src);
+
 // With an argument: compile that file instead (e.g. a module dumped by
-// RSE_JIT_DUMP=dir) and report the time.
+// RSE_JIT_DUMP=dir) and report the time.  PROBE_THREADS=n: n compiles of it
+// at once on n threads of this process (does hiprtc build in parallel?).
 int main(int argc, char** argv) {
   std::string file_src;
   if (argc > 1) {
@@ -43,6 +48,23 @@ int main(int argc, char** argv) {
     ss << f.rdbuf();
     file_src = ss.str();
   }
+  const char* nt = std::getenv("PROBE_THREADS");
+  const int n = nt ? std::atoi(nt) : 1;
+  if (n <= 1) return compile_once(argc, argv, file_src);
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  std::vector<int> rc(n);
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] { rc[i] = compile_once(argc > 2 ? 2 : argc, argv, file_src); });
+  for (auto& t : th) t.join();
+  std::printf("%d compiles on %d threads: %.0f ms wall\n", n, n,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  for (int r : rc)
+    if (r) return r;
+  return 0;
+}
+
+static int compile_once(int argc, char** argv, const std::string& file_src) {
   auto t0 = std::chrono::steady_clock::now();
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, argc > 1 ? file_src.c_str() : kSrc, "probe.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return 2;
