@@ -595,13 +595,18 @@ thread_local int64_t g_pattern_launches = 0;  // RSE_OPT_PATTERN_LAUNCHES
 // inputs, one pass at encode speed with no run-time mixing.  Until it is ready
 // the syndrome kernel serves the pattern.  RSE_OPT_JIT 2 builds (and waits
 // for) it on first use.  True if the pattern kernel is ready for this plan.
+// Wide codecs (k > 32) and patterns with more than 8 rows get block kernels
+// instead (jit_register_blocks; run_job launches them once all are ready).
 bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes) {
   const int64_t mode = rse::get_option(RSE_OPT_JIT);
   if (mode == 0 || !rse::get_option(RSE_OPT_JIT_PATTERNS) || !rse::get_option(RSE_OPT_BITSLICE) ||
-      len_bytes < rse::bitslice_chunk_bytes() || plan.rows.n_out > rse::kJitMaxOut ||
-      c->k > (size_t)kMaxIn || (mode < 2 && plan.pattern_uses < 2))
+      len_bytes < rse::bitslice_chunk_bytes() || (mode < 2 && plan.pattern_uses < 2))
     return false;
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
+  if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
+    if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data())) return false;
+    return rse::jit_blocks_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+  }
   if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), rse::kJitPattern)) return false;
   return rse::jit_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
 }

@@ -1192,3 +1192,51 @@ def test_wide_codec_blocks(R, field, k, p):
                 assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
     finally:
         lib.rse_set_option(9, old)
+
+
+@pytest.mark.parametrize("field,k,p,erased", [(8, 40, 2, [3, 39]), (8, 6, 10, [0, 1, 2, 5, 6, 8, 9, 12, 15]),
+                                              (16, 36, 3, [0, 35, 37])])
+def test_wide_reconstruct_pattern_blocks(R, field, k, p, erased):
+    """A wide codec's repeated erasure pattern (RSE_OPT_JIT 2: the first use)
+    gets block kernels for its composed decode rows; reconstruct and
+    reconstruct_data_flat then run them (pattern-launch counter) and match the
+    oracle."""
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 16384 + 4096 + 32 * es
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(field * 7 + k * 3 + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    present = [i not in erased for i in range(k + p)]
+    old = lib.rse_get_option(9)
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        r = R.core.ReedSolomon(k, p, field)
+        tb = [dev(x).reshape(shape) for x in full]
+        for e in erased:
+            tb[e].fill_(0x33)
+        n0 = lib.rse_get_option(12)
+        r.reconstruct(list(zip(tb, present)))
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(12) - n0 == 1
+        for i in range(k + p):
+            assert (host(tb[i]).reshape(-1) == full[i]).all(), i
+        stripes = 2
+        flat = torch.empty((stripes, k + p, nbytes), dtype=torch.uint8, device="cuda")
+        for s_ in range(stripes):
+            for i in range(k + p):
+                flat[s_, i] = dev(full[i]) if present[i] else 0x77
+        n0 = lib.rse_get_option(12)
+        r.reconstruct_data_flat(flat, n_elems, stripes, present)
+        torch.cuda.synchronize()
+        if any(e < k for e in erased):
+            assert lib.rse_get_option(12) - n0 == 1
+        got = host(flat)
+        for s_ in range(stripes):
+            for i in range(k):
+                assert (got[s_, i] == full[i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old)

@@ -14,4 +14,8 @@ case "$1" in
       "w8_50_20:200:$T --k 50 --p 20 --shard-mib 1 --stripes 64" \
       "w16_100_30:300:$T --field 16 --k 100 --p 30 --shard-mib 1 --stripes 32" \
       "w16_200_56:600:$T --field 16 --k 200 --p 56 --shard-kib 256 --stripes 32" ;;
+  c) R="python -u tools/tune.py --rounds 3 --nt-only --shapes 0:0 --op reconstruct --patterns 1 --bitslice 0,1"
+     bash tools/gpu_session.sh \
+      "r16_40_12:300:$R --field 16 --k 40 --p 12 --shard-mib 1 --stripes 64 --erase 0,1,2,3" \
+      "r8_50_20:300:$R --k 50 --p 20 --shard-mib 1 --stripes 64 --erase 0,1,2,3,4,5,6,7,8,9" ;;
 esac
