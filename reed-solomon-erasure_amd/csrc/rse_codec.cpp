@@ -71,6 +71,7 @@ struct rse_codec {
   mutable std::map<std::vector<size_t>, decltype(lru)::iterator> index;
   // run-time specialisation requested (rse_jit.cpp; see want_bitslice)
   mutable std::atomic<bool> jit_requested{false};
+  mutable std::atomic<uint64_t> wide_bytes{0};  // shard bytes a wide codec has coded (want_bitslice)
 
   size_t esize() const { return field == 16 ? 2 : 1; }
   uint16_t mat(size_t r, size_t c) const { return field == 16 ? m16.at(r, c) : m8.at(r, c); }
@@ -307,14 +308,23 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
 // CPU only).  The first call that codes at least one whole bit-sliced chunk
 // (4 KiB: the per-wave chunks) requests it, so codecs only ever used on short
 // shards never pay for a build.  Wide codecs (k > 32 or p > 8) get one
-// kernel pair per 8 x 32 block of their parity rows instead (store and
-// accumulate mode; run_job launches them block by block).
-void want_bitslice(const rse_codec* c, size_t len_bytes) {
+// module per 8 x 32 block of their parity rows instead (store or accumulate
+// mode; run_job launches them block by block), requested once the codec has
+// coded 1 GiB of shards on the table kernels (at once under RSE_OPT_JIT 2, or
+// `now`: kernel_kind with wait): each block is seconds of hiprtc, worth it
+// for a codec that streams data, not for one used a few times.
+constexpr uint64_t kWideJitBytes = 1ull << 30;
+void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_t n_stripes = 1) {
   if (len_bytes < 4096 || c->jit_requested.load(std::memory_order_relaxed)) return;
+  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
+  if (wide && !now && rse::get_option(RSE_OPT_JIT) < 2) {
+    const uint64_t b = (uint64_t)len_bytes * c->total * n_stripes;
+    if (c->wide_bytes.fetch_add(b, std::memory_order_relaxed) + b < kWideJitBytes) return;
+  }
   c->jit_requested.store(true, std::memory_order_relaxed);
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
-  if (c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut)
+  if (wide)
     rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data());
   else
     rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
@@ -596,7 +606,8 @@ thread_local int64_t g_pattern_launches = 0;  // RSE_OPT_PATTERN_LAUNCHES
 // the syndrome kernel serves the pattern.  RSE_OPT_JIT 2 builds (and waits
 // for) it on first use.  True if the pattern kernel is ready for this plan.
 // Wide codecs (k > 32) and patterns with more than 8 rows get block kernels
-// instead (jit_register_blocks; run_job launches them once all are ready).
+// instead (jit_register_blocks; run_job launches them once all are ready),
+// for shards of 1 MiB or more (each block is seconds of hiprtc).
 bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes) {
   const int64_t mode = rse::get_option(RSE_OPT_JIT);
   if (mode == 0 || !rse::get_option(RSE_OPT_JIT_PATTERNS) || !rse::get_option(RSE_OPT_BITSLICE) ||
@@ -604,6 +615,7 @@ bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes)
     return false;
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
   if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
+    if (mode < 2 && len_bytes < (1u << 20)) return false;
     if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data())) return false;
     return rse::jit_blocks_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
   }
@@ -781,7 +793,7 @@ size_t rse_codec_total_shard_count(const rse_codec* c) { return c ? c->total : 0
 int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
-  if (wait) want_bitslice(c, rse::bitslice_chunk_bytes());
+  if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const Rows rows = parity_rows(c);
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
   switch (wide ? rse::jit_blocks_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
@@ -883,7 +895,7 @@ int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t 
   std::vector<uint8_t*> out(c->p);
   for (size_t i = 0; i < c->k; ++i) in[i] = base + i * sb;
   for (size_t r = 0; r < c->p; ++r) out[r] = base + (c->k + r) * sb;
-  want_bitslice(c, sb);
+  want_bitslice(c, sb, false, n_stripes);
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
         (uint64_t)c->total * sb, n_stripes};
@@ -900,7 +912,7 @@ int rse_verify_flat(const rse_codec* c, const void* stripes, size_t shard_len, s
   std::vector<const uint8_t*> in(c->k), cmp(c->p);
   for (size_t i = 0; i < c->k; ++i) in[i] = base + i * sb;
   for (size_t r = 0; r < c->p; ++r) cmp[r] = base + (c->k + r) * sb;
-  want_bitslice(c, sb);
+  want_bitslice(c, sb, false, n_stripes);
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, in.data(), nullptr, cmp.data(), sb, rse::kCheck, false, nullptr,
         (uint64_t)c->total * sb, n_stripes, true};
@@ -965,7 +977,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   //    run-time specialised codecs), planned per stripe on the device
   if (fits && sb >= rse::bitslice_chunk_bytes() && sb % 16u == 0 && aligned16(base) &&
       rse::get_option(RSE_OPT_BITSLICE)) {
-    want_bitslice(c, sb);
+    want_bitslice(c, sb, false, n_stripes);
     uint32_t need = 0;  // sigma rows any stripe uses: its R and missing parity rows
     for (size_t s = 0; s < n_stripes; ++s) {
       const uint8_t* pr = present + s * T;

@@ -74,7 +74,14 @@ struct Entry {
 
 std::mutex g_mu;  // guards the registry and the job queues
 std::condition_variable g_cv;
-std::deque<Entry*> g_jobs[2];  // per stage; every encode job runs before any reconstruct job
+// Build queues, in priority order: encode modules of codecs and decode
+// patterns, reconstruct modules, then wide-codec blocks (many, each seconds of
+// hiprtc: they must not delay the modules the narrow codecs wait for).
+constexpr int kBlkQueue = 2;
+std::deque<Entry*> g_jobs[3];
+int queue_of(const Entry& e, int stage) {
+  return (e.kind == kJitBlock || e.kind == kJitBlockAcc) ? kBlkQueue : stage;
+}
 std::atomic<int64_t> g_built{0};
 int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
 constexpr int kMaxPatterns = 64;
@@ -330,7 +337,8 @@ class Worker {
     g_cv.notify_all();
     if (th_.joinable()) th_.join();
     for (auto& q : g_jobs)
-      for (Entry* e : q) e->promise[&q - g_jobs].set_value(std::make_shared<Compiled>());
+      for (Entry* e : q)
+        e->promise[&q - g_jobs == kRec ? kRec : kEnc].set_value(std::make_shared<Compiled>());
   }
 
  private:
@@ -340,11 +348,15 @@ class Worker {
       int stage = 0;
       {
         std::unique_lock<std::mutex> g(g_mu);
-        g_cv.wait(g, [&] { return stop_ || !g_jobs[kEnc].empty() || !g_jobs[kRec].empty(); });
+        g_cv.wait(g, [&] {
+          return stop_ || !g_jobs[kEnc].empty() || !g_jobs[kRec].empty() ||
+                 !g_jobs[kBlkQueue].empty();
+        });
         if (stop_) return;
-        stage = g_jobs[kEnc].empty() ? kRec : kEnc;
-        e = g_jobs[stage].front();
-        g_jobs[stage].pop_front();
+        const int q = !g_jobs[kEnc].empty() ? kEnc : !g_jobs[kRec].empty() ? kRec : kBlkQueue;
+        stage = q == kRec ? kRec : kEnc;
+        e = g_jobs[q].front();
+        g_jobs[q].pop_front();
       }
       e->promise[stage].set_value(compile(*e, stage));
     }
@@ -372,7 +384,7 @@ void add_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t 
     for (uint32_t i = 0; i < k; ++i) e->rows[o * k + i] = rows[o * stride + i];
   for (int st = 0; st < e->stages; ++st) {
     e->built[st] = e->promise[st].get_future().share();
-    g_jobs[st].push_back(e.get());
+    g_jobs[queue_of(*e, st)].push_back(e.get());
   }
   if (kind == kJitPattern) ++g_patterns;
   if (kind == kJitBlock || kind == kJitBlockAcc) ++g_blocks;
@@ -389,8 +401,23 @@ void for_each_block(uint32_t k, uint32_t p, F&& f) {
         i0 == 0 ? kJitBlock : kJitBlockAcc);
 }
 
+// A caller about to wait for `e`: its queued builds move to the front of
+// their queues (a codec waited for is not built after every block queued
+// before it).
+void promote(Entry* e) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& q : g_jobs)
+    for (auto it = q.begin(); it != q.end(); ++it)
+      if (*it == e) {
+        q.erase(it);
+        q.push_front(e);
+        break;
+      }
+}
+
 int status_of(Entry* e, bool wait) {
   if (!e) return 0;
+  if (wait) promote(e);
   for (int st = 0; st < e->stages; ++st) {
     if (wait) e->built[st].wait();
     else if (e->built[st].wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 1;
@@ -462,7 +489,10 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
   Entry* e = find_entry(field, k, p, rows, stride, acc ? (int)kJitBlockAcc : -2);
   if (!e || stage >= e->stages) return false;
   auto& b = e->built[stage];
-  if (mode >= 2) b.wait();
+  if (mode >= 2) {
+    promote(e);
+    b.wait();
+  }
   else if (b.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;
   const std::shared_ptr<const Compiled> c = b.get();
   if (!c->ok) return false;
