@@ -95,66 +95,70 @@ def job_throughput(steps: int, stripes_per_rank: int, world: int, stripe_bytes: 
 
 
 # ------------------------------------------------------------ CPU baseline
-def cpu_baseline(k, p, shard_bytes, seconds):
-    """The reference's simd-accel path (simd_c/reedsolomon.c compiled from the
-    reference sources into oracle/_ref, driven in core.rs:481-509 loop order),
-    1 thread, on a bounded sample: one k+p stripe re-encoded for ~`seconds`."""
+def host_cpu():
+    """Host CPU description for the baseline legs (model, CPUs visible)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
+def cpu_threads():
+    """Threads for the all-cores legs: the CPUs this process may run on,
+    capped at 16 -- the GPU box's CPU share for one GPU (the box reports the
+    whole machine's CPUs through nproc / os.cpu_count)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _cpu_workload(field, k, p, shard_bytes, rows_fn, seed):
+    """One stripe's inputs, outputs and coding rows for a CPU leg."""
     import numpy as np
     from oracle import oracle as O
-    data = [O.splitmix_bytes(SEED, i, shard_bytes) for i in range(k)]
-    par = [np.zeros(shard_bytes, np.uint8) for _ in range(p)]
-    rows = np.ascontiguousarray(O.Codec(8, k, p).matrix()[k:])
-    if O.ref_available():
-        kind = "reference"
-        ref = O.ref()
-
-        def run():
-            ref.ref_gf8_code_some_slices(rows.ctypes.data_as(O._u8p), p, k, O._ptrs(data),
-                                         O._ptrs(par), shard_bytes)
-    else:
-        kind = "port"
-
-        def run():
-            O.code_some_slices(8, rows, data, par)
-    run()  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    mbps = n * (k + p) * shard_bytes / dt / MiB
-    return {"value": round(mbps, 1), "unit": "MB/s", "cores": 1, "kind": kind,
-            "sample": f"{n} encodes of one {k}+{p} x {shard_bytes // MiB} MiB stripe "
-                      f"({dt:.1f} s, 1 thread, reference simd_c kernel -O3 -march=haswell)"}
+    data = [O.splitmix_bytes(seed, i, shard_bytes) for i in range(k)]
+    out = [np.zeros(shard_bytes, np.uint8) for _ in range(p)]
+    return data, out, np.ascontiguousarray(rows_fn(O))
 
 
-def cpu_baseline_parallel(k, p, shard_bytes, seconds, threads):
-    """Stripe-parallel CPU leg: `threads` host threads, each
-    encoding its own stripe with the reference kernel (ctypes drops the GIL
-    for the foreign call), for ~`seconds`.  Reported beside cpu_baseline."""
+def cpu_leg(name, field, k, n_out, shard_bytes, rows_fn, alg_bytes, seconds, threads):
+    """The reference's CPU path on this host for one workload: GF(2^8) runs the
+    reference's own simd_c kernel (compiled from the reference sources into
+    oracle/_ref, driven in core.rs:481-509 loop order: "reference"); GF(2^16)
+    runs the C restatement of the Field default loops the reference uses for it
+    (lib.rs:99-118 over galois_16.rs:146-162: "port").  `threads` threads each
+    code their own stripe (ctypes drops the GIL), for ~`seconds`; the rate
+    counts `alg_bytes` per stripe (the metric's data+parity convention)."""
     import threading
 
-    import numpy as np
     from oracle import oracle as O
-    if not O.ref_available():
-        return None
-    ref = O.ref()
-    rows = np.ascontiguousarray(O.Codec(8, k, p).matrix()[k:])
-    stripes = [([O.splitmix_bytes(SEED + t, i, shard_bytes) for i in range(k)],
-                [np.zeros(shard_bytes, np.uint8) for _ in range(p)]) for t in range(threads)]
+    use_ref = field == 8 and O.ref_available()
+    work = [_cpu_workload(field, k, n_out, shard_bytes, rows_fn, SEED + t) for t in range(threads)]
+    if use_ref:
+        ref = O.ref()
+
+        def run(t):
+            data, out, rows = work[t]
+            ref.ref_gf8_code_some_slices(rows.ctypes.data_as(O._u8p), n_out, k, O._ptrs(data),
+                                         O._ptrs(out), shard_bytes)
+    else:
+        def run(t):
+            data, out, rows = work[t]
+            O.code_some_slices(field, rows, data, out)
+    run(0)  # warm
     counts = [0] * threads
     stop = threading.Event()
 
-    def work(t):
-        data, par = stripes[t]
-        dp, pp = O._ptrs(data), O._ptrs(par)
+    def loop(t):
         while not stop.is_set():
-            ref.ref_gf8_code_some_slices(rows.ctypes.data_as(O._u8p), p, k, dp, pp, shard_bytes)
+            run(t)
             counts[t] += 1
 
-    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    ths = [threading.Thread(target=loop, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
     for th in ths:
         th.start()
@@ -164,28 +168,127 @@ def cpu_baseline_parallel(k, p, shard_bytes, seconds, threads):
         th.join()
     dt = time.perf_counter() - t0
     n = sum(counts)
-    return {"value": round(n * (k + p) * shard_bytes / dt / MiB, 1), "unit": "MB/s",
-            "cores": threads, "kind": "reference",
-            "sample": f"{n} encodes of {threads} independent {k}+{p} x {shard_bytes // MiB} MiB "
-                      f"stripes ({dt:.1f} s, {threads} threads, reference simd_c kernel)"}
+    kernel = ("reference simd_c kernel -O3 -march=haswell" if use_ref else
+              "C restatement of the scalar Field loops")
+    return {"value": round(n * alg_bytes / dt / MiB, 1), "unit": "MB/s", "cores": threads,
+            "kind": "reference" if use_ref else "port",
+            "sample": f"{name}: {n} stripes ({threads} thread(s), each its own stripe, "
+                      f"{dt:.1f} s, {kernel})"}
 
 
-def load_traffic(workload, kernel):
-    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary for
-    this workload (profiles/*pmc_traffic*.json, written by
-    tools/pmc_traffic.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+def cpu_baselines(seconds, threads):
+    """CPU legs beside the GPU numbers (rank 0, N = 1): the headline 10+4 x
+    16 MiB encode at 1 thread (`cpu_baseline`) and on all cores, plus the other
+    BASELINE configs: 10+2 x 1 MiB encode, 10+4 reconstruct of data shards 0,1
+    (decode rows of the k valid shards, core.rs:850-861) and GF(2^16) 20+8 x
+    4 MiB encode (BASELINE.md:37-45, benches/bandwidth.rs:58-86)."""
+    from oracle import oracle as O
+
+    def parity(field, k, p):
+        return lambda O_: O_.Codec(field, k, p).matrix()[k:]
+
+    def decode_0_1(O_):
+        m = O_.Codec(8, 10, 4).matrix()
+        valid = [i for i in range(14) if i not in (0, 1)][:10]
+        return O_.matrix_invert(8, m[valid])[[0, 1]]
+
+    L = 16 * MiB
+    head = cpu_leg("10+4 x 16 MiB encode", 8, 10, 4, L, parity(8, 10, 4), 14 * L, seconds, 1)
+    out = {"cpu_baseline": head}
+    legs = {}
+    specs = [("encode_10_4_16MiB", "10+4 x 16 MiB encode", 8, 10, 4, L, parity(8, 10, 4), 14 * L),
+             ("encode_10_2_1MiB", "10+2 x 1 MiB encode", 8, 10, 2, MiB, parity(8, 10, 2), 12 * MiB),
+             ("reconstruct_10_4_16MiB_0_1", "10+4 x 16 MiB reconstruct_data, shards 0,1 erased",
+              8, 10, 2, L, decode_0_1, 12 * L),
+             ("gf16_encode_20_8_4MiB", "GF(2^16) 20+8 x 4 MiB encode", 16, 20, 8, 4 * MiB,
+              parity(16, 20, 8), 28 * 4 * MiB)]
+    for key, name, field, k, n_out, sb, rows_fn, alg in specs:
+        one = head if key == "encode_10_4_16MiB" else cpu_leg(name, field, k, n_out, sb, rows_fn,
+                                                              alg, seconds / 2, 1)
+        legs[key] = {"1_thread": one,
+                     "all_cores": cpu_leg(name, field, k, n_out, sb, rows_fn, alg, seconds / 2,
+                                          threads)}
+    out["cpu_baseline_legs"] = legs
+    out["cpu_host"] = dict(host_cpu(), threads_used_all_cores=threads,
+                           cap="16 threads: the GPU box's CPU share for one GPU")
+    return out
+
+
+def load_traffic(workload, kernel_id):
+    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary
+    (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py: FETCH_SIZE
+    x2 gfx950 correction + WRITE_SIZE) -- only if it was measured on this
+    workload AND on the kernel that ran here (rse_last_kernel); else None."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("kernel_family", "table") == kernel:
-            best = d
+        if d.get("workload") == workload and d.get("kernel_id") == kernel_id:
+            best = dict(d, file=os.path.relpath(path, ROOT))
     return best
 
 
 # ----------------------------------------------------------------- main
+def golden_stripes():
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
+    return g["gf8_10_4_stripe_parity"]
+
+
+def check_stripes(v, mine, resident, k, p):
+    """This rank's verdict on its own output: the parity of its first and last
+    resident stripe against the reference digests (tests/golden).  1 = every
+    checked stripe matches, 0 = a mismatch, -1 = no digest for these stripes."""
+    gold = golden_stripes()
+    checked, ok = [], True
+    for s in sorted({0, resident - 1}):
+        g = mine.start + s
+        if str(g) not in gold:
+            continue
+        got = [hashlib.sha256(v[s, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
+        checked.append(g)
+        ok = ok and got == gold[str(g)]
+    return (1 if ok else 0) if checked else -1, checked
+
+
+def gather(values, world, rank, device):
+    """Every rank's value (float64), in rank order, on every rank."""
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[rank] = float(values)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.cpu()]
+
+
+def host_leg(r, v, k, p, L, stream, world, rank, coll_dev):
+    """Host-memory encode on every rank at once (multi-GPU host bandwidth,
+    SURVEY 8f): each rank streams 4 of its stripes from pinned host memory
+    through its GPU; the job rate is all ranks' bytes over the slowest rank."""
+    import torch
+    import torch.distributed as dist
+    ns = min(4, v.shape[0])
+    hflat = v[:ns].reshape(-1).cpu().pin_memory()
+    r.encode_host_flat(hflat, L, ns)  # warm
+    reps = 3
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r.encode_host_flat(hflat, L, ns)
+    dt = (time.perf_counter() - t0) / reps
+    ok = torch.equal(hflat.view(ns, k + p, L)[:, k:], v[:ns, k:].cpu())
+    per = gather(dt, world, rank, coll_dev)
+    oks = gather(1.0 if ok else 0.0, world, rank, coll_dev)
+    return {"what": f"rse_encode_host_flat on every rank at once, {ns} stripes each from pinned "
+                    "host memory (H2D data, kernel, D2H parity)",
+            "ranks": world, "MB_per_s_all_ranks": round(world * ns * (k + p) * L / max(per) / MiB, 1),
+            "GB_per_s_pcie_h2d_all_ranks": round(world * ns * k * L / max(per) / 1e9, 1),
+            "parity_matches_device_all_ranks": all(x == 1.0 for x in oks)}
+
+
 def main(argv=None):
     args = parse(argv)
     world, rank, local = init_dist(args)
@@ -206,7 +309,7 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     coll_dev = None if rehearsal else "cuda"
     import reed_solomon_erasure as R
-    from reed_solomon_erasure.core import fill_splitmix
+    from reed_solomon_erasure.core import fill_splitmix, last_kernel
 
     k, p = args.data_shards, args.parity_shards
     L = args.shard_mib * MiB
@@ -217,7 +320,8 @@ def main(argv=None):
     free, _ = torch.cuda.mem_get_info()
     # one HBM region per stripe when it fits (it does on 288 GB); otherwise a
     # pool far larger than the 256 MiB Infinity Cache, cycled.
-    pool = min(n_local, max(8, int(0.8 * free) // stripe_bytes))
+    share = world if rehearsal else 1  # rehearsal ranks share one GPU
+    pool = min(n_local, max(8, int(0.8 * free / share) // stripe_bytes))
     buf = torch.empty(pool * stripe_bytes, dtype=torch.uint8, device="cuda")
     v = buf.view(pool, k + p, L)
     for s in range(pool):
@@ -240,16 +344,19 @@ def main(argv=None):
         step()
     torch.cuda.synchronize()
     kernel = "bitslice" if lib.rse_get_option(6) > n_bs else "table"
-    # correctness gate: global stripe 0's parity equals the reference's digest
-    check = None
-    if rank == 0 and (k, p, L) == (10, 4, 16 * MiB):
-        g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
-        want = g["generated"]["full_size"][f"gf8_10_4_{16 * MiB}"]["parity_sha256"]
-        got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
-        check = got == want
-        if not check:
-            print("PARITY MISMATCH vs reference digests", file=sys.stderr)
-            sys.exit(3)
+    kernel_id = last_kernel()
+    # correctness gate, every rank on its own stripes, verdicts combined
+    verdict, checked = (check_stripes(v, mine, pool, k, p) if (k, p, L) == (10, 4, 16 * MiB)
+                        else (-1, []))
+    verdicts = gather(verdict, world, rank, coll_dev)
+    if any(x == 0 for x in verdicts):
+        if rank == 0:
+            print(f"PARITY MISMATCH vs reference digests, per-rank verdicts {verdicts}",
+                  file=sys.stderr)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)  # every rank together: nobody is left waiting in a collective
+    check = all(x == 1 for x in verdicts) if any(x == 1 for x in verdicts) else None
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -269,30 +376,36 @@ def main(argv=None):
     kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
     elapsed = reduce_timing(elapsed, world, device=coll_dev)
     value = job_throughput(args.steps, n_local, world, stripe_bytes, elapsed)
+    launches = -(-n_local // pool)
+    mean_ms = sum(kern_ms) / len(kern_ms) / launches
+    rank_ms = gather(mean_ms, world, rank, coll_dev)
 
     extras = {}
+    if not args.no_extras:
+        extras["end_to_end_host_all_ranks"] = host_leg(r, v, k, p, L, stream, world, rank,
+                                                       coll_dev)
     if rank == 0 and not args.no_extras and world == 1:  # single-GPU legs
-        extras = extra_legs(r, v, k, p, L, min(pool, 256), stream)
+        extras.update(extra_legs(r, v, k, p, L, min(pool, 256), stream))
         if (k, p, L) == (10, 4, 16 * MiB):
             extras["other_configs"] = other_configs(stream)
 
     if rank == 0:
-        launches = -(-n_local // pool)
         per_launch_bytes = n_local * stripe_bytes / launches
-        mean_ms = sum(kern_ms) / len(kern_ms) / launches
         achieved = per_launch_bytes / (mean_ms * 1e-3) / 1e9
         workload = f"gf8 {k}+{p} x {args.shard_mib} MiB encode, {pool} stripes/launch"
-        tr = load_traffic(workload, kernel)
+        tr = load_traffic(workload, kernel_id)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
-                "kernel": kernel, "kernel_ms_per_launch": round(mean_ms, 4),
+                "traffic_source": ({"file": tr["file"], "kernel_id": tr["kernel_id"],
+                                    "commit": tr.get("commit")} if tr else None),
+                "kernel": kernel, "kernel_id": kernel_id,
+                "kernel_ms_per_launch": round(mean_ms, 4),
+                "kernel_ms_per_launch_per_rank": [round(x, 4) for x in rank_ms],
                 "algorithmic_bytes_per_launch": int(per_launch_bytes)}
-        cpu = cpu_par = None
+        cpu = {}
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(k, p, L, args.cpu_seconds)
-            cpu_par = cpu_baseline_parallel(k, p, L, args.cpu_seconds,
-                                            min(16, len(os.sched_getaffinity(0))))
+            cpu = cpu_baselines(args.cpu_seconds, cpu_threads())
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -303,11 +416,14 @@ def main(argv=None):
                        "parity_shards": p, "shard_bytes": L,
                        "stripes_per_gpu_per_step": n_local, "global_stripes_per_step":
                        total_stripes, "parallelism": f"stripes split over {world} GPU(s), no collective",
-                       "parity_check_vs_reference": check},
-            "roofline": roof, "cpu_baseline": cpu,
+                       "parity_check_vs_reference": check,
+                       "parity_check_per_rank": [int(x) for x in verdicts],
+                       "parity_checked_stripes_rank0": checked},
+            "roofline": roof, "cpu_baseline": cpu.get("cpu_baseline"),
         }
-        if cpu_par:
-            line["cpu_baseline_all_cores"] = cpu_par
+        for key in ("cpu_baseline_legs", "cpu_host"):
+            if key in cpu:
+                line[key] = cpu[key]
         line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -490,6 +606,33 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
         "MB_per_s": round(ns * (k + p) * L / dt / MiB, 1),
         "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1),
         "raw_pinned_h2d_copy_GB_per_s": round(raw_h2d, 1), "parity_matches_device": ok}
+    # the decode direction from host memory: data shards 0 and 1 of every
+    # stripe lost; only the k valid shards go up, only the 2 rebuilt come back
+    want = hflat.view(ns, k + p, L)[:, :2].clone()
+    pres = [[i not in (0, 1) for i in range(k + p)]] * ns
+    hflat.view(ns, k + p, L)[:, :2].zero_()
+    r.reconstruct_host_batch(hflat, L, ns, pres, data_only=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hflat.view(ns, k + p, L)[:, :2].zero_()
+        r.reconstruct_host_batch(hflat, L, ns, pres, data_only=True)
+    dt = (time.perf_counter() - t0) / reps
+    ok = torch.equal(hflat.view(ns, k + p, L)[:, :2], want)
+    out["end_to_end_pinned_host_reconstruct"] = {
+        "what": f"rse_reconstruct_host_batch (data_only), {ns} stripes in pinned host memory, "
+                "data shards 0,1 erased: H2D of the 10 valid shards, kernel, D2H of 2",
+        "MB_per_s": round(ns * (k + 2) * L / dt / MiB, 1),
+        "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1),
+        "raw_pinned_h2d_copy_GB_per_s": round(raw_h2d, 1), "rebuilt_matches": ok}
+    # verify from host memory (reads all k + p shards over PCIe)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oks = r.verify_host_flat(hflat, L, ns)
+    dt = (time.perf_counter() - t0) / reps
+    out["end_to_end_pinned_host_verify"] = {
+        "what": f"rse_verify_host_flat, {ns} stripes in pinned host memory (H2D of k + p shards)",
+        "MB_per_s": round(ns * (k + p) * L / dt / MiB, 1),
+        "GB_per_s_pcie_h2d": round(ns * (k + p) * L / dt / 1e9, 1), "all_ok": bool(oks.all())}
     return out
 
 

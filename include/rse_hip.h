@@ -17,7 +17,9 @@
  *  - On any error nothing is written (core.rs:673-676).
  *  - Work is enqueued on `stream` (a hipStream_t; NULL = the legacy default
  *    stream) and runs asynchronously, except verify*, whose boolean result
- *    requires a stream synchronisation before returning.
+ *    requires a stream synchronisation before returning.  Each call runs on
+ *    the device that owns `stream` (NULL: the current device); the caller's
+ *    current device is restored on return.
  *  - A codec is immutable after rse_codec_new except for its mutex-guarded
  *    decode-matrix LRU cache (capacity 254, core.rs:24), so concurrent calls on
  *    different streams are allowed (core.rs:349).
@@ -67,6 +69,11 @@ const char *rse_strerror(int status);
 int rse_last_device_error(void);
 /* Library version string. */
 const char *rse_version(void);
+/* Identity of the last coding kernel this thread launched, e.g. "bitslice gf8
+ * 10+4 v1 nt1" (compiled-in bit-sliced), "bitslice-jit gf16 12+8" (specialised
+ * at run time), "table gf8 50+20 fused nt1"; "" before the first launch.
+ * Diagnostics: profiles are attributed to the kernel that actually ran. */
+const char *rse_last_kernel(void);
 
 /* ---- codec: core.rs:343-923 ------------------------------------------ */
 /* ReedSolomon::new (core.rs:445-467): TooFewDataShards / TooFewParityShards /
@@ -170,11 +177,33 @@ int rse_reconstruct_batch(const rse_codec *codec, void *stripes, size_t shard_le
 int rse_code_shards(int field, const uint8_t *rows, size_t n_out, size_t n_in,
                     const void *const *inputs, void *const *outputs, size_t len,
                     int accumulate, rse_stream_t stream);
-/* The reference FFI kernel's contract (reedsolomon_gal_mul(_xor),
- * simd_c/reedsolomon.h:30-42) on device memory: out = c*in (or out ^= c*in)
- * over GF(2^8).  Returns RSE_OK; the whole length is processed (no tail). */
+/* rse_code_shards on HOST inputs and outputs (the host pipeline above): the
+ * one hook that puts the reference's code_some_slices (core.rs:481-490) on
+ * the GPU unchanged -- encode, verify and reconstruct all funnel into it
+ * (core.rs:522, 629, 861, 918).  Synchronous. */
+int rse_code_shards_host(int field, const uint8_t *rows, size_t n_out, size_t n_in,
+                         const void *const *inputs, void *const *outputs, size_t len,
+                         int accumulate, rse_stream_t stream);
+/* galois_8 mul_slice / mul_slice_xor (galois_8.rs:291-327) on device memory:
+ * out = c*in (or out ^= c*in) over GF(2^8), asynchronous on `stream`. */
 int rse_gf8_mul_slice(uint8_t c, const void *in, void *out, size_t len, int xor_into,
                       rse_stream_t stream);
+/* The reference FFI kernel itself, same signature and contract:
+ * reedsolomon_gal_mul / reedsolomon_gal_mul_xor (simd_c/reedsolomon.h:30-42,
+ * bound at galois_8.rs:267-283).  low/high are the coefficient's 16-entry
+ * nibble tables (MUL_TABLE_LOW/HIGH[c], build.rs:75-94; host memory), in/out
+ * DEVICE memory.  Returns the bytes processed -- always len (no scalar tail
+ * for the caller to finish, galois_8.rs:301-304) -- or 0 on error.  Runs on
+ * the null stream and returns when done, as the CPU kernel does. */
+size_t rse_gal_mul(const uint8_t *low, const uint8_t *high, const uint8_t *in, uint8_t *out,
+                   size_t len);
+size_t rse_gal_mul_xor(const uint8_t *low, const uint8_t *high, const uint8_t *in, uint8_t *out,
+                       size_t len);
+/* galois_16's Field::mul_slice / mul_slice_add (the trait defaults,
+ * lib.rs:99-118) on device memory: c is one [u8;2] element {coefficient of x,
+ * constant}; len counts elements.  add_into = 0: out = c*in, 1: out += c*in. */
+int rse_gf16_mul_slice(const uint8_t *c, const void *in, void *out, size_t len, int add_into,
+                       rse_stream_t stream);
 
 /* ---- device matrix inversion (matrix.rs:249-261 semantics) ----------- */
 /* Invert `batch` n x n GF(2^8) matrices (device memory, row-major, n <= 255),
@@ -183,14 +212,45 @@ int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, si
                          size_t batch, rse_stream_t stream);
 
 /* ---- host-memory (end-to-end) path ----------------------------------- */
-/* encode with host shards: data staged H2D through pinned buffers, parity
- * staged D2H, chunked and double-buffered on `stream`.  Synchronous. */
+/* The reference API's own form: shards are caller slices in HOST memory
+ * (core.rs:597-695).  Each call pipelines chunks of every shard through the
+ * device -- H2D of the shards the operation reads, the kernels, D2H of the
+ * shards it writes, on separate streams over a ring of device buffers -- and
+ * returns when the results are in host memory (synchronous).  Only what the
+ * operation needs crosses PCIe: reconstruct uploads the k valid shards of
+ * core.rs:801-841 and downloads only the rebuilt ones.  Pinned host memory
+ * gives overlapped DMA; pageable memory works but serialises the copies.
+ * Same validation, error precedence and results as the device entries. */
+/* encode (core.rs:597-611) */
 int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *lens,
                     size_t n_shards, rse_stream_t stream);
 /* Flat host stripes (rse_encode_flat layout, HOST memory): the same pipeline
  * over every chunk of every stripe, so PCIe stays busy across stripes. */
 int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len,
                          size_t n_stripes, rse_stream_t stream);
+/* verify (core.rs:637-651) / verify_with_buffer (core.rs:654-669; the host
+ * buffer receives the correct parity on RSE_OK) */
+int rse_verify_host(const rse_codec *codec, const void *const *shards, const size_t *lens,
+                    size_t n_shards, int *ok, rse_stream_t stream);
+int rse_verify_with_buffer_host(const rse_codec *codec, const void *const *shards,
+                                const size_t *lens, size_t n_shards, void *const *buffer,
+                                const size_t *buffer_lens, size_t n_buffer, int *ok,
+                                rse_stream_t stream);
+/* rse_verify_flat over flat HOST stripes: ok[s] per stripe. */
+int rse_verify_host_flat(const rse_codec *codec, const void *stripes, size_t shard_len,
+                         size_t n_stripes, uint8_t *ok, rse_stream_t stream);
+/* reconstruct / reconstruct_data (core.rs:680-695) with (T, bool) semantics,
+ * as rse_reconstruct / rse_reconstruct_data. */
+int rse_reconstruct_host(const rse_codec *codec, void *const *shards, const size_t *lens,
+                         const uint8_t *present, size_t n_shards, rse_stream_t stream);
+int rse_reconstruct_data_host(const rse_codec *codec, void *const *shards, const size_t *lens,
+                              const uint8_t *present, size_t n_shards, rse_stream_t stream);
+/* rse_reconstruct_batch over flat HOST stripes: every stripe its own erasure
+ * pattern (present: n_stripes x (k+p)); stripes with nothing missing move no
+ * bytes.  Errors are detected before any stripe is touched. */
+int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t shard_len,
+                               size_t n_stripes, const uint8_t *present, int data_only,
+                               rse_stream_t stream);
 
 /* ---- launch-shape options (performance only; results never change) ----- */
 #define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */
@@ -201,8 +261,8 @@ int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len
 #define RSE_OPT_BITSLICE 5          /* 1: bit-sliced kernels for compiled codecs (default) */
 #define RSE_OPT_BITSLICE_LAUNCHES 6 /* read-only, per thread: number of bit-sliced kernel
                                        launches so far (diagnostics / tests) */
-#define RSE_OPT_HOST_CHUNK_KIB 7    /* rse_encode_host*: bytes per shard per pipeline chunk, KiB */
-#define RSE_OPT_HOST_H2D_STREAMS 8  /* rse_encode_host*: streams carrying H2D copies (1..4) */
+#define RSE_OPT_HOST_CHUNK_KIB 7    /* rse_*_host*: bytes per shard per pipeline chunk, KiB */
+#define RSE_OPT_HOST_H2D_STREAMS 8  /* rse_*_host*: streams carrying H2D copies (1..4) */
 #define RSE_OPT_JIT 9               /* run-time specialised kernels: 0 off, 1 used once built
                                        (default), 2 the first launch waits for the build */
 #define RSE_OPT_JIT_MODULES 10      /* read-only: specialised modules built in this process */

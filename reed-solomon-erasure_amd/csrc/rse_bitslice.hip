@@ -530,6 +530,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   BsFn f16 = nullptr, f4 = nullptr;
   hipFunction_t j16 = nullptr, j4 = nullptr;
   bool compiled = false;
+  int vopt_used = -1;
   for (const BsShape& sh : kBsShapes) {
     if (a.accumulate) break;
     if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
@@ -543,6 +544,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                                      : (field == 16 ? kBsDefaultVariant16 : kBsDefaultVariant8);
     f16 = sh.fn[v][nt ? 1 : 0];
     if (!f16) f16 = sh.fn[v][1];
+    vopt_used = v;
     f4 = sh.w4;
     compiled = true;
     break;
@@ -574,6 +576,12 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   };
   // whole 16 KiB chunks, then whole 4 KiB chunks of the rest (one per wave)
   const uint64_t cps16 = a.n_vec / kV16, cps4 = (a.n_vec - cps16 * kV16) / kV4;
+  if (compiled)
+    note_kernel("bitslice gf%d %u+%u v%d nt%d%s", field, a.n_in, a.n_out,
+                (int)(vopt_used), nt ? 1 : 0, cps16 ? "" : " w4");
+  else
+    note_kernel("bitslice-jit gf%d %u+%u%s%s", field, a.n_in, a.n_out, a.accumulate ? " acc" : "",
+                cps16 ? "" : " w4");
   if (cps16) {
     const hipError_t e = launch(f16, j16, a, cps16, cps16 * a.n_stripes);
     if (e != hipSuccess) return e;
@@ -619,6 +627,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     for (int q = 0; q < 4 && slot < 0; ++q)
       if (sh.rec[q] && (1u << q) >= need) slot = q;
     if (slot < 0) return hipSuccess;
+    note_kernel("bitslice-recon gf%d %u+%u ns%d", field, k, p, 1 << slot);
     hipLaunchKernelGGL(sh.rec[slot], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -634,6 +643,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     if ((uint32_t)jf.rec_ns[q] >= need) slot = q;
   if (slot < 0) return hipSuccess;
   uint64_t cps_arg = cps;
+  note_kernel("bitslice-jit-recon gf%d %u+%u ns%d", field, k, p, jf.rec_ns[slot]);
   void* args[] = {const_cast<BsReconArgs*>(&a), &cps_arg};
   e = hipModuleLaunchKernel(jf.rec[slot], (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args,
                             nullptr);

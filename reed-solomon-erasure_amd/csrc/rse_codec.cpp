@@ -103,6 +103,31 @@ int check_multi(const size_t* lens, size_t n) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Every entry point works on the device that owns its stream: allocations
+// (per-thread verdict words), run-time specialised modules (loaded per device)
+// and launches all follow hipGetDevice, so for a stream of another device the
+// call makes that device current and restores the caller's on return.  The
+// null stream means the current device, as in HIP.
+class OnStreamDevice {
+ public:
+  explicit OnStreamDevice(void* stream) {
+    if (!stream) return;
+    int dev = 0, cur = 0;
+    if (hipStreamGetDevice(static_cast<hipStream_t>(stream), &dev) != hipSuccess) return;
+    if (hipGetDevice(&cur) != hipSuccess || cur == dev) return;
+    if (hipSetDevice(dev) == hipSuccess) prev_ = cur;
+  }
+  ~OnStreamDevice() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  OnStreamDevice(const OnStreamDevice&) = delete;
+  OnStreamDevice& operator=(const OnStreamDevice&) = delete;
+
+ private:
+  int prev_ = -1;
+};
+#define RSE_ON_STREAM(stream) OnStreamDevice rse_on_stream_device_(stream)
+
 // ------------------------------------------------------------- launching
 // One fused pass: outputs (+)= rows x inputs over len_bytes, chunked so every
 // launch fits the kernel-argument block (<= kMaxIn inputs, <= kMaxOut outputs).
@@ -286,7 +311,12 @@ int run_check(Job j, hipStream_t s, int* ok) {
   RSE_HIP(hipMemsetAsync(w->d, 0, words * sizeof(uint32_t), s));
   j.mismatch = w->d;
   int rc = run_job(j, s);
-  if (rc != RSE_OK) return rc;
+  if (rc != RSE_OK) {
+    // kernels already queued may still OR into this thread's words: drain
+    // them before the words can be reused by the thread's next verify
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
   RSE_HIP(hipMemcpyAsync(w->h, w->d, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   RSE_HIP(hipStreamSynchronize(s));
   for (size_t i = 0; i < words; ++i) ok[i] = w->h[i] == 0 ? 1 : 0;
@@ -325,7 +355,7 @@ void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
   if (wide)
-    rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data());
+    rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else
     rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
 }
@@ -616,7 +646,7 @@ bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes)
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
   if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
     if (mode < 2 && len_bytes < (1u << 20)) return false;
-    if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data())) return false;
+    if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data(), true)) return false;
     return rse::jit_blocks_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
   }
   if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), rse::kJitPattern)) return false;
@@ -690,9 +720,10 @@ int encode_single_sep_impl(const rse_codec* c, size_t i_data, const void* single
   return run_job(j, s);
 }
 
-int verify_impl(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
-                void* const* buffer, const size_t* buf_lens, size_t n_buf, bool with_buffer,
-                int* ok, hipStream_t s) {
+// verify / verify_with_buffer argument checks (core.rs:637-669 via macros.rs).
+int verify_checks(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+                  void* const* buffer, const size_t* buf_lens, size_t n_buf, bool with_buffer,
+                  int* ok) {
   int rc;
   if (!c || !ok) return RSE_ERR_INVALID_ARGUMENT;
   if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
@@ -706,6 +737,14 @@ int verify_impl(const rse_codec* c, const void* const* shards, const size_t* len
     if ((rc = check_multi(buf_lens, n_buf))) return rc;
     if (lens[0] != buf_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
   }
+  return RSE_OK;
+}
+
+int verify_impl(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+                void* const* buffer, const size_t* buf_lens, size_t n_buf, bool with_buffer,
+                int* ok, hipStream_t s) {
+  int rc = verify_checks(c, shards, lens, n, buffer, buf_lens, n_buf, with_buffer, ok);
+  if (rc) return rc;
   want_bitslice(c, lens[0] * c->esize());
   const Rows rows = parity_rows(c);
   Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(shards),
@@ -713,6 +752,242 @@ int verify_impl(const rse_codec* c, const void* const* shards, const size_t* len
         reinterpret_cast<const uint8_t* const*>(shards) + c->k, lens[0] * c->esize(),
         with_buffer ? rse::kCheckStore : rse::kCheck, false, nullptr, 0, 1};
   return run_check(j, s, ok);
+}
+
+// ------------------------------------------------------------ host memory
+// The reference's API takes caller slices in host memory (core.rs:597-695).
+// The *_host entries do the same work on host shards through a three-stage
+// pipeline over chunks of every shard: H2D of the shards the operation reads
+// (on one of RSE_OPT_HOST_H2D_STREAMS streams), the device operation on a
+// second stream, D2H of the shards it writes on a third.  A ring of device
+// buffer sets means chunk c's H2D overlaps chunk c-1's kernels and chunk c-2's
+// D2H (and H2D overlaps D2H on the full-duplex link).  Only the shards an
+// operation reads cross PCIe towards the device -- for reconstruct the k valid
+// shards of core.rs:801-841, not every present one -- and only the shards it
+// writes come back.  Pinned host memory gives asynchronous DMA; pageable
+// memory works (the runtime stages it) but serialises the copies.
+enum class HostOp { kEncode, kVerify, kVerifyBuf, kRecon, kReconData, kCode };
+
+struct HostStripe {
+  void* const* sh;         // the stripe's k + p host shards (kCode: inputs, then outputs)
+  void* const* buf;        // kVerifyBuf: its p host buffer shards
+  const uint8_t* present;  // kRecon*: its k + p presence flags
+};
+
+// Shards one stripe's operation reads (up) and writes (down); index total + r
+// is buffer shard r (verify_with_buffer).
+// kCode: inputs [0, k), outputs [k, T), read too when accumulating.
+void host_sets(uint32_t k, uint32_t T, uint32_t p, HostOp op, bool accumulate,
+               const uint8_t* present, std::vector<uint32_t>& up, std::vector<uint32_t>& down) {
+  up.clear();
+  down.clear();
+  switch (op) {
+    case HostOp::kCode:
+      for (uint32_t i = 0; i < T; ++i) {
+        if (i < k || accumulate) up.push_back(i);
+        if (i >= k) down.push_back(i);
+      }
+      break;
+    case HostOp::kEncode:
+      for (uint32_t i = 0; i < T; ++i) (i < k ? up : down).push_back(i);
+      break;
+    case HostOp::kVerify:
+    case HostOp::kVerifyBuf:
+      for (uint32_t i = 0; i < T; ++i) up.push_back(i);
+      if (op == HostOp::kVerifyBuf)
+        for (uint32_t r = 0; r < p; ++r) down.push_back(T + r);
+      break;
+    case HostOp::kRecon:
+    case HostOp::kReconData: {
+      uint32_t nv = 0;  // the valid inputs: the first k present shards
+      for (uint32_t i = 0; i < T; ++i) {
+        if (present[i]) {
+          if (nv < k) {
+            up.push_back(i);
+            ++nv;
+          }
+        } else if (i < k || op == HostOp::kRecon) {
+          down.push_back(i);
+        }
+      }
+      break;
+    }
+  }
+}
+
+// Copies bytes [off, off + sz) of the listed shards between the host and the
+// ring slot `dset` (shard i at dset + i * chunk): one 2D copy per run of
+// consecutive indices whose host shards are equally spaced (flat stripes),
+// one plain copy otherwise.
+template <class HostPtr>
+hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<uint32_t>& idx,
+                       HostPtr host, size_t off, size_t sz, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  for (size_t a = 0; a < idx.size() && e == hipSuccess;) {
+    size_t b = a + 1;
+    ptrdiff_t pitch = 0;
+    if (b < idx.size() && idx[b] == idx[a] + 1) pitch = host(idx[b]) - host(idx[a]);
+    if (pitch > 0 && (size_t)pitch >= sz)
+      while (b < idx.size() && idx[b] == idx[b - 1] + 1 && host(idx[b]) - host(idx[b - 1]) == pitch)
+        ++b;
+    else
+      b = a + 1;
+    uint8_t* d = dset + (size_t)idx[a] * chunk;
+    uint8_t* h = host(idx[a]) + off;
+    const size_t rows = b - a;
+    if (rows == 1)
+      e = hipMemcpyAsync(h2d ? d : h, h2d ? h : d, sz,
+                         h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s);
+    else if (h2d)
+      e = hipMemcpy2DAsync(d, chunk, h, (size_t)pitch, sz, rows, hipMemcpyHostToDevice, s);
+    else
+      e = hipMemcpy2DAsync(h, (size_t)pitch, d, chunk, sz, rows, hipMemcpyDeviceToHost, s);
+    a = b;
+  }
+  return e;
+}
+
+// The low-level op (rse_code_shards_host): rows over n_in inputs.
+struct HostCode {
+  int field;
+  const Rows* rows;
+  bool accumulate;
+};
+
+// Runs `op` over `bytes` of every shard of every stripe (codec ops: `c`;
+// kCode: `code`).  verify ops: ok[s] receives stripe s's verdict.
+int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& stripes,
+                  size_t bytes, hipStream_t user, int* ok, const HostCode* code = nullptr) {
+  const int64_t chunk_kib = rse::get_option(RSE_OPT_HOST_CHUNK_KIB);
+  const int nh = (int)std::max<int64_t>(1, std::min<int64_t>(4, rse::get_option(RSE_OPT_HOST_H2D_STREAMS)));
+  const int ring = std::max(3, nh + 2);  // slots: nh filling, one coding, one draining
+  const size_t chunk = std::min<size_t>(bytes, (size_t)std::max<int64_t>(64, chunk_kib) << 10);
+  const size_t per_stripe = (bytes + chunk - 1) / chunk;
+  const size_t nchunks = per_stripe * stripes.size();
+  const bool verify = op == HostOp::kVerify || op == HostOp::kVerifyBuf;
+  const bool low = op == HostOp::kCode;
+  const int field = low ? code->field : c->field;
+  const size_t k = low ? code->rows->n_in : c->k;
+  const size_t T = low ? k + code->rows->n_out : c->total;
+  const size_t p = T - k, es = field == RSE_FIELD_GF16 ? 2 : 1;
+  const size_t nbuf = T + (op == HostOp::kVerifyBuf ? p : 0);  // shards per slot
+  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H
+  std::vector<hipStream_t> st(nh + 2, nullptr);
+  std::vector<hipEvent_t> h2d(ring, nullptr), coded(ring, nullptr), d2h(ring, nullptr);
+  uint8_t* dbuf = nullptr;
+  uint32_t *dwords = nullptr, *hwords = nullptr;
+  hipEvent_t start = nullptr;
+  hipError_t e = hipSuccess;
+  for (auto& q : st)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+  for (auto* ev : {&h2d, &coded, &d2h})
+    for (auto& q : *ev)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&start, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), ring * nbuf * chunk, user);
+  if (verify) {  // one mismatch word per stripe
+    const size_t wb = stripes.size() * sizeof(uint32_t);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dwords), wb, user);
+    if (e == hipSuccess) e = hipMemsetAsync(dwords, 0, wb, user);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hwords), wb, hipHostMallocDefault);
+  }
+  if (e == hipSuccess) e = hipEventRecord(start, user);  // everything starts after the caller's work
+  for (auto& q : st)
+    if (e == hipSuccess) e = hipStreamWaitEvent(q, start, 0);
+  if (op == HostOp::kEncode || verify) want_bitslice(c, chunk);
+  const Rows rows = low ? Rows{} : parity_rows(c);
+  const Rows& code_rows = low ? *code->rows : rows;
+  std::vector<uint8_t*> dev(nbuf);
+  std::vector<size_t> lens(T);
+  std::vector<uint32_t> up, down;
+  hipStream_t kst = st[nh], dst = st[nh + 1];
+  int rc = RSE_OK;
+  size_t set_for = ~size_t(0);
+  for (size_t ci = 0; e == hipSuccess && rc == RSE_OK && ci < nchunks; ++ci) {
+    const size_t si = ci / per_stripe;
+    const HostStripe& hs = stripes[si];
+    if (si != set_for) {
+      host_sets((uint32_t)k, (uint32_t)T, (uint32_t)p, op, low && code->accumulate, hs.present,
+                up, down);
+      set_for = si;
+    }
+    if (down.empty() && !verify) continue;  // nothing to rebuild in this stripe
+    const size_t off = (ci % per_stripe) * chunk, sz = std::min(chunk, bytes - off);
+    const int b = (int)(ci % ring);
+    hipStream_t hst = st[ci % nh];
+    uint8_t* set = dbuf + b * nbuf * chunk;
+    auto host = [&](uint32_t i) {
+      return static_cast<uint8_t*>(i < T ? hs.sh[i] : hs.buf[i - T]);
+    };
+    if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);  // slot drained
+    if (e == hipSuccess) e = copy_shards(true, set, chunk, up, host, off, sz, hst);
+    if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
+    if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
+    if (e != hipSuccess) break;
+    for (size_t i = 0; i < nbuf; ++i) dev[i] = set + i * chunk;
+    switch (op) {
+      case HostOp::kEncode:
+      case HostOp::kCode: {
+        Job j{field, &code_rows, dev.data(), dev.data() + k, nullptr, sz, rse::kStore,
+              low && code->accumulate, nullptr, 0, 1};
+        rc = run_job(j, kst);
+        break;
+      }
+      case HostOp::kVerify:
+      case HostOp::kVerifyBuf: {
+        const bool wb = op == HostOp::kVerifyBuf;
+        Job j{field, &rows, dev.data(), wb ? dev.data() + T : nullptr, dev.data() + k, sz,
+              wb ? rse::kCheckStore : rse::kCheck, false, dwords + si, 0, 1};
+        rc = run_job(j, kst);
+        break;
+      }
+      case HostOp::kRecon:
+      case HostOp::kReconData:
+        std::fill(lens.begin(), lens.end(), sz / es);
+        rc = reconstruct_impl(c, reinterpret_cast<void* const*>(dev.data()), lens.data(),
+                              hs.present, T, op == HostOp::kReconData, kst);
+        break;
+    }
+    if (rc) break;
+    e = hipEventRecord(coded[b], kst);
+    if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
+    if (e == hipSuccess) e = copy_shards(false, set, chunk, down, host, off, sz, dst);
+    if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
+  }
+  // join: the caller's stream waits for every stream, frees the ring, syncs
+  hipError_t e2 = hipSuccess;
+  for (auto& q : st)
+    if (q && e2 == hipSuccess) {
+      e2 = hipEventRecord(start, q);
+      if (e2 == hipSuccess) e2 = hipStreamWaitEvent(user, start, 0);
+    }
+  if (verify && dwords && hwords && e == hipSuccess && e2 == hipSuccess && rc == RSE_OK)
+    e2 = hipMemcpyAsync(hwords, dwords, stripes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        user);
+  if (dbuf) (void)hipFreeAsync(dbuf, user);
+  if (dwords) (void)hipFreeAsync(dwords, user);
+  const hipError_t e3 = hipStreamSynchronize(user);
+  if (e2 == hipSuccess) e2 = e3;
+  if (verify && ok && hwords && e == hipSuccess && e2 == hipSuccess && rc == RSE_OK)
+    for (size_t s = 0; s < stripes.size(); ++s) ok[s] = hwords[s] == 0 ? 1 : 0;
+  if (hwords) (void)hipHostFree(hwords);
+  for (auto* ev : {&h2d, &coded, &d2h})
+    for (auto& q : *ev)
+      if (q) (void)hipEventDestroy(q);
+  for (auto& q : st)
+    if (q) (void)hipStreamDestroy(q);
+  if (start) (void)hipEventDestroy(start);
+  if (rc) return rc;
+  if (e != hipSuccess) return dev_fail(e);
+  if (e2 != hipSuccess) return dev_fail(e2);
+  return RSE_OK;
+}
+
+// Flat host stripes: shard i of stripe s at base + (s * total + i) * sb.
+std::vector<void*> flat_ptrs(const rse_codec* c, void* base, size_t sb, size_t n_stripes) {
+  std::vector<void*> ptrs(n_stripes * c->total);
+  for (size_t i = 0; i < ptrs.size(); ++i) ptrs[i] = static_cast<uint8_t*>(base) + i * sb;
+  return ptrs;
 }
 
 }  // namespace
@@ -747,6 +1022,7 @@ const char* rse_strerror(int status) {
 }
 
 int rse_last_device_error(void) { return g_last_hip_error; }
+const char* rse_last_kernel(void) { return rse::last_kernel(); }
 const char* rse_version(void) { return "rse-mi355x 0.1.0 (gfx950)"; }
 
 int rse_codec_new(int field, size_t data_shards, size_t parity_shards, rse_codec** out) {
@@ -826,6 +1102,7 @@ int rse_codec_matrix(const rse_codec* c, uint8_t* out, size_t out_bytes) {
 
 int rse_encode(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
                rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   int rc;
   if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
@@ -838,6 +1115,7 @@ int rse_encode(const rse_codec* c, void* const* shards, const size_t* lens, size
 int rse_encode_sep(const rse_codec* c, const void* const* data, const size_t* data_lens,
                    size_t n_data, void* const* parity, const size_t* parity_lens,
                    size_t n_parity, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   return encode_sep_impl(c, data, data_lens, n_data, parity, parity_lens, n_parity,
                          (hipStream_t)stream);
@@ -845,6 +1123,7 @@ int rse_encode_sep(const rse_codec* c, const void* const* data, const size_t* da
 
 int rse_encode_single(const rse_codec* c, size_t i_data, void* const* shards, const size_t* lens,
                       size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   int rc;
   if (i_data >= c->k) return RSE_INVALID_INDEX;  // core.rs:552
@@ -858,6 +1137,7 @@ int rse_encode_single(const rse_codec* c, size_t i_data, void* const* shards, co
 int rse_encode_single_sep(const rse_codec* c, size_t i_data, const void* single,
                           size_t single_len, void* const* parity, const size_t* parity_lens,
                           size_t n_parity, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   return encode_single_sep_impl(c, i_data, single, single_len, parity, parity_lens, n_parity,
                                 (hipStream_t)stream);
@@ -865,27 +1145,32 @@ int rse_encode_single_sep(const rse_codec* c, size_t i_data, const void* single,
 
 int rse_verify(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
                int* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   return verify_impl(c, shards, lens, n, nullptr, nullptr, 0, false, ok, (hipStream_t)stream);
 }
 
 int rse_verify_with_buffer(const rse_codec* c, const void* const* shards, const size_t* lens,
                            size_t n, void* const* buffer, const size_t* buf_lens, size_t n_buf,
                            int* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   return verify_impl(c, shards, lens, n, buffer, buf_lens, n_buf, true, ok, (hipStream_t)stream);
 }
 
 int rse_reconstruct(const rse_codec* c, void* const* shards, const size_t* lens,
                     const uint8_t* present, size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   return reconstruct_impl(c, shards, lens, present, n, false, (hipStream_t)stream);
 }
 
 int rse_reconstruct_data(const rse_codec* c, void* const* shards, const size_t* lens,
                          const uint8_t* present, size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   return reconstruct_impl(c, shards, lens, present, n, true, (hipStream_t)stream);
 }
 
 int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
                     rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c || !stripes) return RSE_ERR_INVALID_ARGUMENT;
   if (shard_len == 0) return RSE_EMPTY_SHARD;
   if (n_stripes == 0) return RSE_OK;
@@ -904,6 +1189,7 @@ int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t 
 
 int rse_verify_flat(const rse_codec* c, const void* stripes, size_t shard_len, size_t n_stripes,
                     uint8_t* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c || !stripes || !ok) return RSE_ERR_INVALID_ARGUMENT;
   if (shard_len == 0) return RSE_EMPTY_SHARD;
   if (n_stripes == 0) return RSE_OK;
@@ -930,6 +1216,7 @@ int rse_verify_flat(const rse_codec* c, const void* stripes, size_t shard_len, s
 
 int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_len,
                               size_t n_stripes, const uint8_t* present, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
   const size_t sb = shard_len * c->esize();
@@ -960,6 +1247,7 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
 // stripe untouched.
 int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
                           const uint8_t* present, int data_only, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
   const size_t k = c->k, p = c->p, T = c->total, sb = shard_len * c->esize();
@@ -1053,6 +1341,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
 int rse_code_shards(int field, const uint8_t* rows, size_t n_out, size_t n_in,
                     const void* const* inputs, void* const* outputs, size_t len, int accumulate,
                     rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if ((field != RSE_FIELD_GF8 && field != RSE_FIELD_GF16) || !rows || !inputs || !outputs)
     return RSE_ERR_INVALID_ARGUMENT;
   if (n_out == 0 || n_in == 0 || len == 0) return RSE_OK;
@@ -1076,8 +1365,56 @@ int rse_gf8_mul_slice(uint8_t c, const void* in, void* out, size_t len, int xor_
   return rse_code_shards(RSE_FIELD_GF8, &c, 1, 1, ins, outs, len, xor_into, stream);
 }
 
+int rse_code_shards_host(int field, const uint8_t* rows, size_t n_out, size_t n_in,
+                         const void* const* inputs, void* const* outputs, size_t len,
+                         int accumulate, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if ((field != RSE_FIELD_GF8 && field != RSE_FIELD_GF16) || !rows || !inputs || !outputs)
+    return RSE_ERR_INVALID_ARGUMENT;
+  if (n_out == 0 || n_in == 0 || len == 0) return RSE_OK;
+  const size_t es = field == RSE_FIELD_GF16 ? 2 : 1;
+  Rows r;
+  r.n_out = n_out;
+  r.n_in = n_in;
+  r.c.resize(n_out * n_in);
+  for (size_t i = 0; i < n_out * n_in; ++i)
+    r.c[i] = es == 2 ? (uint16_t)((rows[2 * i] << 8) | rows[2 * i + 1]) : rows[i];
+  std::vector<void*> ptrs(n_in + n_out);
+  for (size_t i = 0; i < n_in; ++i) ptrs[i] = const_cast<void*>(inputs[i]);
+  for (size_t o = 0; o < n_out; ++o) ptrs[n_in + o] = outputs[o];
+  for (void* q : ptrs)
+    if (!q) return RSE_ERR_INVALID_ARGUMENT;
+  const HostCode hc{field, &r, accumulate != 0};
+  return host_pipeline(nullptr, HostOp::kCode, {HostStripe{ptrs.data(), nullptr, nullptr}},
+                       len * es, (hipStream_t)stream, nullptr, &hc);
+}
+
+size_t rse_gal_mul(const uint8_t* low, const uint8_t* high, const uint8_t* in, uint8_t* out,
+                   size_t len) {
+  // low[n] = c * n and high[n] = c * (n << 4) (build.rs:75-94), so c = low[1]
+  if (!low || !high || (len && (!in || !out))) return 0;
+  if (rse_gf8_mul_slice(low[1], in, out, len, 0, nullptr) != RSE_OK) return 0;
+  return hipDeviceSynchronize() == hipSuccess ? len : 0;
+}
+
+size_t rse_gal_mul_xor(const uint8_t* low, const uint8_t* high, const uint8_t* in, uint8_t* out,
+                       size_t len) {
+  if (!low || !high || (len && (!in || !out))) return 0;
+  if (rse_gf8_mul_slice(low[1], in, out, len, 1, nullptr) != RSE_OK) return 0;
+  return hipDeviceSynchronize() == hipSuccess ? len : 0;
+}
+
+int rse_gf16_mul_slice(const uint8_t* c, const void* in, void* out, size_t len, int add_into,
+                       rse_stream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  const void* ins[1] = {in};
+  void* outs[1] = {out};
+  return rse_code_shards(RSE_FIELD_GF16, c, 1, 1, ins, outs, len, add_into, stream);
+}
+
 int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
                          size_t batch, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!d_in || !d_out || !d_singular || n == 0 || n > 255 || batch == 0 || batch > 0x7fffffff)
     return RSE_ERR_INVALID_ARGUMENT;
   RSE_HIP(rse::launch_gf8_invert(static_cast<const uint8_t*>(d_in), static_cast<uint8_t*>(d_out),
@@ -1085,108 +1422,9 @@ int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, si
   return RSE_OK;
 }
 
-// Host shards in, host parity out: a three-stage pipeline over chunks of every
-// shard (H2D of the data chunk on one of RSE_OPT_HOST_H2D_STREAMS streams, the
-// coding kernel on another, D2H of the parity chunk on a third), with a ring
-// of device buffer sets so chunk c's H2D overlaps chunk c-1's kernel and chunk
-// c-2's D2H (and H2D overlaps D2H on the full-duplex link).  Pinned host memory gives truly
-// asynchronous DMA; pageable memory works (the runtime stages it) but
-// serialises the copies.  `stripes` lists, per stripe, the k data pointers
-// then the p parity pointers.
-int encode_host_pipeline(const rse_codec* c, const std::vector<void* const*>& stripes,
-                         size_t bytes, hipStream_t user) {
-  const int64_t chunk_kib = rse::get_option(RSE_OPT_HOST_CHUNK_KIB);
-  const int nh = (int)std::max<int64_t>(1, std::min<int64_t>(4, rse::get_option(RSE_OPT_HOST_H2D_STREAMS)));
-  const int ring = std::max(3, nh + 2);  // slots: nh filling, one coding, one draining
-  const size_t chunk = std::min<size_t>(bytes, (size_t)std::max<int64_t>(64, chunk_kib) << 10);
-  const size_t per_stripe = (bytes + chunk - 1) / chunk;
-  const size_t nchunks = per_stripe * stripes.size();
-  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H
-  std::vector<hipStream_t> st(nh + 2, nullptr);
-  std::vector<hipEvent_t> h2d(ring, nullptr), coded(ring, nullptr), d2h(ring, nullptr);
-  uint8_t* dbuf = nullptr;
-  hipEvent_t start = nullptr;
-  hipError_t e = hipSuccess;
-  for (auto& q : st)
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
-  for (auto* ev : {&h2d, &coded, &d2h})
-    for (auto& q : *ev)
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), ring * c->total * chunk, user);
-  if (e == hipSuccess) e = hipEventRecord(start, user);  // everything starts after the caller's work
-  for (auto& q : st)
-    if (e == hipSuccess) e = hipStreamWaitEvent(q, start, 0);
-  want_bitslice(c, chunk);
-  const Rows rows = parity_rows(c);
-  std::vector<const uint8_t*> in(c->k);
-  std::vector<uint8_t*> out(c->p);
-  hipStream_t kst = st[nh], dst = st[nh + 1];
-  int rc = RSE_OK;
-  for (size_t ci = 0; e == hipSuccess && rc == RSE_OK && ci < nchunks; ++ci) {
-    void* const* sh = stripes[ci / per_stripe];
-    const size_t off = (ci % per_stripe) * chunk, sz = std::min(chunk, bytes - off);
-    const int b = (int)(ci % ring);
-    hipStream_t hst = st[ci % nh];
-    uint8_t* set = dbuf + b * c->total * chunk;
-    // H2D: the slot's previous D2H must have drained
-    if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);
-    for (size_t i = 0; i < c->k; ++i) in[i] = set + i * chunk;
-    // equally spaced host shards (flat stripes): one 2D copy for all k chunks
-    const ptrdiff_t pitch = c->k > 1 ? static_cast<uint8_t*>(sh[1]) - static_cast<uint8_t*>(sh[0]) : 0;
-    bool strided = c->k > 1 && pitch > 0 && (size_t)pitch >= sz;
-    for (size_t i = 2; strided && i < c->total; ++i)
-      strided = static_cast<uint8_t*>(sh[i]) - static_cast<uint8_t*>(sh[i - 1]) == pitch;
-    if (e == hipSuccess && strided) {
-      e = hipMemcpy2DAsync(set, chunk, static_cast<uint8_t*>(sh[0]) + off, (size_t)pitch, sz, c->k,
-                           hipMemcpyHostToDevice, hst);
-    } else {
-      for (size_t i = 0; e == hipSuccess && i < c->k; ++i)
-        e = hipMemcpyAsync(set + i * chunk, static_cast<uint8_t*>(sh[i]) + off, sz,
-                           hipMemcpyHostToDevice, hst);
-    }
-    if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
-    if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
-    if (e != hipSuccess) break;
-    for (size_t r = 0; r < c->p; ++r) out[r] = set + (c->k + r) * chunk;
-    Job j{c->field, &rows, in.data(), out.data(), nullptr, sz, rse::kStore, false, nullptr, 0, 1};
-    rc = run_job(j, kst);
-    if (rc) break;
-    e = hipEventRecord(coded[b], kst);
-    if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
-    if (e == hipSuccess && strided && c->p > 1) {
-      e = hipMemcpy2DAsync(static_cast<uint8_t*>(sh[c->k]) + off, (size_t)pitch, out[0], chunk, sz,
-                           c->p, hipMemcpyDeviceToHost, dst);
-    } else {
-      for (size_t r = 0; e == hipSuccess && r < c->p; ++r)
-        e = hipMemcpyAsync(static_cast<uint8_t*>(sh[c->k + r]) + off, out[r], sz,
-                           hipMemcpyDeviceToHost, dst);
-    }
-    if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
-  }
-  // join: the caller's stream waits for every stream, frees the ring, syncs
-  hipError_t e2 = hipSuccess;
-  for (auto& q : st)
-    if (q && e2 == hipSuccess) {
-      e2 = hipEventRecord(start, q);
-      if (e2 == hipSuccess) e2 = hipStreamWaitEvent(user, start, 0);
-    }
-  if (dbuf) (void)hipFreeAsync(dbuf, user);
-  if (e2 == hipSuccess) e2 = hipStreamSynchronize(user);
-  for (auto* ev : {&h2d, &coded, &d2h})
-    for (auto& q : *ev)
-      if (q) (void)hipEventDestroy(q);
-  for (auto& q : st)
-    if (q) (void)hipStreamDestroy(q);
-  if (start) (void)hipEventDestroy(start);
-  if (rc) return rc;
-  if (e != hipSuccess) return dev_fail(e);
-  if (e2 != hipSuccess) return dev_fail(e2);
-  return RSE_OK;
-}
-
 int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
                     rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   int rc;
   if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
@@ -1194,23 +1432,111 @@ int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens,
   if ((rc = check_multi(lens, n))) return rc;
   for (size_t i = 0; i < n; ++i)
     if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
-  return encode_host_pipeline(c, {shards}, lens[0] * c->esize(), (hipStream_t)stream);
+  return host_pipeline(c, HostOp::kEncode, {HostStripe{shards, nullptr, nullptr}},
+                       lens[0] * c->esize(), (hipStream_t)stream, nullptr);
 }
 
 int rse_encode_host_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
                          rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!c || !stripes) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
   if (shard_len == 0) return RSE_EMPTY_SHARD;
   const size_t sb = shard_len * c->esize();
-  std::vector<void*> ptrs(n_stripes * c->total);
-  std::vector<void* const*> list(n_stripes);
-  for (size_t s = 0; s < n_stripes; ++s) {
-    for (size_t i = 0; i < c->total; ++i)
-      ptrs[s * c->total + i] = static_cast<uint8_t*>(stripes) + (s * c->total + i) * sb;
-    list[s] = &ptrs[s * c->total];
+  const std::vector<void*> ptrs = flat_ptrs(c, stripes, sb, n_stripes);
+  std::vector<HostStripe> list(n_stripes);
+  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr};
+  return host_pipeline(c, HostOp::kEncode, list, sb, (hipStream_t)stream, nullptr);
+}
+
+int rse_verify_host(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+                    int* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  int rc = verify_checks(c, shards, lens, n, nullptr, nullptr, 0, false, ok);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
+  return host_pipeline(c, HostOp::kVerify,
+                       {HostStripe{const_cast<void* const*>(shards), nullptr, nullptr}},
+                       lens[0] * c->esize(), (hipStream_t)stream, ok);
+}
+
+int rse_verify_with_buffer_host(const rse_codec* c, const void* const* shards, const size_t* lens,
+                                size_t n, void* const* buffer, const size_t* buf_lens,
+                                size_t n_buf, int* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  int rc = verify_checks(c, shards, lens, n, buffer, buf_lens, n_buf, true, ok);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
+  for (size_t i = 0; i < n_buf; ++i)
+    if (!buffer[i]) return RSE_ERR_INVALID_ARGUMENT;
+  return host_pipeline(c, HostOp::kVerifyBuf,
+                       {HostStripe{const_cast<void* const*>(shards), buffer, nullptr}},
+                       lens[0] * c->esize(), (hipStream_t)stream, ok);
+}
+
+int rse_verify_host_flat(const rse_codec* c, const void* stripes, size_t shard_len,
+                         size_t n_stripes, uint8_t* ok, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if (!c || !stripes || !ok) return RSE_ERR_INVALID_ARGUMENT;
+  if (shard_len == 0) return RSE_EMPTY_SHARD;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t sb = shard_len * c->esize();
+  const std::vector<void*> ptrs = flat_ptrs(c, const_cast<void*>(stripes), sb, n_stripes);
+  std::vector<HostStripe> list(n_stripes);
+  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr};
+  std::vector<int> res(n_stripes, 0);
+  const int rc = host_pipeline(c, HostOp::kVerify, list, sb, (hipStream_t)stream, res.data());
+  if (rc == RSE_OK)
+    for (size_t s = 0; s < n_stripes; ++s) ok[s] = (uint8_t)res[s];
+  return rc;
+}
+
+static int reconstruct_host_impl(const rse_codec* c, void* const* shards, const size_t* lens,
+                                 const uint8_t* present, size_t n, bool data_only,
+                                 hipStream_t stream) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  ReconPlan plan;  // validation only (core.rs:744-772, lib.rs:185-199): no memory is touched
+  int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
+  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  return host_pipeline(c, data_only ? HostOp::kReconData : HostOp::kRecon,
+                       {HostStripe{shards, nullptr, present}}, plan.len * c->esize(), stream,
+                       nullptr);
+}
+
+int rse_reconstruct_host(const rse_codec* c, void* const* shards, const size_t* lens,
+                         const uint8_t* present, size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  return reconstruct_host_impl(c, shards, lens, present, n, false, (hipStream_t)stream);
+}
+
+int rse_reconstruct_data_host(const rse_codec* c, void* const* shards, const size_t* lens,
+                              const uint8_t* present, size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  return reconstruct_host_impl(c, shards, lens, present, n, true, (hipStream_t)stream);
+}
+
+int rse_reconstruct_host_batch(const rse_codec* c, void* stripes, size_t shard_len,
+                               size_t n_stripes, const uint8_t* present, int data_only,
+                               rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
+  if (n_stripes == 0) return RSE_OK;
+  const size_t k = c->k, T = c->total;
+  for (size_t s = 0; s < n_stripes; ++s) {  // core.rs:747-772, stripe by stripe
+    size_t np = 0;
+    for (size_t i = 0; i < T; ++i) np += present[s * T + i] ? 1 : 0;
+    if (np && shard_len == 0) return RSE_EMPTY_SHARD;
+    if (np < k) return RSE_TOO_FEW_SHARDS_PRESENT;
   }
-  return encode_host_pipeline(c, list, sb, (hipStream_t)stream);
+  const size_t sb = shard_len * c->esize();
+  const std::vector<void*> ptrs = flat_ptrs(c, stripes, sb, n_stripes);
+  std::vector<HostStripe> list(n_stripes);
+  for (size_t s = 0; s < n_stripes; ++s)
+    list[s] = HostStripe{&ptrs[s * T], nullptr, present + s * T};
+  return host_pipeline(c, data_only ? HostOp::kReconData : HostOp::kRecon, list, sb,
+                       (hipStream_t)stream, nullptr);
 }
 
 int rse_set_option(int key, int64_t value) {
@@ -1223,6 +1549,7 @@ int64_t rse_get_option(int key) {
 
 int rse_fill_splitmix(void* dst, size_t nbytes, uint64_t seed, uint64_t shard_id,
                       rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
   if (!dst && nbytes) return RSE_ERR_INVALID_ARGUMENT;
   RSE_HIP(rse::launch_fill_splitmix(dst, nbytes, seed, shard_id, (hipStream_t)stream));
   return RSE_OK;

@@ -60,6 +60,7 @@ struct Entry {
   uint32_t k = 0, p = 0;
   std::vector<uint16_t> rows;  // p x k: a codec's parity rows, or a decode pattern's rows
   JitKind kind = kJitCodec;
+  bool pattern_block = false;  // a block of a decode pattern's rows (own budget)
   int stages = 2;              // kEnc only (decode pattern, block) or kEnc + kRec (codec)
   std::promise<std::shared_ptr<const Compiled>> promise[2];
   std::shared_future<std::shared_ptr<const Compiled>> built[2];
@@ -87,6 +88,12 @@ int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
 constexpr int kMaxPatterns = 64;
 int g_blocks = 0;  // wide-codec block entries (capped: kMaxBlocks)
 constexpr int kMaxBlocks = 256;
+// blocks of wide decode patterns: a separate budget, so patterns can never
+// use up the codecs' own (and never queue more than a few patterns' builds)
+int g_pattern_blocks = 0;
+constexpr int kMaxPatternBlocks = 64;
+constexpr int kMaxPendingPatternBlocks = 16;
+int g_pending_pattern_blocks = 0;  // queued, not yet built
 constexpr size_t kMaxPendingPatternJobs = 8;
 
 std::vector<std::unique_ptr<Entry>>& registry() {
@@ -359,6 +366,10 @@ class Worker {
         g_jobs[q].pop_front();
       }
       e->promise[stage].set_value(compile(*e, stage));
+      if (e->pattern_block) {
+        std::lock_guard<std::mutex> g(g_mu);
+        --g_pending_pattern_blocks;
+      }
     }
   }
   std::thread th_;
@@ -372,12 +383,13 @@ Worker& worker() {
 
 // Caller holds g_mu; rows[o * stride + i].  Queues the entry's builds.
 void add_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride,
-                JitKind kind) {
+                JitKind kind, bool pattern_block = false) {
   auto e = std::make_unique<Entry>();
   e->field = field;
   e->k = k;
   e->p = p;
   e->kind = kind;
+  e->pattern_block = pattern_block;
   e->stages = kind == kJitCodec ? 2 : 1;
   e->rows.resize((size_t)k * p);
   for (uint32_t o = 0; o < p; ++o)
@@ -387,7 +399,12 @@ void add_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t 
     g_jobs[queue_of(*e, st)].push_back(e.get());
   }
   if (kind == kJitPattern) ++g_patterns;
-  if (kind == kJitBlock || kind == kJitBlockAcc) ++g_blocks;
+  if (pattern_block) {
+    ++g_pattern_blocks;
+    ++g_pending_pattern_blocks;
+  } else if (kind == kJitBlock || kind == kJitBlockAcc) {
+    ++g_blocks;
+  }
   registry().push_back(std::move(e));
 }
 
@@ -447,7 +464,7 @@ int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKin
   return 1;
 }
 
-int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
+int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern) {
   if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || p == 0) return 0;
   registry();
   Worker& w = worker();
@@ -457,10 +474,13 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows)
     need += !find_locked(field, ni, no, rows + (size_t)o0 * k + i0, k, kind);
   });
   if (need == 0) return 1;
-  if (g_blocks + need > kMaxBlocks) return 0;
+  if (pattern ? (g_pattern_blocks + need > kMaxPatternBlocks ||
+                 g_pending_pattern_blocks + need > kMaxPendingPatternBlocks)
+              : g_blocks + need > kMaxBlocks)
+    return 0;
   for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
     const uint16_t* r = rows + (size_t)o0 * k + i0;
-    if (!find_locked(field, ni, no, r, k, kind)) add_locked(field, ni, no, r, k, kind);
+    if (!find_locked(field, ni, no, r, k, kind)) add_locked(field, ni, no, r, k, kind, pattern);
   });
   w.start();
   g_cv.notify_all();

@@ -23,6 +23,9 @@
 // (galois_16.rs:146-162 with reduce_from :97-107 folded in), so a GF(2^16)
 // shard is two GF(2^8) byte planes and one GF(2^16) coefficient is a 2x2 block
 // of GF(2^8) coefficients.  Planes are split/merged in registers with v_perm.
+#include <cstdarg>
+#include <cstdio>
+
 #include "rse_device.hpp"
 
 namespace rse {
@@ -758,6 +761,7 @@ struct Options {
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
+thread_local char g_last_kernel[128] = "";  // rse_last_kernel()
 
 // ---------------------------------------------------------------------------
 // splitmix64 fill (synthetic shards; same byte stream as oracle/oracle.py).
@@ -1012,12 +1016,16 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
       CodeArgs r = args;
       for (uint32_t i = 0; i < r.n_in; ++i) r.in[i] += done;
       for (uint32_t o = 0; o < r.n_out; ++o) {
-        r.out[o] += done;
+        if (r.out[o]) r.out[o] += done;  // null in kCheck mode
         if (r.cmp[o]) r.cmp[o] += done;
       }
       r.len -= done;
       r.n_vec -= done / 16u;
-      return launch_table(field, r, stream);
+      char keep[sizeof g_last_kernel];  // the bit-sliced launch is the one to report
+      __builtin_memcpy(keep, g_last_kernel, sizeof keep);
+      e = launch_table(field, r, stream);
+      __builtin_memcpy(g_last_kernel, keep, sizeof keep);
+      return e;
     }
   }
   return launch_table(field, args, stream);
@@ -1026,6 +1034,8 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream) {
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream) {
   const Variant* var = pick(field, args, g_opt.variant);
   KernelFn fn = var->fn[g_opt.nontemporal ? 1 : 0];
+  note_kernel("table gf%d %u+%u %s nt%d", field, args.n_in, args.n_out,
+              var->pipe ? "pipe" : "fused", (int)g_opt.nontemporal);
   uint64_t gy = g_opt.stripes_in_flight > 0 ? (uint64_t)g_opt.stripes_in_flight : args.n_stripes;
   if (gy > args.n_stripes) gy = args.n_stripes;
   if (gy > 65535) gy = 65535;
@@ -1089,6 +1099,14 @@ int set_option(int key, int64_t value) {
 }
 
 void count_bitslice_launch() { ++g_bs_launches; }
+
+void note_kernel(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_last_kernel, sizeof g_last_kernel, fmt, ap);
+  va_end(ap);
+}
+const char* last_kernel() { return g_last_kernel; }
 
 int64_t get_option(int key) {
   switch (key) {

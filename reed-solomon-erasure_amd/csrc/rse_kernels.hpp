@@ -150,7 +150,9 @@ int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKin
 // Registers every kJitBlock block of a wide codec's p x k parity rows -- all of
 // them or, past the block cap, none.  Blocks: rows [o0, o0 + 8) x inputs
 // [i0, i0 + 32), the chunking of run_job (rse_codec.cpp).
-int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows);
+// pattern: the rows are a wide decode pattern's (a separate, smaller budget:
+// patterns never take the codecs' blocks, and never queue without bound).
+int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern);
 // jit_status over all of a wide codec's blocks (the least ready one).
 int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 // 2 ready, 1 building, 0 not registered, -1 build failed; wait != 0 blocks
@@ -179,6 +181,10 @@ int64_t jit_modules_built();  // RSE_OPT_JIT_MODULES
 int set_option(int key, int64_t value);
 int64_t get_option(int key);
 void count_bitslice_launch();  // RSE_OPT_BITSLICE_LAUNCHES
+// Identity of the last coding kernel launched on this thread ("bitslice gf8
+// 10+4 v1 nt1", "table gf16 20+8 fused nt1", ...): rse_last_kernel().
+void note_kernel(const char* fmt, ...);
+const char* last_kernel();
 
 // Fill nbytes of device memory with the splitmix64 byte stream of
 // (seed, shard_id) -- identical to oracle/oracle.py: splitmix_bytes.

@@ -21,8 +21,12 @@ EXPORTS = (
     "rse_verify", "rse_verify_with_buffer", "rse_reconstruct", "rse_reconstruct_data",
     "rse_encode_flat", "rse_verify_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
     "rse_code_shards",
-    "rse_gf8_mul_slice", "rse_gf8_invert_batch", "rse_encode_host", "rse_encode_host_flat", "rse_fill_splitmix",
-    "rse_set_option", "rse_get_option",
+    "rse_code_shards_host", "rse_gf8_mul_slice", "rse_gal_mul", "rse_gal_mul_xor",
+    "rse_gf16_mul_slice", "rse_gf8_invert_batch",
+    "rse_encode_host", "rse_encode_host_flat", "rse_verify_host", "rse_verify_with_buffer_host",
+    "rse_verify_host_flat", "rse_reconstruct_host", "rse_reconstruct_data_host",
+    "rse_reconstruct_host_batch", "rse_fill_splitmix",
+    "rse_set_option", "rse_get_option", "rse_last_kernel",
 )
 
 _c = ctypes
@@ -61,6 +65,17 @@ _SIGS = {
     "rse_gf8_mul_slice": (_c.c_int, [_c.c_uint8, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "rse_encode_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
+    "rse_verify_host": (_c.c_int, [_vp, _vp, _szp, _sz, _ip, _vp]),
+    "rse_verify_with_buffer_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _ip, _vp]),
+    "rse_verify_host_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
+    "rse_reconstruct_host": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
+    "rse_reconstruct_data_host": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),
+    "rse_reconstruct_host_batch": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _c.c_int, _vp]),
+    "rse_code_shards_host": (_c.c_int, [_c.c_int, _u8p, _sz, _sz, _vp, _vp, _sz, _c.c_int, _vp]),
+    "rse_gal_mul": (_sz, [_u8p, _u8p, _vp, _vp, _sz]),
+    "rse_gal_mul_xor": (_sz, [_u8p, _u8p, _vp, _vp, _sz]),
+    "rse_gf16_mul_slice": (_c.c_int, [_u8p, _vp, _vp, _sz, _c.c_int, _vp]),
+    "rse_last_kernel": (_c.c_char_p, []),
     "rse_fill_splitmix": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64, _vp]),
     "rse_set_option": (_c.c_int, [_c.c_int, _c.c_int64]),
     "rse_get_option": (_c.c_int64, [_c.c_int]),

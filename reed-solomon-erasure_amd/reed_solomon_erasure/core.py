@@ -300,42 +300,149 @@ class ReedSolomon:
             pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1 if data_only else 0,
             _stream(stripes)))
 
+    # ---------------------------------------------- host memory (end to end)
+    # The reference's own form: shards are slices in HOST memory (numpy arrays
+    # or CPU tensors; pinned memory gives overlapped DMA).  Each call pipelines
+    # chunks through the GPU and returns with the results in host memory.
     def encode_host(self, shards: Sequence) -> None:
-        """encode() for shards in HOST memory (numpy arrays or CPU tensors;
-        pinned memory gives overlapped DMA).  Synchronous."""
-        ptrs, lens = [], []
-        for s in shards:
-            if isinstance(s, torch.Tensor):
-                if s.is_cuda:
-                    raise ValueError("encode_host takes host memory")
-                ptrs.append(s.data_ptr())
-                lens.append(_elems(s, self.field))
-            else:  # numpy
-                if s.dtype.itemsize != 1 or not s.flags["C_CONTIGUOUS"]:
-                    raise ValueError("host shards must be contiguous uint8 arrays")
-                ptrs.append(s.ctypes.data)
-                lens.append(s.size // (2 if self.field == 16 else 1))
-        n = len(shards)
-        pa = (ctypes.c_void_p * max(1, n))(*ptrs)
-        la = (ctypes.c_size_t * max(1, n))(*lens)
-        _raise(_lib.rse_encode_host(self._h, pa, la, n, _stream()))
+        """encode() (core.rs:597-611) of host shards."""
+        pa, la = _host_arrays(shards, self.field)
+        _raise(_lib.rse_encode_host(self._h, pa, la, len(shards), _stream()))
 
-    def encode_host_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int) -> None:
-        """encode_flat() for a HOST buffer (pinned for overlapped DMA): one
-        H2D / kernel / D2H pipeline across all stripes.  Synchronous."""
-        if stripes.is_cuda:
-            raise ValueError("encode_host_flat takes host memory")
-        if stripes.dtype != torch.uint8 or not stripes.is_contiguous():
-            raise ValueError("stripes must be a contiguous uint8 tensor")
-        need = n_stripes * self.total_shard_count() * shard_len * (self.field // 8)
-        if stripes.numel() < need:
-            raise ValueError(f"stripes holds {stripes.numel()} bytes, {need} needed")
-        _raise(_lib.rse_encode_host_flat(self._h, stripes.data_ptr(), shard_len, n_stripes,
+    def verify_host(self, shards: Sequence) -> bool:
+        """verify() (core.rs:637-651) of host shards."""
+        pa, la = _host_arrays(shards, self.field)
+        ok = ctypes.c_int(0)
+        _raise(_lib.rse_verify_host(self._h, pa, la, len(shards), ctypes.byref(ok), _stream()))
+        return bool(ok.value)
+
+    def verify_with_buffer_host(self, shards: Sequence, buffer: Sequence) -> bool:
+        """verify_with_buffer() (core.rs:654-669) of host shards into a host buffer."""
+        pa, la = _host_arrays(shards, self.field)
+        ba, bl = _host_arrays(buffer, self.field)
+        ok = ctypes.c_int(0)
+        _raise(_lib.rse_verify_with_buffer_host(self._h, pa, la, len(shards), ba, bl, len(buffer),
+                                                ctypes.byref(ok), _stream()))
+        return bool(ok.value)
+
+    def reconstruct_host(self, shards: list) -> None:
+        """reconstruct() (core.rs:680-682) of host shards: Option (None =
+        missing, filled with a new host array) or (array, present) tuples."""
+        self._reconstruct_host(shards, data_only=False)
+
+    def reconstruct_data_host(self, shards: list) -> None:
+        """reconstruct_data() (core.rs:693-695) of host shards."""
+        self._reconstruct_host(shards, data_only=True)
+
+    def _reconstruct_host(self, shards: list, data_only: bool) -> None:
+        T = self.total_shard_count()
+        if len(shards) < T:
+            raise RSError(Error.TooFewShards)
+        if len(shards) > T:
+            raise RSError(Error.TooManyShards)
+        flagged = len(shards) > 0 and all(isinstance(s, tuple) for s in shards)
+        if flagged:
+            bufs = [s[0] for s in shards]
+            present = [bool(s[1]) for s in shards]
+        else:
+            bufs = list(shards)
+            present = [s is not None for s in shards]
+            lens = [_host_elems(s, self.field) for s in bufs if s is not None]
+            # core.rs:744-772 before allocating (lib.rs:151-165)
+            for n in lens:
+                if n == 0:
+                    raise RSError(Error.EmptyShard)
+                if n != lens[0]:
+                    raise RSError(Error.IncorrectShardSize)
+            if len(lens) == T:
+                return
+            if len(lens) < self._k:
+                raise RSError(Error.TooFewShardsPresent)
+            like = next(s for s in bufs if s is not None)
+            for i, s in enumerate(bufs):
+                if s is None and (i < self._k or not data_only):
+                    bufs[i] = (np.zeros(like.shape, np.uint8) if isinstance(like, np.ndarray)
+                               else torch.zeros(like.shape, dtype=torch.uint8))
+        n = len(bufs)
+        ptrs = (ctypes.c_void_p * max(1, n))(*[_host_ptr(b) if b is not None else None for b in bufs])
+        lens = (ctypes.c_size_t * max(1, n))(
+            *[_host_elems(b, self.field) if b is not None else 0 for b in bufs])
+        pres = (ctypes.c_uint8 * max(1, n))(*[1 if p else 0 for p in present])
+        fn = _lib.rse_reconstruct_data_host if data_only else _lib.rse_reconstruct_host
+        _raise(fn(self._h, ptrs, lens, pres, n, _stream()))
+        if not flagged:
+            for i in range(n):
+                shards[i] = bufs[i]
+
+    def encode_host_flat(self, stripes, shard_len: int, n_stripes: int) -> None:
+        """encode_flat() for a HOST buffer: one H2D / kernel / D2H pipeline
+        across all stripes."""
+        _check_host_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
+        _raise(_lib.rse_encode_host_flat(self._h, _host_ptr(stripes), shard_len, n_stripes,
                                          _stream()))
+
+    def verify_host_flat(self, stripes, shard_len: int, n_stripes: int) -> np.ndarray:
+        """verify_flat() of a HOST buffer; one bool per stripe."""
+        _check_host_flat(stripes, shard_len, n_stripes, self.total_shard_count(), self.field)
+        ok = np.zeros(max(1, n_stripes), np.uint8)
+        _raise(_lib.rse_verify_host_flat(self._h, _host_ptr(stripes), shard_len, n_stripes,
+                                         ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                         _stream()))
+        return ok[:n_stripes].astype(bool)
+
+    def reconstruct_host_batch(self, stripes, shard_len: int, n_stripes: int, present,
+                               data_only: bool = False) -> None:
+        """reconstruct_batch() of a HOST buffer: every stripe its own pattern."""
+        T = self.total_shard_count()
+        flags = np.ascontiguousarray(np.asarray(
+            present.cpu() if isinstance(present, torch.Tensor) else present, dtype=bool))
+        if flags.shape != (n_stripes, T):
+            raise RSError(Error.InvalidShardFlags)
+        _check_host_flat(stripes, shard_len, n_stripes, T, self.field)
+        pres = flags.astype(np.uint8)
+        _raise(_lib.rse_reconstruct_host_batch(
+            self._h, _host_ptr(stripes), shard_len, n_stripes,
+            pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1 if data_only else 0, _stream()))
 
 
 def _first(shards):
     return shards[0] if len(shards) else None
+
+
+def _host_ptr(s) -> int:
+    """Address of a host shard: a CPU tensor or a contiguous uint8 numpy array."""
+    if isinstance(s, torch.Tensor):
+        if s.is_cuda:
+            raise ValueError("the *_host calls take host memory")
+        if s.dtype != torch.uint8 or not s.is_contiguous():
+            raise ValueError("host shards must be contiguous uint8")
+        return s.data_ptr()
+    if s.dtype.itemsize != 1 or not s.flags["C_CONTIGUOUS"]:
+        raise ValueError("host shards must be contiguous uint8 arrays")
+    return s.ctypes.data
+
+
+def _host_elems(s, field: int) -> int:
+    if isinstance(s, torch.Tensor):
+        _host_ptr(s)
+        return _elems(s, field)
+    n = s.size
+    return n if field == 8 else n // 2
+
+
+def _host_arrays(shards, field):
+    n = len(shards)
+    pa = (ctypes.c_void_p * max(1, n))(*[_host_ptr(s) for s in shards])
+    la = (ctypes.c_size_t * max(1, n))(*[_host_elems(s, field) for s in shards])
+    return pa, la
+
+
+def _check_host_flat(stripes, shard_len: int, n_stripes: int, total: int, field: int) -> None:
+    _host_ptr(stripes)
+    size = stripes.numel() if isinstance(stripes, torch.Tensor) else stripes.size
+    need = n_stripes * total * shard_len * (field // 8)
+    if size < need:
+        raise ValueError(f"stripes holds {size} bytes, {need} needed")
 
 
 class ShardByShard:
@@ -430,6 +537,29 @@ def code_shards(field: int, rows, inputs: ShardList, outputs: ShardList,
     n = _elems(inputs[0], field) if n_in else 0
     _raise(_lib.rse_code_shards(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
                                 _stream(inputs[0] if n_in else None)))
+
+
+def code_shards_host(field: int, rows, inputs: Sequence, outputs: Sequence,
+                     accumulate: bool = False) -> None:
+    """code_shards() on HOST inputs/outputs (the code_some_slices hook,
+    core.rs:481-490): pipelined through the GPU, synchronous."""
+    n_out, n_in = len(outputs), len(inputs)
+    flat = []
+    for r in range(n_out):
+        for i in range(n_in):
+            v = int(rows[r][i])
+            flat += [v >> 8, v & 0xFF] if field == 16 else [v & 0xFF]
+    rb = (ctypes.c_uint8 * max(1, len(flat)))(*flat)
+    ip = (ctypes.c_void_p * max(1, n_in))(*[_host_ptr(t) for t in inputs])
+    op = (ctypes.c_void_p * max(1, n_out))(*[_host_ptr(t) for t in outputs])
+    n = _host_elems(inputs[0], field) if n_in else 0
+    _raise(_lib.rse_code_shards_host(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
+                                     _stream()))
+
+
+def last_kernel() -> str:
+    """The last coding kernel this thread launched (rse_last_kernel)."""
+    return _lib.rse_last_kernel().decode()
 
 
 def fill_splitmix(t: torch.Tensor, seed: int, shard_id: int) -> None:

@@ -2,7 +2,9 @@
 
 Shards are uint8 tensors of shape (n, 2): element j = [coefficient of x,
 constant] (galois_16.rs:49-51)."""
-from .core import ReedSolomon as _RS, ShardByShard as _SBS
+import ctypes
+
+from .core import ReedSolomon as _RS, ShardByShard as _SBS, _dev, _elems, _lib, _raise, _stream
 
 FIELD = 16
 ORDER = 65536
@@ -18,3 +20,24 @@ class ReedSolomon(_RS):
 
 
 ShardByShard = _SBS
+
+
+def mul_slice(c, input, out) -> None:
+    """Field::mul_slice for galois_16 (the trait default, lib.rs:99-108):
+    out = c * input; c = (coefficient of x, constant) or (c1 << 8) | c0."""
+    _mul(c, input, out, 0)
+
+
+def mul_slice_add(c, input, out) -> None:
+    """Field::mul_slice_add (lib.rs:110-118): out += c * input."""
+    _mul(c, input, out, 1)
+
+
+def _mul(c, input, out, add):
+    if isinstance(c, int):
+        c = (c >> 8, c & 0xFF)
+    n = _elems(input, 16)
+    if n != _elems(out, 16):  # lib.rs:100 assert_eq!
+        raise ValueError("input and out must have the same length")
+    cb = (ctypes.c_uint8 * 2)(c[0] & 0xFF, c[1] & 0xFF)
+    _raise(_lib.rse_gf16_mul_slice(cb, _dev(input), _dev(out), n, add, _stream(input)))

@@ -1,5 +1,7 @@
 """GF(2^8) backend (galois_8.rs): type aliases of the codec over the 8-bit field."""
-from .core import ReedSolomon as _RS, ShardByShard as _SBS
+import ctypes
+
+from .core import ReedSolomon as _RS, ShardByShard as _SBS, _dev, _lib, _raise, _stream
 
 FIELD = 8
 ORDER = 256
@@ -15,3 +17,20 @@ class ReedSolomon(_RS):
 
 
 ShardByShard = _SBS
+
+
+def mul_slice(c: int, input, out) -> None:
+    """galois_8::mul_slice (galois_8.rs:291-308): out = c * input (device tensors)."""
+    _mul(c, input, out, 0)
+
+
+def mul_slice_xor(c: int, input, out) -> None:
+    """galois_8::mul_slice_xor (galois_8.rs:310-327): out ^= c * input."""
+    _mul(c, input, out, 1)
+
+
+def _mul(c, input, out, xor):
+    if input.numel() != out.numel():  # lib.rs:100 assert_eq!
+        raise ValueError("input and out must have the same length")
+    _raise(_lib.rse_gf8_mul_slice(c & 0xFF, _dev(input), _dev(out), input.numel(), xor,
+                                  _stream(input)))

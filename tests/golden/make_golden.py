@@ -163,7 +163,35 @@ def generated():
     full[f"gf16_{k}_{p}_{nbytes}"] = {"data_sha256": [sha(d) for d in data],
                                       "parity_sha256": [sha(x) for x in par]}
     out["full_size"] = full
+    out["gf8_10_4_stripe_parity"] = stripe_parity(ref)
     return out
+
+
+def bench_stripes():
+    """Global stripes whose parity bench.py checks at N ranks: every rank's
+    first and last stripe at 512 stripes per rank (N = 1..8, BASELINE config
+    4's 4096 stripes), and at 4 stripes per rank for the one-GPU rehearsals of
+    the N > 1 path (2 and 4 ranks)."""
+    ids = set()
+    for per in (512, 4):
+        for r in range(8):
+            ids |= {per * r, per * r + per - 1}
+    return sorted(ids)
+
+
+def stripe_parity(ref):
+    """Parity digests of 10+4 x 16 MiB global stripe g, whose shard i holds
+    oracle.splitmix_bytes(SEED, (g << 8) | i, 16 MiB) (bench.py shard_id)."""
+    k, p, n = 10, 4, 16 << 20
+    rr = np.ascontiguousarray(O.Codec(8, k, p).matrix()[k:])
+    res = {}
+    for g in bench_stripes():
+        data = [O.splitmix_bytes(SEED, (g << 8) | i, n) for i in range(k)]
+        par = [np.zeros(n, np.uint8) for _ in range(p)]
+        ref.ref_gf8_code_some_slices(rr.ctypes.data_as(O._u8p), p, k, O._ptrs(data),
+                                     O._ptrs(par), n)
+        res[str(g)] = [sha(x) for x in par]
+    return res
 
 
 def main():

@@ -49,6 +49,9 @@ def test_codec_new_errors():  # core.rs:445-454, tests/mod.rs:97-116
         R.galois_16.ReedSolomon(65536, 1)
     with pytest.raises(RSError):
         R.galois_16.ReedSolomon(1, 65536)
+    # tests/galois_16.rs:33: the widest GF(2^16) codecs are Ok
+    r = R.galois_16.ReedSolomon(1, 65535)
+    assert r.total_shard_count() == 65536
 
 
 def test_shard_counts_and_clone():  # tests/mod.rs:118-141

@@ -1113,25 +1113,36 @@ def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
 
 
 # ------------------------------------------------------------ bench, N > 1
-def test_bench_two_ranks_rehearsal(tmp_path):
+@pytest.mark.parametrize("ranks,extras", [(2, False), (4, True)])
+def test_bench_ranks_rehearsal(ranks, extras):
     """bench.py's multi-rank path (torch.distributed.run, barrier, max-over-
-    ranks timing, whole-job value) with 2 ranks sharing the one GPU over gloo."""
+    ranks timing, whole-job value) with `ranks` ranks sharing the one GPU over
+    gloo.  Every rank checks its own first and last stripe against the
+    reference digests and the verdicts are combined (BASELINE config 4's
+    self-check, rehearsed at 4 stripes per rank); with extras, every rank also
+    runs the host-memory leg at once."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, RSE_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--stripes", "4", "--no-cpu",
-           "--no-extras"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr", "127.0.0.1", "--master-port",
+           str(29533 + ranks), os.path.join(root, "bench.py"), "--gpus", str(ranks), "--steps",
+           "2", "--warmup", "1", "--stripes", "4", "--no-cpu"] + ([] if extras else ["--no-extras"])
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_stripes_per_step"] == 8
+    assert d["n_gpus"] == ranks and d["config"]["global_stripes_per_step"] == 4 * ranks
     assert d["config"]["parity_check_vs_reference"] is True
+    assert d["config"]["parity_check_per_rank"] == [1] * ranks
+    assert d["config"]["parity_checked_stripes_rank0"] == [0, 3]
+    assert len(d["roofline"]["kernel_ms_per_launch_per_rank"]) == ranks
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
+    if extras:
+        h = d["end_to_end_host_all_ranks"]
+        assert h["ranks"] == ranks and h["parity_matches_device_all_ranks"] is True
 
 
 WIDE_CODECS = [(8, 40, 2), (8, 6, 10), (16, 36, 3), (8, 33, 9)]

@@ -48,9 +48,10 @@ def _worker(rank, world, port, q):
     t = bench.reduce_timing(elapsed, world)
     gathered = [None] * world
     dist.all_gather_object(gathered, digests)
+    verdicts = bench.gather(1 if rank else -1, world, rank, None)  # per-rank verdicts
     if rank == 0:
         q.put((t, gathered, [list(bench.stripes_for_rank(STRIPES_PER_RANK * world, r, world))
-                             for r in range(world)]))
+                             for r in range(world)], verdicts))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,7 +64,7 @@ def test_two_rank_stripe_split_and_reduction():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    t, gathered, parts = q.get(timeout=120)
+    t, gathered, parts, verdicts = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -73,6 +74,7 @@ def test_two_rank_stripe_split_and_reduction():
     assert all(len(part) == STRIPES_PER_RANK for part in parts)
     # timing reduction is the max over ranks; throughput counts every rank's bytes
     assert t == 1.5
+    assert verdicts == [-1.0, 1.0]  # every rank's verdict, in rank order, on rank 0
     stripe_bytes = (K + P) * L
     v = bench.job_throughput(3, STRIPES_PER_RANK, world, stripe_bytes, t)
     assert v == pytest.approx(3 * STRIPES_PER_RANK * world * stripe_bytes / 1.5 / (1 << 20))
@@ -88,3 +90,28 @@ def test_uneven_partition():
     parts = [bench.stripes_for_rank(10, r, 4) for r in range(4)]
     assert [len(p) for p in parts] == [3, 3, 2, 2]
     assert sorted(g for p in parts for g in p) == list(range(10))
+
+
+def test_golden_covers_every_rank_first_and_last_stripe():
+    """BASELINE config 4 (4096 stripes over 8 GPUs, 512 each) and the 2/4-rank
+    rehearsals (4 stripes each): every rank's first and last stripe has a
+    reference digest, so no rank's output goes unchecked."""
+    gold = bench.golden_stripes()
+    for per, ranks in ((512, 8), (512, 4), (512, 2), (512, 1), (4, 4), (4, 2)):
+        for r in range(ranks):
+            part = bench.stripes_for_rank(per * ranks, r, ranks)
+            assert str(part.start) in gold and str(part.stop - 1) in gold
+
+
+def test_check_stripes_detects_a_flipped_byte():
+    import torch
+    k, p, n = 10, 4, 16 << 20
+    v = torch.zeros((1, k + p, n), dtype=torch.uint8)
+    shards = [O.splitmix_bytes(bench.SEED, bench.shard_id(0, i), n) for i in range(k)]
+    shards += [np.zeros(n, np.uint8) for _ in range(p)]
+    O.Codec(8, k, p).encode(shards)
+    v[0] = torch.from_numpy(np.stack(shards))
+    assert bench.check_stripes(v, range(0, 1), 1, k, p) == (1, [0])
+    v[0, k + 2, 12345] ^= 1
+    assert bench.check_stripes(v, range(0, 1), 1, k, p) == (0, [0])
+    assert bench.check_stripes(v, range(5, 6), 1, k, p) == (-1, [])  # no digest: unchecked

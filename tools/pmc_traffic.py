@@ -7,13 +7,16 @@ encode kernel with the bench's grid, and applies the gfx950 correction of
 MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide
 coalesced stream, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 Writes profiles/<tag>_pmc_traffic.json, which bench.py reports as
-roofline.traffic.
+roofline.traffic when the kernel that ran (rse_last_kernel, "kernel_id") is the
+one profiled here.  RSE_COMMIT (set by the caller: the GPU box has no .git)
+and the library's SHA-256 record what was measured.
 
     python tools/pmc_traffic.py --tag r01 [bench args...]
 """
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import subprocess
@@ -50,9 +53,13 @@ def main():
     fetch_b = 2 * sum(f) / len(f) * 1024
     write_b = sum(w) / len(w) * 1024
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    lib_path = os.path.join(ROOT, "reed-solomon-erasure_amd", "reed_solomon_erasure", "librse_hip.so")
     res = {
         "workload": bench["config"]["workload"],
         "kernel_family": bench["roofline"].get("kernel", "table"),
+        "kernel_id": bench["roofline"].get("kernel_id"),
+        "commit": os.environ.get("RSE_COMMIT"),
+        "library_sha256": hashlib.sha256(open(lib_path, "rb").read()).hexdigest(),
         "kernel": [r["Kernel_Name"] for r in fetch][0],
         "dispatches": len(f),
         "fetch_size_kb_raw_mean": sum(f) / len(f),
