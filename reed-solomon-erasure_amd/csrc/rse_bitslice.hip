@@ -185,6 +185,7 @@ struct Code {
   static constexpr int k = K, p = P;
   static constexpr int NP = F::kPlanes, NG = 16 / F::kPlanes;
   static constexpr int kTemps = Planes<F, K, P, CSE>::kTemps;
+  static constexpr int kGTemps = 0;  // GF(2^8) group temporaries: run-time specialised wide codecs
   static constexpr Planes<F, K, P, CSE> planes{};
 };
 

@@ -173,9 +173,38 @@ __device__ __forceinline__ void load4(u32x4 (&v)[4], const uint8_t* p) {
 // every output o, group g and plane p.
 // ACC: the accumulators already hold a partial sum (accumulate mode), so
 // input 0 adds to them like every other input.
+// GF(2^8) with shared subexpressions (C::kGTemps > 0): both 8-plane groups
+// use the same bit matrices, so the temporaries are defined once per input
+// (planes.tmp[I][t] = sources {a, b}, a source j < 8 a plane of the group,
+// 8 + t a temporary) and computed per group; the outputs' rows of group G are
+// coded from that group's sources.
+template <class C, int I, bool ACC, int G, int N, int... OP>
+__device__ __forceinline__ void mac_group(uint32_t (&acc)[N], const uint32_t (&pl)[16],
+                                          int_seq<int, OP...>) {
+  uint32_t src[8 + C::kGTemps];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) src[q] = pl[G * 8 + q];
+#pragma unroll
+  for (int t = 0; t < C::kGTemps; ++t)
+    if (t < C::planes.ntmp[I]) src[8 + t] = src[C::planes.tmp[I][t][0]] ^ src[C::planes.tmp[I][t][1]];
+  // OP runs over outputs; plane q of group G of output o is acc[o * 16 + G * 8 + q]
+  if constexpr (I == 0 && !ACC)
+    ((acc[(OP / 8) * 16 + G * 8 + OP % 8] = xinit<C::planes.sel[OP / 8][I][OP % 8]>(src)), ...);
+  else
+    ((acc[(OP / 8) * 16 + G * 8 + OP % 8] =
+          xacc<C::planes.sel[OP / 8][I][OP % 8]>(acc[(OP / 8) * 16 + G * 8 + OP % 8], src)),
+     ...);
+}
+
 template <class C, int I, bool ACC, int N, int... OP>
 __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&pl)[16],
                                           int_seq<int, OP...>) {
+  if constexpr (C::kGTemps > 0) {
+    static_assert(C::NP == 8, "group temporaries are for GF(2^8)");
+    mac_group<C, I, ACC, 0>(acc, pl, make_int_seq<N / 2>{});
+    mac_group<C, I, ACC, 1>(acc, pl, make_int_seq<N / 2>{});
+    return;
+  }
   uint32_t in[16 + C::kTemps];
 #pragma unroll
   for (int q = 0; q < 16; ++q) in[q] = pl[q];
@@ -196,8 +225,11 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
 
 // Output phase of one chunk: un-slice every output's planes and store them
 // (kStore), compare them with the stored parity (kCheck), or both.
-template <class C, bool NT, bool WT = false, uint32_t S = kBsBlock * 16>
-__device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const CodeArgs& a,
+// A: the argument block (CodeArgs, or a wide codec's WideArgs: O0 is then the
+// first output of the wave's share).
+template <class C, bool NT, bool WT = false, uint32_t S = kBsBlock * 16, int O0 = 0,
+          class A = CodeArgs>
+__device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const A& a,
                                               uint64_t off, uint32_t mode, bool& diff) {
 #pragma unroll
   for (int o = 0; o < C::p; ++o) {
@@ -209,9 +241,9 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t o16 = off + j * S;
-      if (mode != kCheck) stv_policy<NT, WT>(a.out[o] + o16, v[j]);
+      if (mode != kCheck) stv_policy<NT, WT>(a.out[O0 + o] + o16, v[j]);
       if (mode != kStore) {
-        const u32x4 w = ldv<NT>(a.cmp[o] + o16);
+        const u32x4 w = ldv<NT>(a.cmp[O0 + o] + o16);
         diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
       }
     }
@@ -226,9 +258,9 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 //  XC: the last input prefetches input 0 of the workgroup's next chunk
 //      (next_off, ~0 if none) into cur, so the output phase overlaps it too.
 template <class C, bool NT, bool SB, bool XC, int I, uint32_t S = kBsBlock * 16,
-          bool ACC = false>
+          bool ACC = false, class A = CodeArgs>
 __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
-                                            const CodeArgs& a, uint64_t off, uint64_t next_off) {
+                                            const A& a, uint64_t off, uint64_t next_off) {
   u32x4 nxt[4];
   if constexpr (I + 1 < C::k) {
     load4<NT, S>(nxt, a.in[I + 1] + off);
@@ -246,7 +278,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
   if constexpr (I + 1 < C::k) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    code_inputs<C, NT, SB, XC, I + 1, S, ACC>(acc, cur, a, off, next_off);
+    code_inputs<C, NT, SB, XC, I + 1, S, ACC, A>(acc, cur, a, off, next_off);
   } else if constexpr (XC) {
     if (next_off != ~0ull) {
 #pragma unroll
@@ -361,6 +393,38 @@ __device__ __forceinline__ void bitslice_body_deep(const CodeArgs& a, uint64_t c
     }
   }
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+}
+
+// ------------------------------------------------------------ wide codecs
+// Codecs with more than 8 parity rows (or 32 data shards): one workgroup of W
+// waves per 4 KiB chunk of every shard, and wave w codes its own share of the
+// outputs (C: those rows over ALL k inputs, O0 the first of them) from the
+// same inputs.  Every wave loads every input chunk itself (plain loads: the
+// workgroup's waves run side by side on one CU, so the lines are fetched from
+// HBM once and served to the other waves by L1/L2); every output is written
+// once.  Lane layout of the 4 KiB chunks: lane l loads vectors l, l+64,
+// l+128, l+192 (each load instruction 1 KiB contiguous per wave).
+template <class C, int O0, class A>
+__device__ __forceinline__ void wide_body(const A& a) {
+  const WideHdr& h = a.h;
+  const uint64_t total = h.chunks_per_stripe * h.n_stripes;
+  const uint32_t lane_off = (threadIdx.x & 63u) * 16u;
+  const uint32_t mode = h.mode;
+  bool diff = false;
+  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const uint64_t stripe = c / h.chunks_per_stripe, chunk = c - stripe * h.chunks_per_stripe;
+    const uint64_t off = stripe * h.stripe_stride + chunk * 4096u + lane_off;
+    uint32_t acc[C::p * 16];
+    u32x4 cur[4];
+    load4<false, 1024u>(cur, a.in[0] + off);
+    code_inputs<C, false, true, false, 0, 1024u, false, A>(acc, cur, a, off, ~0ull);
+    store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
+    if (h.per_stripe && diff) {
+      atomicOr(h.mismatch + stripe, 1u);
+      diff = false;
+    }
+  }
+  if (mode != kStore && diff) atomicOr(h.mismatch, 1u);
 }
 
 // ------------------------------------------------------------ reconstruct

@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/rse_hip.h"
@@ -197,6 +198,44 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
 int run_job(const Job& j, hipStream_t s) {
   const size_t n_out = j.rows->n_out, n_in = j.rows->n_in;
   if (n_out == 0 || j.len_bytes == 0) return RSE_OK;
+  // a wide codec's (or pattern's) rows with their one-module kernel built:
+  // every whole 4 KiB chunk in one launch (each input read once, each output
+  // written once), the rest of every shard below
+  if ((n_in > (size_t)kMaxIn || n_out > rse::kJitMaxOut) && !j.accumulate &&
+      j.len_bytes >= 4096 && j.stripe_stride % 16u == 0 && rse::get_option(RSE_OPT_BITSLICE) &&
+      rse::wide_eligible((uint32_t)n_in, (uint32_t)n_out) && j.n_stripes <= 0xffffffffu) {
+    bool al = true;
+    for (size_t i = 0; i < n_in; ++i) al = al && aligned16(j.in[i]);
+    for (size_t r = 0; r < n_out; ++r) {
+      if (j.mode != rse::kCheck) al = al && aligned16(j.out[r]);
+      if (j.mode != rse::kStore) al = al && aligned16(j.cmp[r]);
+    }
+    uint64_t done = 0;
+    if (al)
+      RSE_HIP(rse::launch_wide(j.field, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data(), j.in,
+                               j.out, j.cmp, j.len_bytes, j.stripe_stride, (uint32_t)j.n_stripes,
+                               j.mode, j.mismatch, j.per_stripe, s, &done));
+    if (done) {
+      if (done == j.len_bytes) return RSE_OK;
+      std::vector<const uint8_t*> in(j.in, j.in + n_in);
+      std::vector<uint8_t*> out(n_out, nullptr);
+      std::vector<const uint8_t*> cmp(n_out, nullptr);
+      for (auto& q : in) q += done;
+      for (size_t r = 0; r < n_out; ++r) {
+        if (j.out && j.out[r]) out[r] = j.out[r] + done;
+        if (j.cmp && j.cmp[r]) cmp[r] = j.cmp[r] + done;
+      }
+      Job rest = j;
+      rest.in = in.data();
+      rest.out = j.out ? out.data() : nullptr;
+      rest.cmp = j.cmp ? cmp.data() : nullptr;
+      rest.len_bytes = j.len_bytes - done;
+      const std::string wide_kernel = rse::last_kernel();  // the launch to report
+      const int rc = run_job(rest, s);
+      rse::note_kernel("%s", wide_kernel.c_str());
+      return rc;
+    }
+  }
   const bool single_in = n_in <= (size_t)kMaxIn;
   if (j.mode == rse::kStore || single_in) {
     // a wide codec's parity rows whose bit-sliced blocks are built (see
@@ -354,7 +393,9 @@ void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_
   c->jit_requested.store(true, std::memory_order_relaxed);
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
-  if (wide)
+  if (wide && rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p))
+    rse::jit_register_wide(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
+  else if (wide)
     rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else
     rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
@@ -646,6 +687,10 @@ bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes)
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
   if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
     if (mode < 2 && len_bytes < (1u << 20)) return false;
+    if (rse::wide_eligible(k, n)) {  // run_job launches it
+      if (!rse::jit_register_wide(c->field, k, n, plan.rows.c.data(), true)) return false;
+      return rse::jit_wide_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+    }
     if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data(), true)) return false;
     return rse::jit_blocks_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
   }
@@ -1072,8 +1117,11 @@ int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const Rows rows = parity_rows(c);
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
-  switch (wide ? rse::jit_blocks_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
-                                        wait != 0)
+  const bool one = rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
+  switch (wide ? (one ? rse::jit_wide_status(c->field, (uint32_t)c->k, (uint32_t)c->p,
+                                             rows.c.data(), wait != 0)
+                      : rse::jit_blocks_status(c->field, (uint32_t)c->k, (uint32_t)c->p,
+                                               rows.c.data(), wait != 0))
                : rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
                                  wait != 0)) {
     case 2: return RSE_KERNELS_SPECIALISED;

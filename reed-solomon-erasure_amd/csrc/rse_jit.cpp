@@ -21,6 +21,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstring>
 #include <deque>
 #include <cstdio>
 #include <cstdlib>
@@ -81,7 +82,7 @@ std::condition_variable g_cv;
 constexpr int kBlkQueue = 2;
 std::deque<Entry*> g_jobs[3];
 int queue_of(const Entry& e, int stage) {
-  return (e.kind == kJitBlock || e.kind == kJitBlockAcc) ? kBlkQueue : stage;
+  return (e.kind == kJitBlock || e.kind == kJitBlockAcc || e.kind == kJitWide) ? kBlkQueue : stage;
 }
 std::atomic<int64_t> g_built{0};
 int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
@@ -109,12 +110,13 @@ bool same_rows(const Entry& e, const uint16_t* rows, size_t stride) {
 }
 
 // Caller holds g_mu.  want >= 0: only entries of that kind match; -2: any
-// but kJitBlockAcc (the kernels for store and check modes).
+// with encode/verify kernels over CodeArgs (not kJitBlockAcc, not kJitWide).
 Entry* find_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride,
                    int want = -1) {
   for (auto& e : registry())
     if (e->field == field && e->k == k && e->p == p &&
-        (want == -1 || (want == -2 ? e->kind != kJitBlockAcc : e->kind == want)) &&
+        (want == -1 || (want == -2 ? (e->kind != kJitBlockAcc && e->kind != kJitWide)
+                                   : e->kind == want)) &&
         same_rows(*e, rows, stride))
       return e.get();
   return nullptr;
@@ -136,19 +138,20 @@ int recon_ns(uint32_t p, int* ns) {
 }
 
 // Greedy common-subexpression elimination over one input's XOR network.
-// rows: the source mask of every output plane (bit j: source j, planes 0..15).
-// Repeatedly the pair of sources that occurs together in the most rows (at
-// least 3: a temporary costs one v_bitop3 and saves about half of one per row
-// that uses it, the rows absorbing two sources per op) becomes a new source
-// 16 + t, up to `budget` temporaries.
+// rows: the source mask of every output plane (bit j: source j; the first
+// `planes` sources are the input's planes).  Repeatedly the pair of sources
+// that occurs together in the most rows (at least 3: a temporary costs one
+// v_bitop3 and saves about half of one per row that uses it, the rows
+// absorbing two sources per op) becomes a new source planes + t, up to
+// `budget` temporaries.
 struct Cse {
   int n = 0;
   uint8_t tmp[16][2] = {};
 };
-Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget) {
+Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget, int planes) {
   Cse c;
   while (c.n < budget && c.n < 16) {
-    const int ns = 16 + c.n;
+    const int ns = planes + c.n;
     int best = 0, ba = -1, bb = -1;
     for (int a = 0; a < ns; ++a)
       for (int b = a + 1; b < ns; ++b) {
@@ -172,27 +175,22 @@ Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget) {
   return c;
 }
 
-// The device source of one codec: the shared kernel code, the codec's
-// plane-selection table, and extern "C" entry points.
-std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage, JitKind kind) {
+// Appends the plane-selection table and code struct `name` of p x k rows:
+// sel[o][i][q] has bit j set iff input source j feeds output plane q -- column
+// j of the bit matrix of rows[o][i] is rows[o][i] * (the element with only
+// plane j's bit set).  GF(2^16): one 16-plane group per input, `budget`
+// shared temporaries per input (kTemps).  GF(2^8): two 8-plane groups that
+// share their bit matrices, `gbudget` temporaries per input computed per
+// group (kGTemps; wide codecs, where an input feeds many outputs).
+void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t p,
+               const std::vector<uint16_t>& rows, int budget, int gbudget) {
   const int np = field == 16 ? 16 : 8;
   auto bit = [&](int q) { return field == 16 ? (q ^ 8) : q; };
   auto mul = [&](uint16_t a, uint16_t b) {
     return field == 16 ? Gf16Field::mul(a, b) : Gf8Field::mul(a, b);
   };
-  std::string s;
-  s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * np);
-  // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
-  // types in __hip_internal
-  s += "#define RSE_JIT 1\n"
-       "using __hip_internal::uint8_t;\nusing __hip_internal::uint16_t;\n"
-       "using __hip_internal::uint32_t;\nusing __hip_internal::uint64_t;\n"
-       "using __hip_internal::int32_t;\n";
-  s += kJitSource;
-  // sel[o][i][q]: bit j set iff input plane j feeds output plane q -- column j
-  // of the bit matrix of rows[o][i] is rows[o][i] * (the element with only
-  // plane j's bit set)
+  if (field == 16) gbudget = 0;
+  else budget = 0;
   std::vector<uint32_t> sel((size_t)p * k * np, 0);
   auto at = [&](uint32_t o, uint32_t i, int q) -> uint32_t& { return sel[((size_t)o * k + i) * np + q]; };
   for (uint32_t o = 0; o < p; ++o)
@@ -202,30 +200,28 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
         for (int q = 0; q < np; ++q)
           if ((col >> bit(q)) & 1u) at(o, i, q) |= 1u << j;
       }
-  // GF(2^16): one 16-plane group per input, so an input's p x 16 rows share
-  // their sources -- common pairs become temporaries (RSE_OPT_JIT_CSE)
-  const int budget = field == 16 ? (int)get_option(13) : 0;
+  const int nt = budget > 0 ? budget : gbudget;
   std::vector<Cse> cse(k);
-  if (budget > 0)
+  if (nt > 0)
     for (uint32_t i = 0; i < k; ++i) {
       std::vector<uint32_t> r;
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) r.push_back(at(o, i, q));
-      cse[i] = eliminate_common_pairs(r, budget);
+      cse[i] = eliminate_common_pairs(r, nt, np);
       size_t n = 0;
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) at(o, i, q) = r[n++];
     }
-  char buf[512];
+  char buf[640];
   std::snprintf(buf, sizeof buf,
                 "\nnamespace rse {\nnamespace {\n"
-                "struct JitPlanes {\n  uint32_t sel[%u][%u][%d];\n  uint8_t ntmp[%u];\n"
+                "struct %sPlanes {\n  uint32_t sel[%u][%u][%d];\n  uint8_t ntmp[%u];\n"
                 "  uint8_t tmp[%u][%d][2];\n};\n"
-                "struct JitCode {\n  using Field = %s;\n"
-                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d;\n"
-                "  static constexpr JitPlanes planes = {{",
-                p, k, np, k, k, budget > 0 ? budget : 1, field == 16 ? "BitsF16" : "BitsF8", k, p,
-                np, 16 / np, budget > 0 ? budget : 0);
+                "struct %s {\n  using Field = %s;\n"
+                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d, kGTemps = %d;\n"
+                "  static constexpr %sPlanes planes = {{",
+                name, p, k, np, k, k, nt > 0 ? nt : 1, name, field == 16 ? "BitsF16" : "BitsF8",
+                k, p, np, 16 / np, budget > 0 ? budget : 0, gbudget > 0 ? gbudget : 0, name);
   s += buf;
   for (uint32_t o = 0; o < p; ++o) {
     s += "{";
@@ -247,13 +243,72 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   s += "}, {";
   for (uint32_t i = 0; i < k; ++i) {
     s += "{";
-    for (int t = 0; t < (budget > 0 ? budget : 1); ++t) {
+    for (int t = 0; t < (nt > 0 ? nt : 1); ++t) {
       std::snprintf(buf, sizeof buf, "{%d,%d},", cse[i].tmp[t][0], cse[i].tmp[t][1]);
       s += buf;
     }
     s += "},";
   }
   s += "}};\n};\n}  // namespace\n}  // namespace rse\n";
+}
+
+// A wide codec's outputs split over the waves of one workgroup: W = ceil(p/8)
+// waves, shares as equal as possible (the waves run side by side).
+int wide_waves(uint32_t p) { return (int)((p + kJitMaxOut - 1) / kJitMaxOut); }
+void wide_share(uint32_t p, int w, uint32_t* o0, uint32_t* n) {
+  const uint32_t W = (uint32_t)wide_waves(p), base = p / W, extra = p % W;
+  *o0 = w * base + std::min<uint32_t>(w, extra);
+  *n = base + (w < (int)extra ? 1u : 0u);
+}
+
+// The device source of one codec: the shared kernel code, the codec's
+// plane-selection table, and extern "C" entry points.
+std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
+                        int stage, JitKind kind) {
+  std::string s;
+  s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * (field == 16 ? 16 : 8));
+  // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
+  // types in __hip_internal
+  s += "#define RSE_JIT 1\n"
+       "using __hip_internal::uint8_t;\nusing __hip_internal::uint16_t;\n"
+       "using __hip_internal::uint32_t;\nusing __hip_internal::uint64_t;\n"
+       "using __hip_internal::int32_t;\n";
+  s += kJitSource;
+  if (kind == kJitWide) {
+    // one code struct per wave's share of the outputs, and the kernel
+    const int W = wide_waves(p);
+    const int gbudget = 16;
+    for (int w = 0; w < W; ++w) {
+      uint32_t o0, n;
+      wide_share(p, w, &o0, &n);
+      std::vector<uint16_t> sub(rows.begin() + (size_t)o0 * k, rows.begin() + (size_t)(o0 + n) * k);
+      char name[32];
+      std::snprintf(name, sizeof name, "JitWide%d", w);
+      emit_code(s, name, field, k, n, sub, (int)get_option(13), gbudget);
+    }
+    char buf[512];
+    std::snprintf(buf, sizeof buf,
+                  "struct WideArgs {\n  rse::WideHdr h;\n  const uint8_t* in[%u];\n"
+                  "  uint8_t* out[%u];\n  const uint8_t* cmp[%u];\n};\n"
+                  // at least 2 waves per SIMD (256 VGPRs): __launch_bounds__ of a
+                  // 64-thread group would give 64 VGPRs and spill
+                  "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
+                  "    amdgpu_waves_per_eu(2))) void rse_jit_wide(const WideArgs a) {\n"
+                  "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
+                  k, p, p, 64 * W, 64 * W);
+    s += buf;
+    for (int w = 0; w < W; ++w) {
+      uint32_t o0, n;
+      wide_share(p, w, &o0, &n);
+      std::snprintf(buf, sizeof buf,
+                    "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
+      s += buf;
+    }
+    s += "    default: break;\n  }\n}\n";
+    return s;
+  }
+  emit_code(s, "JitCode", field, k, p, rows, field == 16 ? (int)get_option(13) : 0, 0);
+  char buf[512];
   if (stage == kEnc) {
     // encode/verify kernels (16 KiB and 4 KiB chunks); a later block of a wide
     // codec: the same adding to the outputs' bytes instead
@@ -315,7 +370,10 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
   if (const char* dir = std::getenv("RSE_JIT_DUMP")) {  // debugging aid
     char path[1024];
     std::snprintf(path, sizeof path, "%s/rse_jit_gf%d_%u_%u_%s_%p.hip", dir, e.field, e.k, e.p,
-                  stage == kEnc ? (e.kind == kJitBlockAcc ? "block_acc" : "encode") : "reconstruct",
+                  stage == kEnc ? (e.kind == kJitBlockAcc ? "block_acc"
+                                   : e.kind == kJitWide   ? "wide"
+                                                          : "encode")
+                                : "reconstruct",
                   (const void*)&e);
     if (FILE* f = std::fopen(path, "w")) {
       std::fputs(src.c_str(), f);
@@ -399,11 +457,16 @@ void add_locked(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t 
     g_jobs[queue_of(*e, st)].push_back(e.get());
   }
   if (kind == kJitPattern) ++g_patterns;
+  // a wide module costs about as much hiprtc as its blocks would: it counts
+  // as that many against the same budgets
+  const int cost = kind == kJitWide ? (int)(((k + kMaxIn - 1) / kMaxIn) *
+                                            ((p + kJitMaxOut - 1) / kJitMaxOut))
+                                    : 1;
   if (pattern_block) {
-    ++g_pattern_blocks;
+    g_pattern_blocks += cost;
     ++g_pending_pattern_blocks;
-  } else if (kind == kJitBlock || kind == kJitBlockAcc) {
-    ++g_blocks;
+  } else if (kind == kJitBlock || kind == kJitBlockAcc || kind == kJitWide) {
+    g_blocks += cost;
   }
   registry().push_back(std::move(e));
 }
@@ -485,6 +548,96 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   w.start();
   g_cv.notify_all();
   return 1;
+}
+
+bool wide_eligible(uint32_t k, uint32_t p) {
+  return k >= 1 && p >= 1 && (k > (uint32_t)kMaxIn || p > kJitMaxOut) &&
+         p <= kJitMaxOut * 8u && k + 2u * p <= kWideMaxPtrs;
+}
+
+int jit_register_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern) {
+  if (get_option(9) == 0 || (field != 8 && field != 16) || !wide_eligible(k, p)) return 0;
+  registry();
+  Worker& w = worker();
+  std::lock_guard<std::mutex> g(g_mu);
+  if (find_locked(field, k, p, rows, k, kJitWide)) return 1;
+  const int cost = (int)(((k + kMaxIn - 1) / kMaxIn) * ((p + kJitMaxOut - 1) / kJitMaxOut));
+  if (pattern ? (g_pattern_blocks + cost > kMaxPatternBlocks ||
+                 g_pending_pattern_blocks + 1 > kMaxPendingPatternBlocks)
+              : g_blocks + cost > kMaxBlocks)
+    return 0;
+  add_locked(field, k, p, rows, k, kJitWide, pattern);
+  w.start();
+  g_cv.notify_all();
+  return 1;
+}
+
+int jit_wide_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
+  return status_of(find_entry(field, k, p, rows, k, kJitWide), wait);
+}
+
+hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
+                       const uint8_t* const* in, uint8_t* const* out, const uint8_t* const* cmp,
+                       uint64_t len, uint64_t stripe_stride, uint32_t n_stripes, uint32_t mode,
+                       uint32_t* mismatch, bool per_stripe, hipStream_t stream, uint64_t* done) {
+  *done = 0;
+  const uint64_t cps = len / 4096u;
+  if (cps == 0 || n_stripes == 0) return hipSuccess;
+  Entry* e = find_entry(field, k, p, rows, k, kJitWide);
+  if (!e || status_of(e, get_option(9) >= 2) != 2) return hipSuccess;
+  const std::shared_ptr<const Compiled> c = e->built[kEnc].get();
+  int dev = 0;
+  hipError_t he = hipGetDevice(&dev);
+  if (he != hipSuccess) return he;
+  hipFunction_t fn = nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    for (auto& d : e->loaded)
+      if (d.dev == dev) fn = d.fns.wide;
+    if (!fn) {
+      hipModule_t m = nullptr;
+      he = hipModuleLoadData(&m, c->code.data());
+      if (he == hipSuccess) he = hipModuleGetFunction(&fn, m, "rse_jit_wide");
+      if (he != hipSuccess) {
+        if (m) (void)hipModuleUnload(m);
+        return he;
+      }
+      Entry::Loaded l{dev};
+      l.fns.wide = fn;
+      e->loaded.push_back(l);
+    }
+  }
+  // argument block: header, then the k input, p output and p compare pointers
+  std::vector<uint8_t> buf(sizeof(WideHdr) + sizeof(void*) * (k + 2 * (size_t)p), 0);
+  WideHdr h{};
+  h.stripe_stride = stripe_stride;
+  h.chunks_per_stripe = cps;
+  h.mismatch = mismatch;
+  h.n_stripes = n_stripes;
+  h.mode = mode;
+  h.per_stripe = per_stripe ? 1u : 0u;
+  std::memcpy(buf.data(), &h, sizeof h);
+  const uint8_t** ptrs = reinterpret_cast<const uint8_t**>(buf.data() + sizeof h);
+  for (uint32_t i = 0; i < k; ++i) ptrs[i] = in[i];
+  for (uint32_t o = 0; o < p; ++o) {
+    ptrs[k + o] = out ? out[o] : nullptr;
+    ptrs[k + p + o] = cmp ? cmp[o] : nullptr;
+  }
+  size_t size = buf.size();
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                   HIP_LAUNCH_PARAM_END};
+  const uint64_t total = cps * n_stripes;
+  const int64_t grid = get_option(2);
+  uint64_t gx = grid > 0 ? (uint64_t)grid : 4096u;
+  if (gx > total) gx = total;
+  if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+  note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, wide_waves(p));
+  he = hipModuleLaunchKernel(fn, (uint32_t)gx, 1, 1, 64u * (uint32_t)wide_waves(p), 1, 1, 0,
+                             stream, nullptr, extra);
+  if (he != hipSuccess) return he;
+  count_bitslice_launch();
+  *done = cps * 4096u;
+  return hipSuccess;
 }
 
 int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {

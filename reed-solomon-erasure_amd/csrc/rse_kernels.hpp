@@ -74,6 +74,19 @@ struct BsReconArgs {
   uint16_t w[kMaxOut][kMaxOut];   // [o][r], zero unless r is in R
 };
 
+// Header of a wide codec's argument block (rse_jit.cpp kJitWide).  The block
+// is the header followed by the k input, p output and p compare pointers
+// (WideArgs<k, p> in the module's source; the host packs the same bytes).
+struct WideHdr {
+  uint64_t stripe_stride;      // bytes between stripe s and s+1 for every pointer
+  uint64_t chunks_per_stripe;  // whole 4 KiB chunks per shard coded by the launch
+  uint32_t* mismatch;          // CHECK modes
+  uint32_t n_stripes;
+  uint32_t mode;               // CodeMode
+  uint32_t per_stripe;         // CHECK modes: mismatch[stripe] instead of mismatch[0]
+  uint32_t pad;
+};
+
 #ifndef RSE_JIT
 // Launch the fused coding kernel over args.n_stripes stripes on `stream`.
 // field is 8 or 16.  Returns a hipError_t.
@@ -142,7 +155,25 @@ constexpr uint32_t kJitMaxOut = 8;  // p' <= 8: 16 x p' accumulator VGPRs
 //              (jit_register_blocks);
 //  kJitBlockAcc a block over later inputs: accumulate-mode encode kernels
 //              only (each kernel is seconds of hiprtc for 32 x 8 blocks).
-enum JitKind { kJitCodec = 0, kJitPattern = 1, kJitBlock = 2, kJitBlockAcc = 3 };
+//  kJitWide    a wide codec's (or wide decode pattern's) whole rows in ONE
+//              module: each wave of a workgroup codes its share of <= 8
+//              outputs over all k inputs of the same 4 KiB chunk, so every
+//              input is read from HBM once and every output written once
+//              (rse_bitslice_core.hpp wide_body).
+enum JitKind { kJitCodec = 0, kJitPattern = 1, kJitBlock = 2, kJitBlockAcc = 3, kJitWide = 4 };
+// Wide modules: p <= 64 (8 waves of 8 outputs), and k + 2p pointers in the
+// kernel-argument block.
+constexpr uint32_t kWideMaxPtrs = 480;
+bool wide_eligible(uint32_t k, uint32_t p);
+int jit_register_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern);
+int jit_wide_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
+// Codes the whole 4 KiB chunks of every shard (of n_stripes stripes) with the
+// wide module of these rows if it is built (RSE_OPT_JIT 2: waits for it);
+// *done = bytes per shard coded, 0 if it did not launch.
+hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
+                       const uint8_t* const* in, uint8_t* const* out, const uint8_t* const* cmp,
+                       uint64_t len, uint64_t stripe_stride, uint32_t n_stripes, uint32_t mode,
+                       uint32_t* mismatch, bool per_stripe, hipStream_t stream, uint64_t* done);
 // Registers p x k rows (row-major) and queues their build on the background
 // thread.  Returns 1 if registered (now or before), 0 if not eligible or
 // refused.
@@ -166,6 +197,7 @@ struct JitFns {
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
   hipFunction_t rec_desc[5] = {};  // ... over per-stripe BsReconArgs (descs, cps, n_stripes)
+  hipFunction_t wide = nullptr;    // kJitWide: rse_jit_wide (WideArgs)
 };
 // Kernels of `stage` (0: encode/verify, 1: reconstruct) for a launch whose
 // coefficients rows[o * stride + i] equal a registered codec's parity rows,

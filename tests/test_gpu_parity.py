@@ -1145,18 +1145,22 @@ def test_bench_ranks_rehearsal(ranks, extras):
         assert h["ranks"] == ranks and h["parity_matches_device_all_ranks"] is True
 
 
-WIDE_CODECS = [(8, 40, 2), (8, 6, 10), (16, 36, 3), (8, 33, 9)]
+# (field, k, p, modules): one wide module (p <= 64, k + 2p <= 480), or
+# blocks of 8 outputs x 32 inputs beyond that
+WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
+               (8, 4, 66, 9)]
 
 
-@pytest.mark.parametrize("field,k,p", WIDE_CODECS)
-def test_wide_codec_blocks(R, field, k, p):
-    """Wide codecs (k > 32 or p > 8) get bit-sliced kernels per 8 x 32 block of
-    their parity rows (rse_jit.cpp kJitBlock / kJitBlockAcc): run_job launches
-    the blocks output block by output block, later input blocks accumulating
-    into the outputs.  Every block launch is bit-sliced (the launch counter
-    counts one per block), and encode, verify (through the materialised sums
-    of > 32 inputs) and flat multi-stripe encode match the oracle over 16 KiB
-    chunks, a 4 KiB chunk and a table-coded tail."""
+@pytest.mark.parametrize("field,k,p,modules", WIDE_CODECS)
+def test_wide_codec_kernels(R, field, k, p, modules):
+    """Wide codecs (k > 32 or p > 8) on their run-time specialised kernels:
+    one module whose workgroup's waves each code <= 8 outputs over all k
+    inputs of the same 4 KiB chunk (every input read once, every output
+    written once: ONE launch), or -- past 64 outputs -- blocks of 8 outputs x
+    32 inputs launched output block by output block, later input blocks
+    accumulating.  Encode, verify (compare fused into the wide kernel) and flat
+    multi-stripe encode match the oracle over whole 4 KiB chunks and a
+    table-coded tail."""
     lib = R._lib.load()
     es = field // 8
     nbytes = 2 * 16384 + 4096 + 48 * es
@@ -1166,7 +1170,7 @@ def test_wide_codec_blocks(R, field, k, p):
     oc = O.Codec(field, k, p)
     full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
     oc.encode(full)
-    blocks = -(-k // 32) * -(-p // 8)
+    blocks = modules
     old = lib.rse_get_option(9)
     try:
         assert lib.rse_set_option(9, 2) == 0
@@ -1178,6 +1182,9 @@ def test_wide_codec_blocks(R, field, k, p):
         r.encode(t)
         torch.cuda.synchronize()
         assert lib.rse_get_option(6) - n0 == blocks
+        from reed_solomon_erasure.core import last_kernel
+        if modules == 1:
+            assert last_kernel().startswith(f"bitslice-wide gf{field} {k}+{p}"), last_kernel()
         for i in range(p):
             assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
         assert r.verify(t)

@@ -62,8 +62,19 @@ def main():
         fill_splitmix(buf, 1, 0)
     r = R.core.ReedSolomon(k, p, args.field)
     # codecs without compiled-in bit-sliced kernels: let the run-time
-    # specialisation (rse_jit.cpp) finish before timing
-    print(f"kernels: {r.kernel_kind(wait=True)}", flush=True)
+    # specialisation (rse_jit.cpp) finish before timing, printing while it
+    # builds (a wide module is minutes of hiprtc on a slow host)
+    import threading
+    import time
+    t0 = time.time()
+    kind = []
+    th = threading.Thread(target=lambda: kind.append(r.kernel_kind(wait=True)))
+    th.start()  # the build (ctypes drops the GIL while it waits)
+    while th.is_alive():
+        th.join(10)
+        if th.is_alive():
+            print(f"  building ... {time.time() - t0:.0f} s", flush=True)
+    print(f"kernels: {kind[0]} ({time.time() - t0:.1f} s)", flush=True)
     elems = L // (args.field // 8)
     erased = [int(x) for x in args.erase.split(",")]
     present = [i not in erased for i in range(k + p)]
@@ -123,6 +134,8 @@ def main():
         print(f"  bitslice={bs} patterns={pat} variant={var} nt={nt} grid_x={gx:<5} "
               f"stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
+    from reed_solomon_erasure.core import last_kernel
+    print(f"last kernel: {last_kernel()}")
     print(json.dumps({"best": {"bitslice": b[4], "variant": b[3], "nt": b[0], "grid_x": b[1],
                                "stripes_in_flight": b[2], "GBps": round(rows[0][0], 1)}}))
 
