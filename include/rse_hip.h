@@ -272,6 +272,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        decode-pattern kernel */
 #define RSE_OPT_JIT_CSE 13          /* GF(2^16) specialised XOR networks: up to this many shared
                                        subexpressions per input (0..16), for modules built after */
+#define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
+                                       1/W of the inputs and shares the planes through LDS; 0 every
+                                       wave slices every input */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

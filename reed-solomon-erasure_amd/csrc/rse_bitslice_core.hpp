@@ -427,6 +427,91 @@ __device__ __forceinline__ void wide_body(const A& a) {
   if (mode != kStore && diff) atomicOr(h.mismatch, 1u);
 }
 
+// wide_body with the slicing shared through LDS: in round R, wave WI (of W)
+// slices input R*W + WI -- only that one -- and writes its 16 planes to an LDS
+// slot; after a barrier every wave codes the round's W inputs from LDS.  A
+// wave thus slices k/W inputs instead of k (slicing is a third of a wide
+// codec's VALU work).  Two slot sets alternate by a running round counter g,
+// so a set is rewritten only two barriers after it was read, across chunks
+// too: one barrier per round.
+template <int W>
+using WidePlanes = uint4[2][W][4][64];  // [set][slot][quad of planes][lane]
+
+template <class C, int W, int R, int S>
+__device__ __forceinline__ void wide_code_round(uint32_t (&acc)[C::p * 16],
+                                                const uint4 (&set)[W][4][64], uint32_t lane) {
+  if constexpr (S < W && R * W + S < C::k) {
+    uint32_t pl[16];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const uint4 v = set[S][q4][lane];
+      pl[q4 * 4 + 0] = v.x;
+      pl[q4 * 4 + 1] = v.y;
+      pl[q4 * 4 + 2] = v.z;
+      pl[q4 * 4 + 3] = v.w;
+    }
+    mac_input<C, R * W + S, false>(acc, pl, make_int_seq<C::p * 16>{});
+#pragma unroll
+    for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+    wide_code_round<C, W, R, S + 1>(acc, set, lane);
+  }
+}
+
+template <class C, int W, int WI, int R, class A>
+__device__ __forceinline__ void wide_rounds(uint32_t (&acc)[C::p * 16], u32x4 (&cur)[4],
+                                            const A& a, uint64_t off, WidePlanes<W>& lds,
+                                            uint32_t& g, uint32_t lane) {
+  constexpr int K = C::k, NR = (K + W - 1) / W;
+  if constexpr (R < NR) {
+    constexpr int mine = R * W + WI, next = (R + 1) * W + WI;
+    u32x4 nxt[4];
+    if constexpr (next < K) load4<false, 1024u>(nxt, a.in[next] + off);
+    __builtin_amdgcn_sched_barrier(0);
+    uint4(&set)[W][4][64] = lds[g & 1u];
+    if constexpr (mine < K) {
+      uint32_t pl[16];
+      slice<typename C::Field>(cur, pl);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        set[WI][q4][lane] = make_uint4(pl[q4 * 4], pl[q4 * 4 + 1], pl[q4 * 4 + 2], pl[q4 * 4 + 3]);
+    }
+    __syncthreads();
+    wide_code_round<C, W, R, 0>(acc, set, lane);
+    ++g;
+    if constexpr (next < K) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
+    wide_rounds<C, W, WI, R + 1, A>(acc, cur, a, off, lds, g, lane);
+  }
+}
+
+// Wave WI of W; C its share of the outputs (O0 the first).  All W waves call
+// this with the same `lds` (one workgroup-wide array).
+template <class C, int O0, int W, int WI, class A>
+__device__ __forceinline__ void wide_body_lds(const A& a, WidePlanes<W>& lds) {
+  const WideHdr& h = a.h;
+  const uint64_t total = h.chunks_per_stripe * h.n_stripes;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = lane * 16u;
+  const uint32_t mode = h.mode;
+  bool diff = false;
+  uint32_t g = 0;
+  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const uint64_t stripe = c / h.chunks_per_stripe, chunk = c - stripe * h.chunks_per_stripe;
+    const uint64_t off = stripe * h.stripe_stride + chunk * 4096u + lane_off;
+    uint32_t acc[C::p * 16];
+    u32x4 cur[4];
+    if constexpr (WI < C::k) load4<false, 1024u>(cur, a.in[WI] + off);
+    wide_rounds<C, W, WI, 0, A>(acc, cur, a, off, lds, g, lane);
+    store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
+    if (h.per_stripe && diff) {
+      atomicOr(h.mismatch + stripe, 1u);
+      diff = false;
+    }
+  }
+  if (mode != kStore && diff) atomicOr(h.mismatch, 1u);
+}
+
 // ------------------------------------------------------------ reconstruct
 // Bit-sliced syndrome reconstruct (BsReconArgs in rse_kernels.hpp).  The input
 // sequence is the present data shards, then the syndrome parity shards; the

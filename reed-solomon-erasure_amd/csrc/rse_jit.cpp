@@ -294,14 +294,21 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   // 64-thread group would give 64 VGPRs and spill
                   "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
                   "    amdgpu_waves_per_eu(2))) void rse_jit_wide(const WideArgs a) {\n"
+                  "  __shared__ rse::WidePlanes<%d> lds;\n"
                   "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
-                  k, p, p, 64 * W, 64 * W);
+                  k, p, p, 64 * W, 64 * W, W);
     s += buf;
+    const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, w, &o0, &n);
-      std::snprintf(buf, sizeof buf,
-                    "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
+      if (shared)
+        std::snprintf(buf, sizeof buf,
+                      "    case %d: rse::wide_body_lds<rse::JitWide%d, %u, %d, %d>(a, lds); break;\n",
+                      w, w, o0, W, w);
+      else
+        std::snprintf(buf, sizeof buf,
+                      "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
       s += buf;
     }
     s += "    default: break;\n  }\n}\n";

@@ -758,6 +758,7 @@ struct Options {
   int64_t jit = 1;                // run-time specialised bit-sliced kernels (rse_jit.cpp)
   int64_t jit_patterns = 1;       // ... also for repeated decode patterns
   int64_t jit_cse = 16;           // GF(2^16) specialised networks: temporaries per input
+  int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1094,6 +1095,7 @@ int set_option(int key, int64_t value) {
     case 9: g_opt.jit = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case 11: g_opt.jit_patterns = value ? 1 : 0; return 0;
     case 13: g_opt.jit_cse = value < 0 ? 0 : value > 16 ? 16 : value; return 0;
+    case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1122,6 +1124,7 @@ int64_t get_option(int key) {
     case 10: return jit_modules_built();
     case 11: return g_opt.jit_patterns;
     case 13: return g_opt.jit_cse;
+    case 14: return g_opt.wide_lds;
     default: return -1;
   }
 }

@@ -45,8 +45,12 @@ def main():
                          "kernels; the run-time builds are waited for)")
     ap.add_argument("--jit-cse", type=int, default=-1,
                     help="RSE_OPT_JIT_CSE for run-time specialised GF(2^16) modules (-1: default)")
+    ap.add_argument("--wide-lds", type=int, default=-1,
+                    help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
     args = ap.parse_args()
     lib = R._lib.load()
+    if args.wide_lds >= 0:
+        lib.rse_set_option(14, args.wide_lds)
     lib.rse_set_option(9, 2)  # time run-time specialised kernels, not their build
     if args.jit_cse >= 0:
         lib.rse_set_option(13, args.jit_cse)
