@@ -265,13 +265,20 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_HOST_H2D_STREAMS 8  /* rse_*_host*: streams carrying H2D copies (1..4) */
 #define RSE_OPT_JIT 9               /* run-time specialised kernels: 0 off, 1 used once built
                                        (default), 2 the first launch waits for the build */
-#define RSE_OPT_JIT_MODULES 10      /* read-only: specialised modules built in this process */
+#define RSE_OPT_JIT_MODULES 10      /* read-only: specialised modules compiled by this process
+                                       (builds run in rse_jitc helper processes, several at a
+                                       time, when the helper sits next to the library) */
 #define RSE_OPT_JIT_PATTERNS 11     /* 1: decode patterns used twice get their own specialised
                                        kernel (reconstruct at encode speed); 0 off */
 #define RSE_OPT_PATTERN_LAUNCHES 12 /* read-only, per thread: reconstructs that ran on a
                                        decode-pattern kernel */
 #define RSE_OPT_JIT_CSE 13          /* GF(2^16) specialised XOR networks: up to this many shared
                                        subexpressions per input (0..16), for modules built after */
+#define RSE_OPT_JIT_DISK_CACHE 15   /* 1 (default): specialised modules are cached on disk
+                                       ($RSE_JIT_CACHE_DIR, else $XDG_CACHE_HOME/rse_hip, else
+                                       ~/.cache/rse_hip), keyed by library version + source, so
+                                       another process loads them instead of compiling */
+#define RSE_OPT_JIT_CACHE_HITS 16   /* read-only: modules this process loaded from the disk cache */
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */

@@ -15,13 +15,22 @@
 // launch there needs it.  Until the module is ready the table kernels serve the
 // codec (RSE_OPT_JIT 1), or the first launch waits for it (RSE_OPT_JIT 2).
 // Which kernel runs never changes a result.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cerrno>
+#include <csignal>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <deque>
 #include <cstdio>
 #include <cstdlib>
@@ -33,8 +42,11 @@
 #include <utility>
 #include <vector>
 
+#include "../../include/rse_hip.h"
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
+
+extern char** environ;
 
 namespace rse {
 namespace {
@@ -74,13 +86,17 @@ struct Entry {
   std::vector<Loaded> loaded;
 };
 
-std::mutex g_mu;  // guards the registry and the job queues
-std::condition_variable g_cv;
+// The registry, the queues and their lock are never destroyed: a thread of
+// the host program may still be waiting on a build when the library is
+// unloaded at exit (the Worker destructor wakes it), and must find them alive.
+std::mutex& g_mu = *new std::mutex;  // guards the registry and the job queues
+std::condition_variable& g_cv = *new std::condition_variable;
 // Build queues, in priority order: encode modules of codecs and decode
 // patterns, reconstruct modules, then wide-codec blocks (many, each seconds of
 // hiprtc: they must not delay the modules the narrow codecs wait for).
 constexpr int kBlkQueue = 2;
-std::deque<Entry*> g_jobs[3];
+constexpr int kQueues = 3;
+std::deque<Entry*>* const g_jobs = new std::deque<Entry*>[kQueues];
 int queue_of(const Entry& e, int stage) {
   return (e.kind == kJitBlock || e.kind == kJitBlockAcc || e.kind == kJitWide) ? kBlkQueue : stage;
 }
@@ -98,8 +114,8 @@ int g_pending_pattern_blocks = 0;  // queued, not yet built
 constexpr size_t kMaxPendingPatternJobs = 8;
 
 std::vector<std::unique_ptr<Entry>>& registry() {
-  static std::vector<std::unique_ptr<Entry>> v;
-  return v;
+  static auto* v = new std::vector<std::unique_ptr<Entry>>;  // never destroyed (see g_mu)
+  return *v;
 }
 
 bool same_rows(const Entry& e, const uint16_t* rows, size_t stride) {
@@ -351,18 +367,146 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   return s;
 }
 
-std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
-  auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind);
-  const auto t0 = std::chrono::steady_clock::now();
+// ---------------------------------------------------------------- building
+// A module's code object comes from, in order: the on-disk cache (keyed by a
+// hash of the library version, the hiprtc options and the complete source --
+// the source holds the codec's bit matrices, so equal keys mean equal code);
+// the rse_jitc helper process next to the library (several build at once, and
+// a build in flight is stopped when the library is unloaded); or hiprtc in
+// this process.  Fresh builds are written to the cache (atomic rename), so the
+// next process that needs the module loads it in milliseconds.
+const char* const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+std::atomic<int64_t> g_cache_hits{0};
+
+std::string hash_key(const std::string& src) {
+  uint64_t h1 = 0xcbf29ce484222325ull, h2 = 0x84222325cbf29ce4ull;
+  auto mix = [&](const char* p, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      h1 = (h1 ^ (uint8_t)p[i]) * 0x100000001b3ull;
+      h2 = (h2 ^ (uint8_t)p[i]) * 0x100000001b3ull + (h2 >> 29);
+    }
+  };
+  const char* ver = rse_version();
+  mix(ver, std::strlen(ver));
+  for (const char* o : kJitOpts) mix(o, std::strlen(o) + 1);
+  mix(src.data(), src.size());
+  char buf[40];
+  std::snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)h1,
+                (unsigned long long)h2);
+  return buf;
+}
+
+bool make_dirs(const std::string& path) {
+  for (size_t i = 1; i <= path.size(); ++i)
+    if (i == path.size() || path[i] == '/') {
+      const std::string part = path.substr(0, i);
+      if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+  return access(path.c_str(), W_OK) == 0;
+}
+
+// The cache directory ("" = none): $RSE_JIT_CACHE_DIR, else
+// $XDG_CACHE_HOME/rse_hip, else $HOME/.cache/rse_hip.
+const std::string& cache_dir() {
+  static const std::string dir = [] {
+    std::string d;
+    if (const char* e = std::getenv("RSE_JIT_CACHE_DIR")) d = e;
+    else if (const char* x = std::getenv("XDG_CACHE_HOME")) d = std::string(x) + "/rse_hip";
+    else if (const char* h = std::getenv("HOME")) d = std::string(h) + "/.cache/rse_hip";
+    return (!d.empty() && make_dirs(d)) ? d : std::string();
+  }();
+  return dir;
+}
+
+// rse_jitc next to librse_hip.so, if present.
+const std::string& helper_path() {
+  static const std::string path = [] {
+    Dl_info info;
+    if (!dladdr(reinterpret_cast<void*>(&hash_key), &info) || !info.dli_fname) return std::string();
+    std::string p = info.dli_fname;
+    const size_t slash = p.rfind('/');
+    p = (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/rse_jitc";
+    return access(p.c_str(), X_OK) == 0 ? p : std::string();
+  }();
+  return path;
+}
+
+bool read_file(const std::string& path, std::string* out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  *out = ss.str();
+  return !out->empty();
+}
+
+bool write_file(const std::string& path, const std::string& data) {
+  std::ofstream f(path, std::ios::binary | std::ios::trunc);
+  f.write(data.data(), (std::streamsize)data.size());
+  return f.good();
+}
+
+// Children of the build threads (slot per thread), stopped at unload.
+constexpr int kMaxBuilders = 8;
+std::atomic<pid_t> g_child[kMaxBuilders];
+std::atomic<bool> g_unloading{false};
+
+// Builds src with the helper process (thread slot `slot`); false if it could
+// not run (the caller falls back to hiprtc in process).
+bool build_with_helper(const std::string& src, const std::string& key, int slot, Compiled* out) {
+  const std::string& helper = helper_path();
+  if (helper.empty()) return false;
+  std::string dir = cache_dir();
+  if (dir.empty()) {
+    const char* t = std::getenv("TMPDIR");
+    dir = t ? t : "/tmp";
+  }
+  char tag[64];
+  std::snprintf(tag, sizeof tag, ".%d.%d", (int)getpid(), slot);
+  const std::string src_path = dir + "/" + key + tag + ".hip";
+  const std::string out_path = dir + "/" + key + tag + ".co";
+  if (!write_file(src_path, src)) return false;
+  std::vector<std::string> args = {helper, src_path, out_path};
+  for (const char* o : kJitOpts) args.push_back(o);
+  std::vector<char*> argv;
+  for (auto& a : args) argv.push_back(&a[0]);
+  argv.push_back(nullptr);
+  pid_t pid = 0;
+  if (g_unloading.load() || posix_spawn(&pid, helper.c_str(), nullptr, nullptr, argv.data(), environ) != 0) {
+    unlink(src_path.c_str());
+    return false;
+  }
+  g_child[slot].store(pid);
+  int status = 0;
+  pid_t w;
+  do {
+    w = waitpid(pid, &status, 0);
+  } while (w < 0 && errno == EINTR);
+  g_child[slot].store(0);
+  unlink(src_path.c_str());
+  if (w == pid && WIFEXITED(status) && WEXITSTATUS(status) == 0 && read_file(out_path, &out->code)) {
+    out->ok = true;
+    if (cache_dir().empty() || get_option(15) == 0 ||
+        rename(out_path.c_str(), (cache_dir() + "/" + key + ".co").c_str()) != 0)
+      unlink(out_path.c_str());
+  } else {
+    unlink(out_path.c_str());
+    out->log = "rse_jitc failed";
+    if (w == pid && WIFEXITED(status) && WEXITSTATUS(status) == 2) return false;  // I/O: retry here
+  }
+  return true;
+}
+
+// In-process hiprtc (no helper, or it could not run).
+void build_in_process(const std::string& src, Compiled* out) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "rse_jit.hip", 0, nullptr, nullptr) !=
       HIPRTC_SUCCESS) {
     out->log = "hiprtcCreateProgram failed";
-    return out;
+    return;
   }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-  const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  const hiprtcResult r =
+      hiprtcCompileProgram(prog, (int)(sizeof kJitOpts / sizeof kJitOpts[0]), kJitOpts);
   size_t n = 0;
   if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
     out->log.assign(n, '\0');
@@ -373,6 +517,29 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
     out->ok = hiprtcGetCode(prog, &out->code[0]) == HIPRTC_SUCCESS;
   }
   hiprtcDestroyProgram(&prog);
+}
+
+std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
+  auto out = std::make_shared<Compiled>();
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind);
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::string key = hash_key(src);
+  const bool disk = get_option(15) != 0 && !cache_dir().empty();
+  if (disk && read_file(cache_dir() + "/" + key + ".co", &out->code)) {
+    out->ok = true;
+    ++g_cache_hits;
+  } else {
+    if (!build_with_helper(src, key, slot, out.get())) {
+      build_in_process(src, out.get());
+      if (out->ok && disk) {  // cache it (atomic: another process may read it)
+        const std::string tmp = cache_dir() + "/" + key + "." + std::to_string(getpid()) + ".tmp";
+        if (!write_file(tmp, out->code) ||
+            rename(tmp.c_str(), (cache_dir() + "/" + key + ".co").c_str()) != 0)
+          unlink(tmp.c_str());
+      }
+    }
+    if (out->ok) ++g_built;
+  }
   out->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (const char* dir = std::getenv("RSE_JIT_DUMP")) {  // debugging aid
     char path[1024];
@@ -389,32 +556,50 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage) {
       std::fclose(f);
     }
   }
-  if (out->ok) ++g_built;
   return out;
 }
 
-// One background compiler thread, started with the first registration and
-// joined when the library is unloaded (a compile in flight finishes first; jobs
-// still queued then are completed as failed so nothing waits forever).
+// Build threads, started with the first registration: several when the
+// helper process is available (each runs one rse_jitc at a time), else one
+// (comgr serialises in-process compiles anyway).  They take jobs in queue
+// priority order.  At library unload the threads are stopped: a helper still
+// compiling is killed (its job completes as failed), jobs still queued are
+// completed as failed, so nothing waits forever and exit is not held up by a
+// build (an in-process hiprtc call, without the helper, still runs to its end).
 class Worker {
  public:
   void start() {
-    if (!th_.joinable()) th_ = std::thread([this] { run(); });
+    std::lock_guard<std::mutex> g(start_mu_);
+    if (!th_.empty()) return;
+    int n = 1;
+    if (!helper_path().empty()) {
+      const unsigned hw = std::thread::hardware_concurrency();
+      n = (int)std::max(1u, std::min<unsigned>(kMaxBuilders, hw / 2));
+      if (const char* e = std::getenv("RSE_JIT_THREADS")) n = std::max(1, std::min(kMaxBuilders, std::atoi(e)));
+    }
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { run(i); });
   }
   ~Worker() {
     {
       std::lock_guard<std::mutex> g(g_mu);
       stop_ = true;
     }
+    g_unloading.store(true);
     g_cv.notify_all();
-    if (th_.joinable()) th_.join();
-    for (auto& q : g_jobs)
-      for (Entry* e : q)
-        e->promise[&q - g_jobs == kRec ? kRec : kEnc].set_value(std::make_shared<Compiled>());
+    for (auto& c : g_child)
+      if (pid_t pid = c.load()) kill(pid, SIGKILL);
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+    std::lock_guard<std::mutex> g(g_mu);
+    for (int q = 0; q < kQueues; ++q) {
+      for (Entry* e : g_jobs[q])
+        e->promise[q == kRec ? kRec : kEnc].set_value(std::make_shared<Compiled>());
+      g_jobs[q].clear();
+    }
   }
 
  private:
-  void run() {
+  void run(int slot) {
     for (;;) {
       Entry* e = nullptr;
       int stage = 0;
@@ -430,14 +615,15 @@ class Worker {
         e = g_jobs[q].front();
         g_jobs[q].pop_front();
       }
-      e->promise[stage].set_value(compile(*e, stage));
+      e->promise[stage].set_value(compile(*e, stage, slot));
       if (e->pattern_block) {
         std::lock_guard<std::mutex> g(g_mu);
         --g_pending_pattern_blocks;
       }
     }
   }
-  std::thread th_;
+  std::mutex start_mu_;
+  std::vector<std::thread> th_;
   bool stop_ = false;
 };
 
@@ -493,13 +679,15 @@ void for_each_block(uint32_t k, uint32_t p, F&& f) {
 // before it).
 void promote(Entry* e) {
   std::lock_guard<std::mutex> g(g_mu);
-  for (auto& q : g_jobs)
+  for (int qi = 0; qi < kQueues; ++qi) {
+    std::deque<Entry*>& q = g_jobs[qi];
     for (auto it = q.begin(); it != q.end(); ++it)
       if (*it == e) {
         q.erase(it);
         q.push_front(e);
         break;
       }
+  }
 }
 
 int status_of(Entry* e, bool wait) {
@@ -727,5 +915,6 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
 }
 
 int64_t jit_modules_built() { return g_built.load(); }
+int64_t jit_cache_hits() { return g_cache_hits.load(); }
 
 }  // namespace rse

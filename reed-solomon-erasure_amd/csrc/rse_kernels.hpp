@@ -207,7 +207,8 @@ struct JitFns {
 // kJitBlockAcc entry (stage 0) instead.
 bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t stride, int stage,
               JitFns* out, hipError_t* err, bool acc = false);
-int64_t jit_modules_built();  // RSE_OPT_JIT_MODULES
+int64_t jit_modules_built();  // RSE_OPT_JIT_MODULES (compiled in this process)
+int64_t jit_cache_hits();     // RSE_OPT_JIT_CACHE_HITS (loaded from the disk cache)
 
 // Launch-shape options (keys as RSE_OPT_* in include/rse_hip.h).
 int set_option(int key, int64_t value);

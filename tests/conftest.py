@@ -1,7 +1,13 @@
 import os
 import sys
+import tempfile
 
 import pytest
+
+# Run-time specialised modules go to a fresh on-disk cache per test session
+# (RSE_OPT_JIT_DISK_CACHE), so build counters mean builds and no run reuses
+# another's modules; tests of the cache itself set their own directories.
+os.environ.setdefault("RSE_JIT_CACHE_DIR", tempfile.mkdtemp(prefix="rse_jit_cache_"))
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "reed-solomon-erasure_amd")

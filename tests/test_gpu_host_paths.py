@@ -392,3 +392,43 @@ def test_last_kernel_reports_what_ran(R):
     r.encode(small)
     assert last_kernel().startswith("table gf8 10+4"), last_kernel()
     torch.cuda.synchronize()
+
+
+# ------------------------------------------------------ JIT disk cache
+def test_cached_module_gives_oracle_bytes(tmp_path):
+    """A run-time specialised module built by one process and loaded from the
+    on-disk cache by another (no compile: RSE_OPT_JIT_MODULES stays 0) codes
+    the oracle's bytes, on its bit-sliced kernels."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSE_JIT_CACHE_DIR=str(tmp_path))
+    pre = ("import sys; sys.path.insert(0, 'reed-solomon-erasure_amd'); sys.path.insert(0, '.'); "
+           "import reed_solomon_erasure as R; L = R._lib.load(); ")
+    build = subprocess.run([sys.executable, "-c", pre +
+                            "print(R.galois_16.ReedSolomon(11, 5).kernel_kind(wait=True))"],
+                           capture_output=True, text=True, env=env, timeout=600, cwd=root)
+    assert build.stdout.split() == ["bitslice-specialised"], build.stderr[-2000:]
+    use = pre + """
+import numpy as np, torch
+from oracle import oracle as O
+L.rse_set_option(9, 2)
+k, p, n = 11, 5, 3 * 16384 + 4096 + 10
+rng = np.random.default_rng(5)
+full = [rng.integers(0, 256, 2 * n, dtype=np.uint8) for _ in range(k)] + \\
+       [np.zeros(2 * n, np.uint8) for _ in range(p)]
+O.Codec(16, k, p).encode(full)
+r = R.galois_16.ReedSolomon(k, p)
+t = [torch.from_numpy(x).cuda().view(n, 2) for x in full[:k]] + \\
+    [torch.zeros((n, 2), dtype=torch.uint8, device='cuda') for _ in range(p)]
+b0 = L.rse_get_option(6)
+r.encode(t)
+torch.cuda.synchronize()
+same = all((t[k + i].cpu().numpy().reshape(-1) == full[k + i]).all() for i in range(p))
+print(same, L.rse_get_option(6) - b0 > 0, L.rse_get_option(10), L.rse_get_option(16))
+"""
+    out = subprocess.run([sys.executable, "-c", use], capture_output=True, text=True, env=env,
+                         timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    same, bitsliced, built, hits = out.stdout.split()
+    assert same == "True" and bitsliced == "True" and built == "0" and int(hits) >= 1
