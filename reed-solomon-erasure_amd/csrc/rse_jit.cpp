@@ -407,27 +407,29 @@ bool make_dirs(const std::string& path) {
 
 // The cache directory ("" = none): $RSE_JIT_CACHE_DIR, else
 // $XDG_CACHE_HOME/rse_hip, else $HOME/.cache/rse_hip.
+// (Never destroyed, like the registry: build threads read it until the
+// Worker destructor has stopped them, which may run after static strings die.)
 const std::string& cache_dir() {
-  static const std::string dir = [] {
+  static const std::string& dir = *new std::string([] {
     std::string d;
     if (const char* e = std::getenv("RSE_JIT_CACHE_DIR")) d = e;
     else if (const char* x = std::getenv("XDG_CACHE_HOME")) d = std::string(x) + "/rse_hip";
     else if (const char* h = std::getenv("HOME")) d = std::string(h) + "/.cache/rse_hip";
     return (!d.empty() && make_dirs(d)) ? d : std::string();
-  }();
+  }());
   return dir;
 }
 
 // rse_jitc next to librse_hip.so, if present.
 const std::string& helper_path() {
-  static const std::string path = [] {
+  static const std::string& path = *new std::string([] {
     Dl_info info;
     if (!dladdr(reinterpret_cast<void*>(&hash_key), &info) || !info.dli_fname) return std::string();
     std::string p = info.dli_fname;
     const size_t slash = p.rfind('/');
     p = (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/rse_jitc";
     return access(p.c_str(), X_OK) == 0 ? p : std::string();
-  }();
+  }());
   return path;
 }
 

@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librse_hip.so")
+# RSE_LIB_PATH: another build of the same library (the sanitizer builds of
+# tools/sanitize.sh); the default is the in-tree librse_hip.so.
+LIB_PATH = os.environ.get("RSE_LIB_PATH") or os.path.join(HERE, "librse_hip.so")
 
 # Every entry point of include/rse_hip.h (checked by tests/test_capi.py).
 EXPORTS = (
