@@ -279,6 +279,8 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        ~/.cache/rse_hip), keyed by library version + source, so
                                        another process loads them instead of compiling */
 #define RSE_OPT_JIT_CACHE_HITS 16   /* read-only: modules this process loaded from the disk cache */
+#define RSE_OPT_RECON_MIX 17        /* syndrome reconstruct of the compiled-in codecs: 1 (default)
+                                       the e x e mixing bit-sliced, 0 on v_perm tables (A/B) */
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */

@@ -312,14 +312,14 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_dma_kerne
   if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
 }
 
-template <class C, bool NT, int NS>
-__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_kernel(
+template <class C, bool NT, int NS, bool MIXB = true>
+__global__ __launch_bounds__(kBsBlock, NS > 2 ? 2 : 3) void bitslice_recon_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_body<C, NT, NS>(a, chunks_per_stripe);
+  bitslice_recon_body<C, NT, NS, MIXB>(a, chunks_per_stripe);
 }
 
 template <class C, bool NT, int NS>
-__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_kernel(
+__global__ __launch_bounds__(kBsBlock, NS > 2 ? 2 : 3) void bitslice_recon_desc_kernel(
     const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
   bitslice_recon_desc_body<C, NT, NS>(descs, chunks_per_stripe, n_stripes);
 }
@@ -479,12 +479,13 @@ struct BsShape {
                       // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
   BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
   BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
+  BsRecFn rec_tab[4]; // the same with the e x e mixing on v_perm tables (RSE_OPT_RECON_MIX 0)
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
 
-template <class C, int NS>
+template <class C, int NS, bool MIXB = true>
 constexpr BsRecFn rec_fn() {
-  if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS>;
+  if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS, MIXB>;
   else return nullptr;
 }
 template <class C, int NS>
@@ -509,6 +510,8 @@ constexpr BsDescFn rec_desc_fn() {
    bitslice_kernel<Code<F, K, P>, true, true, false, false, false, true>,          \
    {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
     rec_fn<Code<F, K, P>, 8>()},                                                   \
+   {rec_fn<Code<F, K, P>, 1, false>(), rec_fn<Code<F, K, P>, 2, false>(),          \
+    rec_fn<Code<F, K, P>, 4, false>(), rec_fn<Code<F, K, P>, 8, false>()},          \
    {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
     rec_desc_fn<Code<F, K, P>, 4>(), rec_desc_fn<Code<F, K, P>, 8>()}}
 static const BsShape kBsShapes[] = {
@@ -628,8 +631,11 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     for (int q = 0; q < 4 && slot < 0; ++q)
       if (sh.rec[q] && (1u << q) >= need) slot = q;
     if (slot < 0) return hipSuccess;
-    note_kernel("bitslice-recon gf%d %u+%u ns%d", field, k, p, 1 << slot);
-    hipLaunchKernelGGL(sh.rec[slot], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
+    const bool mixb = get_option(17) != 0;
+    note_kernel("bitslice-recon gf%d %u+%u ns%d %s", field, k, p, 1 << slot,
+                mixb ? "mix-bitsliced" : "mix-tables");
+    hipLaunchKernelGGL(mixb ? sh.rec[slot] : sh.rec_tab[slot], dim3((uint32_t)gx), dim3(kBsBlock),
+                       0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     count_bitslice_launch();

@@ -602,9 +602,182 @@ __device__ __forceinline__ void recon_tables(const BsReconArgs& a, uint4* tq, ui
   }
 }
 
+// ---- bit-sliced run-time mixing -------------------------------------------
+// A run-time constant c times sliced planes s, accumulated: c*s is the XOR of
+// y_b = e_b * s over the set bits b of c, e_b the element with only bit b set.
+// The y_b follow from s by compile-time maps: doubling every byte (xtime,
+// generator polynomial 0x11D, build.rs:11) -- a renaming of the 8 planes of a
+// byte plus 3 XORs -- and, for GF(2^16), one multiplication by x
+// (galois_16.rs:146-162: x*(H x + L) = (2H + L) x + 128 H).  The bits of c are
+// wave-uniform, so each selects its XORs with a scalar branch: ~half of c's
+// 8/16 bits are set, each costing 16 planes of XOR (two bits per v_bitop3),
+// with no tables, no v_perm and no un-slicing of the syndromes.
+
+// y *= 2 in every byte (planes 8g..8g+7 are bits 0..7 of byte group g).
+__device__ __forceinline__ void xtime_planes(uint32_t (&y)[16]) {
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    uint32_t* b = y + 8 * g;
+    const uint32_t t = b[7];
+#pragma unroll
+    for (int q = 7; q > 0; --q) b[q] = b[q - 1];
+    b[0] = t;
+    b[2] ^= t;
+    b[3] ^= t;
+    b[4] ^= t;
+  }
+}
+
+// y = x * s for GF(2^16) planes (0..7: H = coefficient of x, 8..15: L).
+__device__ __forceinline__ void mul_x_planes(const uint32_t (&s)[16], uint32_t (&y)[16]) {
+  uint32_t h[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    h[q] = s[q];
+    h[8 + q] = s[q];
+  }
+  xtime_planes(h);  // h[0..7] = 2H (h[8..15] = 2H too: the 128 H chain below starts there)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = h[q] ^ s[8 + q];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) xtime_planes(h);  // h[8..15] = 2^7 H = 128 H
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[8 + q] = h[8 + q];
+}
+
+// out[g] ^= (bits b, b+1 of c[g]) selection of y0 = e_b s, y1 = e_{b+1} s.
+template <int G>
+__device__ __forceinline__ void mix_pair(uint32_t (&out)[G][16], const uint32_t (&c)[G], int b,
+                                         const uint32_t (&y0)[16], const uint32_t (&y1)[16]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t m = (c[g] >> b) & 3u;  // wave-uniform
+    // (the pins keep each case a real branch: speculated into selects, the
+    // three cases' temporaries would all be live at once and spill)
+    if (m == 3u) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        out[g][q] = xor3(out[g][q], y0[q], y1[q]);
+        asm volatile("" : "+v"(out[g][q]));
+      }
+    } else if (m == 1u) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        out[g][q] ^= y0[q];
+        asm volatile("" : "+v"(out[g][q]));
+      }
+    } else if (m == 2u) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        out[g][q] ^= y1[q];
+        asm volatile("" : "+v"(out[g][q]));
+      }
+    }
+  }
+}
+
+// out[g] ^= c[g] * s for G outputs at once (one y chain for all of them).
+template <class F, int G>
+__device__ __forceinline__ void mix_row(uint32_t (&out)[G][16], const uint32_t (&c)[G],
+                                        const uint32_t (&s)[16]) {
+  uint32_t y0[16], y1[16];
+  // low byte of c: e_b = 2^b (GF(2^8), and the constant part of GF(2^16))
+#pragma unroll
+  for (int q = 0; q < 16; ++q) y0[q] = s[q];
+#pragma unroll 1
+  for (int b = 0; b < 8; b += 2) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) y1[q] = y0[q];
+    xtime_planes(y1);
+    mix_pair<G>(out, c, b, y0, y1);
+    if (b < 6) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) y0[q] = y1[q];
+      xtime_planes(y0);
+    }
+  }
+  if constexpr (F::kPlanes == 16) {  // high byte of c: e_b = x * 2^(b-8)
+    mul_x_planes(s, y0);
+#pragma unroll 1
+    for (int b = 8; b < 16; b += 2) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) y1[q] = y0[q];
+      xtime_planes(y1);
+      mix_pair<G>(out, c, b, y0, y1);
+      if (b < 14) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) y0[q] = y1[q];
+        xtime_planes(y0);
+      }
+    }
+  }
+}
+
+// The mixing of recon_chunk on sliced syndromes, outputs in groups of G
+// (NS rows + G outputs + the y pair fit the VGPR budget at NS = 8); each
+// output un-sliced once and stored.  A: BsReconArgs (kernarg or a per-stripe
+// descriptor in memory: read uniform either way).
+template <class C, bool NT, int NS, int G>
+__device__ __forceinline__ void recon_mix_bitsliced(const BsReconArgs& a,
+                                                    const uint32_t (&acc)[NS * 16], uint64_t off) {
+  using F = typename C::Field;
+  const uint32_t n_out = __builtin_amdgcn_readfirstlane(a.n_out);
+  const uint32_t synd = __builtin_amdgcn_readfirstlane(a.synd);
+#pragma unroll 1
+  for (uint32_t o0 = 0; o0 < n_out; o0 += G) {
+    uint32_t out[G][16];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) out[g][q] = 0u;
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      uint32_t c[G];
+      uint32_t any = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t o = o0 + g;
+        const bool live = o < n_out;
+        // a missing parity output starts from its sigma row
+        if (live && __builtin_amdgcn_readfirstlane(a.out_sigma[live ? o : 0]) == r) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) out[g][q] ^= acc[r * 16 + q];
+        }
+        c[g] = (live && ((synd >> r) & 1u)) ? __builtin_amdgcn_readfirstlane(a.w[live ? o : 0][r]) : 0u;
+        any |= c[g];
+      }
+      if (any) {
+        // a fresh copy per pass (the pin): otherwise LICM hoists the y chains
+        // of every row out of the pass loop, NS x 16 more live VGPRs
+        uint32_t s[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          s[q] = acc[r * 16 + q];
+          asm volatile("" : "+v"(s[q]));
+        }
+        mix_row<F, G>(out, c, s);
+      }
+      // keep each row's work together (as recon_inputs does across inputs)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(out[g][q]));
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (o0 + g >= n_out) break;
+      u32x4 v[4];
+      unslice<F>(out[g], v);
+      uint8_t* dst = a.out[o0 + g];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stv<NT>(dst + off + j * (kBsBlock * 16), v[j]);
+    }
+  }
+}
+
 // One 16 KiB chunk of one stripe: off is the lane's byte offset from the
 // argument block's shard pointers.
-template <class C, bool NT, int NS>
+template <class C, bool NT, int NS, bool MIXB = true>
 __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* tq,
                                             const uint32_t* tt2, uint64_t off) {
   using F = typename C::Field;
@@ -617,6 +790,12 @@ __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* t
   u32x4 cur[4];
   load4<NT>(cur, recon_ptr(a, C::k, first) + off);
   recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
+  if constexpr (MIXB) {  // the mixing on the sliced syndromes (recon_mix_bitsliced)
+    // outputs per pass: NS rows + G outputs + the y pair within the VGPR
+    // budget of the launch bounds (3 waves/SIMD up to NS = 2, else 2)
+    recon_mix_bitsliced<C, NT, NS, (NS <= 4 ? NS : 2)>(a, acc, off);
+    return;
+  }
   // back to element order, in place
 #pragma unroll
   for (int r = 0; r < NS; ++r) {
@@ -667,30 +846,49 @@ struct ReconLds {
 };
 
 // Reconstruct body: one argument block for every stripe of the launch.
-// Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
-template <class C, bool NT, int NS>
+// Launch bounds: kBsBlock lanes, NS > 2 ? 2 : 3 waves/SIMD.
+// MIXB: the e x e mixing bit-sliced (default); false: on v_perm tables in LDS.
+template <class C, bool NT, int NS, bool MIXB = true>
 __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
                                                     uint64_t chunks_per_stripe) {
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  if constexpr (MIXB) {
+    for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+      const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+      recon_chunk<C, NT, NS, true>(a, nullptr, nullptr,
+                                   stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
+    }
+    return;
+  }
   constexpr int T = ReconLds<NS, typename C::Field>::kTabs;
   __shared__ uint4 tq[T];
   __shared__ uint32_t tt2[T];
   recon_tables<C, NS>(a, tq, tt2);
   __syncthreads();
-  const uint64_t total = chunks_per_stripe * a.n_stripes;
   for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    recon_chunk<C, NT, NS>(a, tq, tt2,
-                           stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
+    recon_chunk<C, NT, NS, false>(a, tq, tt2,
+                                  stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
   }
 }
 
 // Reconstruct body over per-stripe argument blocks (descs[s], written by the
 // device planner of rse_reconstruct_batch: every stripe its own erasure
 // pattern).  A workgroup rebuilds its mixing tables when its stripe changes.
-template <class C, bool NT, int NS>
+template <class C, bool NT, int NS, bool MIXB = true>
 __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __restrict__ descs,
                                                          uint64_t chunks_per_stripe,
                                                          uint64_t n_stripes) {
+  if constexpr (MIXB) {
+    const uint64_t total = chunks_per_stripe * n_stripes;
+    for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+      const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+      const BsReconArgs& a = descs[stripe];
+      if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
+      recon_chunk<C, NT, NS, true>(a, nullptr, nullptr, chunk * kBsChunk + threadIdx.x * 16u);
+    }
+    return;
+  }
   constexpr int T = ReconLds<NS, typename C::Field>::kTabs;
   __shared__ uint4 tq[T];
   __shared__ uint32_t tt2[T];
@@ -706,7 +904,7 @@ __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __re
       __syncthreads();
       built = stripe;
     }
-    recon_chunk<C, NT, NS>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
+    recon_chunk<C, NT, NS, false>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
   }
 }
 

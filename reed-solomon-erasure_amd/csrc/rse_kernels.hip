@@ -760,6 +760,7 @@ struct Options {
   int64_t jit_cse = 16;           // GF(2^16) specialised networks: temporaries per input
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
+  int64_t recon_mix = 1;          // syndrome reconstruct: bit-sliced mixing (0: v_perm tables)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1098,6 +1099,7 @@ int set_option(int key, int64_t value) {
     case 13: g_opt.jit_cse = value < 0 ? 0 : value > 16 ? 16 : value; return 0;
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
+    case 17: g_opt.recon_mix = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1129,6 +1131,7 @@ int64_t get_option(int key) {
     case 14: return g_opt.wide_lds;
     case 15: return g_opt.jit_disk_cache;
     case 16: return jit_cache_hits();
+    case 17: return g_opt.recon_mix;
     default: return -1;
   }
 }

@@ -45,6 +45,9 @@ def main():
                          "kernels; the run-time builds are waited for)")
     ap.add_argument("--jit-cse", type=int, default=-1,
                     help="RSE_OPT_JIT_CSE for run-time specialised GF(2^16) modules (-1: default)")
+    ap.add_argument("--recon-mix", default="1",
+                    help="comma list of RSE_OPT_RECON_MIX values (syndrome reconstruct mixing: "
+                         "1 bit-sliced, 0 v_perm tables)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
     args = ap.parse_args()
@@ -108,7 +111,8 @@ def main():
     bss = [int(x) for x in args.bitslice.split(",")]
     pats = [int(x) for x in args.patterns.split(",")] if args.op != "encode" else [1]
     nts = (0, 1) if not args.nt_only else (1,)
-    configs = [(nt, gx, gy, var, bs, pat) for pat in pats for bs in bss
+    mixes = [int(x) for x in args.recon_mix.split(",")]
+    configs = [(nt, gx, gy, var, bs, pat, mx) for mx in mixes for pat in pats for bs in bss
                for var in range(args.variants) for nt in nts for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -116,7 +120,8 @@ def main():
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for c in configs:
-            nt, gx, gy, var, bs, pat = c
+            nt, gx, gy, var, bs, pat, mx = c
+            lib.rse_set_option(17, mx)
             lib.rse_set_option(11, pat)
             lib.rse_set_option(5, bs)
             lib.rse_set_option(1, nt)
@@ -134,8 +139,8 @@ def main():
     what = f" erased {erased}" if args.op == "reconstruct" else ""
     size = f"{args.shard_kib} KiB" if args.shard_kib else f"{args.shard_mib} MiB"
     print(f"{args.op} GF(2^{args.field}) {k}+{p} x {size}, {S} stripes{what}; GB/s (1e9)")
-    for med, lo, hi, (nt, gx, gy, var, bs, pat) in rows:
-        print(f"  bitslice={bs} patterns={pat} variant={var} nt={nt} grid_x={gx:<5} "
+    for med, lo, hi, (nt, gx, gy, var, bs, pat, mx) in rows:
+        print(f"  bitslice={bs} patterns={pat} mix={mx} variant={var} nt={nt} grid_x={gx:<5} "
               f"stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
     from reed_solomon_erasure.core import last_kernel
