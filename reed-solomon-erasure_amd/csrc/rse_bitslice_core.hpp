@@ -677,38 +677,37 @@ __device__ __forceinline__ void mix_pair(uint32_t (&out)[G][16], const uint32_t 
 }
 
 // out[g] ^= c[g] * s for G outputs at once (one y chain for all of them).
+// Byte j of c: e_b = 2^(b - 8j) for j = 0 (GF(2^8), and GF(2^16)'s constant
+// part), x * 2^(b - 8j) for j = 1.  A byte's 8 doublings rotate the planes
+// back onto their registers, so the byte loop stays rolled (half the code)
+// at no cost in moves, while the steps inside it are unrolled (a doubling is
+// then a renaming plus 3 XORs per byte group).
 template <class F, int G>
 __device__ __forceinline__ void mix_row(uint32_t (&out)[G][16], const uint32_t (&c)[G],
                                         const uint32_t (&s)[16]) {
-  uint32_t y0[16], y1[16];
-  // low byte of c: e_b = 2^b (GF(2^8), and the constant part of GF(2^16))
-#pragma unroll
-  for (int q = 0; q < 16; ++q) y0[q] = s[q];
 #pragma unroll 1
-  for (int b = 0; b < 8; b += 2) {
+  for (int j = 0; j < F::kPlanes / 8; ++j) {
+    uint32_t y0[16], y1[16];
+    if (j == 0) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) y1[q] = y0[q];
-    xtime_planes(y1);
-    mix_pair<G>(out, c, b, y0, y1);
-    if (b < 6) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) y0[q] = y1[q];
-      xtime_planes(y0);
+      for (int q = 0; q < 16; ++q) y0[q] = s[q];
+    } else {
+      mul_x_planes(s, y0);
     }
-  }
-  if constexpr (F::kPlanes == 16) {  // high byte of c: e_b = x * 2^(b-8)
-    mul_x_planes(s, y0);
-#pragma unroll 1
-    for (int b = 8; b < 16; b += 2) {
+    uint32_t cj[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) cj[g] = c[g] >> (8 * j);
+#pragma unroll
+    for (int b = 0; b < 8; b += 2) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) y1[q] = y0[q];
       xtime_planes(y1);
-      mix_pair<G>(out, c, b, y0, y1);
-      if (b < 14) {
+      mix_pair<G>(out, cj, b, y0, y1);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) y0[q] = y1[q];
-        xtime_planes(y0);
-      }
+      for (int q = 0; q < 16; ++q) y0[q] = y1[q];
+      xtime_planes(y0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(y0[q]));
     }
   }
 }
@@ -793,7 +792,7 @@ __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* t
   if constexpr (MIXB) {  // the mixing on the sliced syndromes (recon_mix_bitsliced)
     // outputs per pass: NS rows + G outputs + the y pair within the VGPR
     // budget of the launch bounds (3 waves/SIMD up to NS = 2, else 2)
-    recon_mix_bitsliced<C, NT, NS, (NS <= 4 ? NS : 2)>(a, acc, off);
+    recon_mix_bitsliced<C, NT, NS, (NS <= 4 ? NS : 2)>(a, acc, off);  // (probed: G = 4 at NS = 8 spills)
     return;
   }
   // back to element order, in place
