@@ -224,6 +224,16 @@ int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, si
 /* encode (core.rs:597-611) */
 int rse_encode_host(const rse_codec *codec, void *const *shards, const size_t *lens,
                     size_t n_shards, rse_stream_t stream);
+/* encode_sep (core.rs:617-632), encode_single (core.rs:545-562) and
+ * encode_single_sep (core.rs:576-592; ShardByShard's calls) on host shards. */
+int rse_encode_sep_host(const rse_codec *codec, const void *const *data, const size_t *data_lens,
+                        size_t n_data, void *const *parity, const size_t *parity_lens,
+                        size_t n_parity, rse_stream_t stream);
+int rse_encode_single_host(const rse_codec *codec, size_t i_data, void *const *shards,
+                           const size_t *lens, size_t n_shards, rse_stream_t stream);
+int rse_encode_single_sep_host(const rse_codec *codec, size_t i_data, const void *single,
+                               size_t single_len, void *const *parity, const size_t *parity_lens,
+                               size_t n_parity, rse_stream_t stream);
 /* Flat host stripes (rse_encode_flat layout, HOST memory): the same pipeline
  * over every chunk of every stripe, so PCIe stays busy across stripes. */
 int rse_encode_host_flat(const rse_codec *codec, void *stripes, size_t shard_len,

@@ -313,13 +313,13 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_dma_kerne
 }
 
 template <class C, bool NT, int NS, bool MIXB = true>
-__global__ __launch_bounds__(kBsBlock, NS > 2 ? 2 : 3) void bitslice_recon_kernel(
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
   bitslice_recon_body<C, NT, NS, MIXB>(a, chunks_per_stripe);
 }
 
 template <class C, bool NT, int NS>
-__global__ __launch_bounds__(kBsBlock, NS > 2 ? 2 : 3) void bitslice_recon_desc_kernel(
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_kernel(
     const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
   bitslice_recon_desc_body<C, NT, NS>(descs, chunks_per_stripe, n_stripes);
 }

@@ -845,13 +845,19 @@ struct ReconLds {
 };
 
 // Reconstruct body: one argument block for every stripe of the launch.
-// Launch bounds: kBsBlock lanes, NS > 2 ? 2 : 3 waves/SIMD.
-// MIXB: the e x e mixing bit-sliced (default); false: on v_perm tables in LDS.
+// Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
+// Which mixing a reconstruct kernel uses: bit-sliced for NS > 4 (up to 8
+// syndromes: +11 % at GF(2^16) 20+8 with 8 data shards lost), v_perm tables
+// in LDS below (with 3 waves/SIMD they are as fast or faster there:
+// profiles/r02_mix_*.log).  MIXB = false forces the tables (A/B).
+template <int NS, bool MIXB>
+constexpr bool kMixBitsliced = MIXB && NS > 4;
+
 template <class C, bool NT, int NS, bool MIXB = true>
 __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
                                                     uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
-  if constexpr (MIXB) {
+  if constexpr (kMixBitsliced<NS, MIXB>) {
     for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
       const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
       recon_chunk<C, NT, NS, true>(a, nullptr, nullptr,
@@ -878,7 +884,7 @@ template <class C, bool NT, int NS, bool MIXB = true>
 __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __restrict__ descs,
                                                          uint64_t chunks_per_stripe,
                                                          uint64_t n_stripes) {
-  if constexpr (MIXB) {
+  if constexpr (kMixBitsliced<NS, MIXB>) {
     const uint64_t total = chunks_per_stripe * n_stripes;
     for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
       const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;

@@ -729,9 +729,14 @@ int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens
   return run_plan_tail(c, plan, done, 0, 1, s);
 }
 
+int host_code(int field, const Rows& rows, const void* const* in, void* const* out, size_t len_bytes,
+              bool accumulate, hipStream_t s);
+
+// host: the shards are in host memory (rse_encode_sep_host): same validation,
+// then the host pipeline instead of device launches.
 int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* data_lens,
                     size_t n_data, void* const* parity, const size_t* parity_lens,
-                    size_t n_parity, hipStream_t s) {
+                    size_t n_parity, hipStream_t s, bool host = false) {
   int rc;
   if ((rc = check_count(n_data, c->k, RSE_TOO_FEW_DATA_SHARDS, RSE_TOO_MANY_DATA_SHARDS))) return rc;
   if ((rc = check_count(n_parity, c->p, RSE_TOO_FEW_PARITY_SHARDS, RSE_TOO_MANY_PARITY_SHARDS)))
@@ -742,6 +747,7 @@ int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* d
   if (data_lens[0] != parity_lens[0]) return RSE_INCORRECT_SHARD_SIZE;
   want_bitslice(c, data_lens[0] * c->esize());
   const Rows rows = parity_rows(c);
+  if (host) return host_code(c->field, rows, data, parity, data_lens[0] * c->esize(), false, s);
   Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(data),
         reinterpret_cast<uint8_t* const*>(parity), nullptr, data_lens[0] * c->esize(),
         rse::kStore, false, nullptr, 0, 1};
@@ -750,7 +756,7 @@ int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* d
 
 int encode_single_sep_impl(const rse_codec* c, size_t i_data, const void* single,
                            size_t single_len, void* const* parity, const size_t* parity_lens,
-                           size_t n_parity, hipStream_t s) {
+                           size_t n_parity, hipStream_t s, bool host = false) {
   int rc;
   if (i_data >= c->k) return RSE_INVALID_INDEX;
   if ((rc = check_count(n_parity, c->p, RSE_TOO_FEW_PARITY_SHARDS, RSE_TOO_MANY_PARITY_SHARDS)))
@@ -759,6 +765,10 @@ int encode_single_sep_impl(const rse_codec* c, size_t i_data, const void* single
   if ((rc = check_multi(parity_lens, n_parity))) return rc;
   if (parity_lens[0] != single_len) return RSE_INCORRECT_SHARD_SIZE;
   const Rows rows = single_column(c, i_data);
+  if (host) {
+    const void* hin[1] = {single};
+    return host_code(c->field, rows, hin, parity, single_len * c->esize(), i_data != 0, s);
+  }
   const uint8_t* in[1] = {static_cast<const uint8_t*>(single)};
   Job j{c->field, &rows, in, reinterpret_cast<uint8_t* const*>(parity), nullptr,
         single_len * c->esize(), rse::kStore, i_data != 0, nullptr, 0, 1};
@@ -1026,6 +1036,19 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   if (e != hipSuccess) return dev_fail(e);
   if (e2 != hipSuccess) return dev_fail(e2);
   return RSE_OK;
+}
+
+// rows x host inputs -> host outputs through the pipeline (kCode).
+int host_code(int field, const Rows& rows, const void* const* in, void* const* out, size_t len_bytes,
+              bool accumulate, hipStream_t s) {
+  std::vector<void*> ptrs(rows.n_in + rows.n_out);
+  for (size_t i = 0; i < rows.n_in; ++i) ptrs[i] = const_cast<void*>(in[i]);
+  for (size_t o = 0; o < rows.n_out; ++o) ptrs[rows.n_in + o] = out[o];
+  for (void* q : ptrs)
+    if (!q) return RSE_ERR_INVALID_ARGUMENT;
+  const HostCode hc{field, &rows, accumulate};
+  return host_pipeline(nullptr, HostOp::kCode, {HostStripe{ptrs.data(), nullptr, nullptr}},
+                       len_bytes, s, nullptr, &hc);
 }
 
 // Flat host stripes: shard i of stripe s at base + (s * total + i) * sb.
@@ -1427,14 +1450,38 @@ int rse_code_shards_host(int field, const uint8_t* rows, size_t n_out, size_t n_
   r.c.resize(n_out * n_in);
   for (size_t i = 0; i < n_out * n_in; ++i)
     r.c[i] = es == 2 ? (uint16_t)((rows[2 * i] << 8) | rows[2 * i + 1]) : rows[i];
-  std::vector<void*> ptrs(n_in + n_out);
-  for (size_t i = 0; i < n_in; ++i) ptrs[i] = const_cast<void*>(inputs[i]);
-  for (size_t o = 0; o < n_out; ++o) ptrs[n_in + o] = outputs[o];
-  for (void* q : ptrs)
-    if (!q) return RSE_ERR_INVALID_ARGUMENT;
-  const HostCode hc{field, &r, accumulate != 0};
-  return host_pipeline(nullptr, HostOp::kCode, {HostStripe{ptrs.data(), nullptr, nullptr}},
-                       len * es, (hipStream_t)stream, nullptr, &hc);
+  return host_code(field, r, inputs, outputs, len * es, accumulate != 0, (hipStream_t)stream);
+}
+
+int rse_encode_sep_host(const rse_codec* c, const void* const* data, const size_t* data_lens,
+                        size_t n_data, void* const* parity, const size_t* parity_lens,
+                        size_t n_parity, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  return encode_sep_impl(c, data, data_lens, n_data, parity, parity_lens, n_parity,
+                         (hipStream_t)stream, true);
+}
+
+int rse_encode_single_host(const rse_codec* c, size_t i_data, void* const* shards,
+                           const size_t* lens, size_t n, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  int rc;
+  if (i_data >= c->k) return RSE_INVALID_INDEX;  // core.rs:552
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  return encode_single_sep_impl(c, i_data, shards[i_data], lens[i_data], shards + c->k,
+                                lens + c->k, c->p, (hipStream_t)stream, true);
+}
+
+int rse_encode_single_sep_host(const rse_codec* c, size_t i_data, const void* single,
+                               size_t single_len, void* const* parity, const size_t* parity_lens,
+                               size_t n_parity, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  return encode_single_sep_impl(c, i_data, single, single_len, parity, parity_lens, n_parity,
+                                (hipStream_t)stream, true);
 }
 
 size_t rse_gal_mul(const uint8_t* low, const uint8_t* high, const uint8_t* in, uint8_t* out,

@@ -25,7 +25,8 @@ EXPORTS = (
     "rse_code_shards",
     "rse_code_shards_host", "rse_gf8_mul_slice", "rse_gal_mul", "rse_gal_mul_xor",
     "rse_gf16_mul_slice", "rse_gf8_invert_batch",
-    "rse_encode_host", "rse_encode_host_flat", "rse_verify_host", "rse_verify_with_buffer_host",
+    "rse_encode_host", "rse_encode_host_flat", "rse_encode_sep_host", "rse_encode_single_host",
+    "rse_encode_single_sep_host", "rse_verify_host", "rse_verify_with_buffer_host",
     "rse_verify_host_flat", "rse_reconstruct_host", "rse_reconstruct_data_host",
     "rse_reconstruct_host_batch", "rse_fill_splitmix",
     "rse_set_option", "rse_get_option", "rse_last_kernel",
@@ -68,6 +69,9 @@ _SIGS = {
     "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "rse_encode_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
     "rse_verify_host": (_c.c_int, [_vp, _vp, _szp, _sz, _ip, _vp]),
+    "rse_encode_sep_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _vp]),
+    "rse_encode_single_host": (_c.c_int, [_vp, _sz, _vp, _szp, _sz, _vp]),
+    "rse_encode_single_sep_host": (_c.c_int, [_vp, _sz, _vp, _sz, _vp, _szp, _sz, _vp]),
     "rse_verify_with_buffer_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _ip, _vp]),
     "rse_verify_host_flat": (_c.c_int, [_vp, _vp, _sz, _sz, _u8p, _vp]),
     "rse_reconstruct_host": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz, _vp]),

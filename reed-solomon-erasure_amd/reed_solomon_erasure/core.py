@@ -309,6 +309,28 @@ class ReedSolomon:
         pa, la = _host_arrays(shards, self.field)
         _raise(_lib.rse_encode_host(self._h, pa, la, len(shards), _stream()))
 
+    def encode_sep_host(self, data: Sequence, parity: Sequence) -> None:
+        """encode_sep() (core.rs:617-632) of host shards."""
+        dp, dl = _host_arrays(data, self.field)
+        pp, pl = _host_arrays(parity, self.field)
+        _raise(_lib.rse_encode_sep_host(self._h, dp, dl, len(data), pp, pl, len(parity), _stream()))
+
+    def encode_single_host(self, i_data: int, shards: Sequence) -> None:
+        """encode_single() (core.rs:545-562) of host shards."""
+        if i_data < 0:
+            raise RSError(Error.InvalidIndex)
+        pa, la = _host_arrays(shards, self.field)
+        _raise(_lib.rse_encode_single_host(self._h, i_data, pa, la, len(shards), _stream()))
+
+    def encode_single_sep_host(self, i_data: int, single, parity: Sequence) -> None:
+        """encode_single_sep() (core.rs:576-592) of host shards."""
+        if i_data < 0:
+            raise RSError(Error.InvalidIndex)
+        pp, pl = _host_arrays(parity, self.field)
+        _raise(_lib.rse_encode_single_sep_host(self._h, i_data, _host_ptr(single),
+                                               _host_elems(single, self.field), pp, pl,
+                                               len(parity), _stream()))
+
     def verify_host(self, shards: Sequence) -> bool:
         """verify() (core.rs:637-651) of host shards."""
         pa, la = _host_arrays(shards, self.field)

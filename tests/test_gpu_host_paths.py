@@ -432,3 +432,35 @@ print(same, L.rse_get_option(6) - b0 > 0, L.rse_get_option(10), L.rse_get_option
     assert out.returncode == 0, out.stderr[-3000:]
     same, bitsliced, built, hits = out.stdout.split()
     assert same == "True" and bitsliced == "True" and built == "0" and int(hits) >= 1
+
+
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 6, 3)])
+def test_encode_sep_and_single_host_match_oracle(R, small_chunks, field, k, p):
+    """encode_sep / encode_single / encode_single_sep on HOST shards
+    (core.rs:545-632) against the oracle, step by step."""
+    rng = np.random.default_rng(81 + k)
+    es, n = field // 8, 90_001
+    oc = O.Codec(field, k, p)
+    data = rand_shards(rng, k, n * es)
+    r = R.core.ReedSolomon(k, p, field)
+    par = [torch.zeros(n * es, dtype=torch.uint8).pin_memory() for _ in range(p)]
+    r.encode_sep_host([torch.from_numpy(d) for d in data], par)
+    want = [np.zeros(n * es, np.uint8) for _ in range(p)]
+    oc.encode_sep(data, want)
+    assert all((a.numpy() == b).all() for a, b in zip(par, want))
+    stale = [rng.integers(0, 256, n * es, dtype=np.uint8) for _ in range(p)]
+    ref = data + [x.copy() for x in stale]
+    ref_sep = [x.copy() for x in stale]
+    hs = [torch.from_numpy(x.copy()) for x in ref]
+    hp = [torch.from_numpy(x.copy()).pin_memory() for x in stale]
+    for i in range(k):
+        oc.encode_single(i, ref)
+        r.encode_single_host(i, hs)
+        oc.encode_single_sep(i, ref[i], ref_sep)
+        r.encode_single_sep_host(i, torch.from_numpy(data[i]), hp)
+        for j in range(p):
+            assert (hs[k + j].numpy() == ref[k + j]).all(), (i, j)
+            assert (hp[j].numpy() == ref_sep[j]).all(), (i, j)
+    with pytest.raises(R.RSError) as ei:
+        r.encode_single_host(k, hs)
+    assert ei.value.error == R.Error.InvalidIndex
