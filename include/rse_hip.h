@@ -283,7 +283,8 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_PATTERN_LAUNCHES 12 /* read-only, per thread: reconstructs that ran on a
                                        decode-pattern kernel */
 #define RSE_OPT_JIT_CSE 13          /* GF(2^16) specialised XOR networks: up to this many shared
-                                       subexpressions per input (0..16), for modules built after */
+                                       subexpressions per input (0..32, default 32), for modules
+                                       built after */
 #define RSE_OPT_JIT_DISK_CACHE 15   /* 1 (default): specialised modules are cached on disk
                                        ($RSE_JIT_CACHE_DIR, else $XDG_CACHE_HOME/rse_hip, else
                                        ~/.cache/rse_hip), keyed by library version + source, so

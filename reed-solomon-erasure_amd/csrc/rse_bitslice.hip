@@ -24,170 +24,13 @@ namespace {
 // barrier); GF(2^16), VALU-heavier, 0 (the scheduler's own interleaving)
 constexpr int kBsDefaultVariant8 = 1, kBsDefaultVariant16 = 0;
 
-// ----------------------------------------------------------- constexpr GF
-// GF(2^8), generating polynomial 0x11D (build.rs:11), log/exp built the way
-// build.rs:27-48 does; GF(2^16) per galois_16.rs:146-162 (x^2 = 2x + 128).
-struct Gf8Tables {
-  uint8_t log[256] = {};
-  uint8_t exp[512] = {};
-  constexpr Gf8Tables() {
-    uint32_t b = 1;
-    for (int l = 0; l < 255; ++l) {
-      log[b] = (uint8_t)l;
-      exp[l] = exp[l + 255] = (uint8_t)b;
-      b <<= 1;
-      if (b & 0x100u) b ^= 0x11Du;
-    }
-  }
-};
-constexpr Gf8Tables kGf8{};
-
-constexpr uint8_t cmul8(uint8_t a, uint8_t b) {
-  return (a && b) ? kGf8.exp[kGf8.log[a] + kGf8.log[b]] : 0;
-}
-constexpr uint16_t cmul16(uint16_t a, uint16_t b) {
-  const uint8_t a1 = a >> 8, a0 = a & 0xFF, b1 = b >> 8, b0 = b & 0xFF;
-  const uint8_t hh = cmul8(a1, b1);
-  const uint8_t x = cmul8(a1, b0) ^ cmul8(a0, b1) ^ cmul8(2, hh);
-  const uint8_t c = cmul8(a0, b0) ^ cmul8(128, hh);
-  return (uint16_t)((x << 8) | c);
-}
-constexpr uint16_t cpow16(uint16_t a, uint32_t n) {  // galois_16.rs:80-93
-  if (n == 0) return 1;
-  if (a == 0) return 0;
-  n %= 65535u;
-  if (n == 0) return 1;
-  uint16_t r = 1, b = a;
-  while (n) {
-    if (n & 1) r = cmul16(r, b);
-    b = cmul16(b, b);
-    n >>= 1;
-  }
-  return r;
-}
-constexpr uint16_t cinv16(uint16_t a) { return cpow16(a, 65534u); }
-
-constexpr uint8_t cexp8(uint8_t a, uint32_t n) {  // galois_8.rs:87-103
-  if (n == 0) return 1;
-  if (a == 0) return 0;
-  return kGf8.exp[(kGf8.log[a] * n) % 255];
-}
-
-// Field policies for the constexpr matrix code.
-struct CF8 : BitsF8 {
-  static constexpr uint16_t mul(uint16_t a, uint16_t b) { return cmul8((uint8_t)a, (uint8_t)b); }
-  static constexpr uint16_t pow(uint16_t a, uint32_t n) { return cexp8((uint8_t)a, n); }
-  static constexpr uint16_t inv(uint16_t a) { return kGf8.exp[255 - kGf8.log[a]]; }
-};
-struct CF16 : BitsF16 {
-  static constexpr uint16_t mul(uint16_t a, uint16_t b) { return cmul16(a, b); }
-  static constexpr uint16_t pow(uint16_t a, uint32_t n) { return cpow16(a, n); }
-  static constexpr uint16_t inv(uint16_t a) { return cinv16(a); }
-};
-
-// Parity rows of the (K + P) x K encoding matrix V * (V[0..K])^-1 with
-// V[r][c] = r^c (matrix.rs:263-276, core.rs:430-436).  The inverse is unique,
-// so Gauss-Jordan here gives the same matrix as matrix.rs:195-261.
-template <class F, int K, int P>
-struct Parity {
-  uint16_t m[P][K] = {};
-  constexpr Parity() {
-    uint16_t w[K][2 * K] = {};
-    for (int r = 0; r < K; ++r) {
-      for (int c = 0; c < K; ++c) w[r][c] = F::pow((uint16_t)r, (uint32_t)c);
-      w[r][K + r] = 1;
-    }
-    for (int col = 0; col < K; ++col) {
-      int piv = col;
-      while (w[piv][col] == 0) ++piv;
-      if (piv != col)
-        for (int c = 0; c < 2 * K; ++c) {
-          const uint16_t t = w[col][c];
-          w[col][c] = w[piv][c];
-          w[piv][c] = t;
-        }
-      const uint16_t s = F::inv(w[col][col]);
-      for (int c = 0; c < 2 * K; ++c) w[col][c] = F::mul(s, w[col][c]);
-      for (int r = 0; r < K; ++r) {
-        const uint16_t f = w[r][col];
-        if (r == col || f == 0) continue;
-        for (int c = 0; c < 2 * K; ++c) w[r][c] ^= F::mul(f, w[col][c]);
-      }
-    }
-    for (int o = 0; o < P; ++o)
-      for (int i = 0; i < K; ++i) {
-        uint16_t v = 0;
-        for (int j = 0; j < K; ++j) v ^= F::mul(F::pow((uint16_t)(K + o), (uint32_t)j), w[j][K + i]);
-        m[o][i] = v;
-      }
-  }
-};
-
-// sel[o][i][p] = the input planes whose XOR is output plane p of the product
-// by coefficient (o, i): column q of the bit matrix is c * (element with only
-// plane q's bit set).
-template <class F, int K, int P, bool CSE = true>
-struct Planes {
-  // GF(2^16): an input's p x 16 output planes share one group of 16 sources,
-  // so common pairs become per-input temporaries (rse_jit.cpp:
-  // eliminate_common_pairs, the same greedy rule); GF(2^8) networks are small
-  static constexpr int kTemps = (CSE && F::kPlanes == 16) ? 16 : 0;
-  Parity<F, K, P> par{};
-  uint32_t sel[P][K][F::kPlanes] = {};
-  uint8_t ntmp[K] = {};
-  uint8_t tmp[K][kTemps > 0 ? kTemps : 1][2] = {};
-  constexpr Planes() {
-    for (int o = 0; o < P; ++o)
-      for (int i = 0; i < K; ++i)
-        for (int q = 0; q < F::kPlanes; ++q) {
-          const uint16_t col = F::mul(par.m[o][i], (uint16_t)(1u << F::bit(q)));
-          for (int p = 0; p < F::kPlanes; ++p)
-            if ((col >> F::bit(p)) & 1u) sel[o][i][p] |= 1u << q;
-        }
-    for (int i = 0; i < K && kTemps > 0; ++i) {
-      int n = 0;
-      while (n < kTemps) {
-        // pair counts over the rows' set bits: cnt[a][b], a < b < 16 + n
-        uint16_t cnt[32][32] = {};
-        for (int o = 0; o < P; ++o)
-          for (int q = 0; q < F::kPlanes; ++q)
-            for (uint32_t m = sel[o][i][q]; m; m &= m - 1) {
-              const int a = __builtin_ctz(m);
-              for (uint32_t r = m & (m - 1); r; r &= r - 1) ++cnt[a][__builtin_ctz(r)];
-            }
-        int best = 0, ba = 0, bb = 0;
-        for (int a = 0; a < 16 + n; ++a)
-          for (int b = a + 1; b < 16 + n; ++b)
-            if (cnt[a][b] > best) {
-              best = cnt[a][b];
-              ba = a;
-              bb = b;
-            }
-        if (best < 3) break;
-        const uint32_t pm = (1u << ba) | (1u << bb);
-        for (int o = 0; o < P; ++o)
-          for (int q = 0; q < F::kPlanes; ++q)
-            if ((sel[o][i][q] & pm) == pm) sel[o][i][q] = (sel[o][i][q] & ~pm) | (1u << (16 + n));
-        tmp[i][n][0] = (uint8_t)ba;
-        tmp[i][n][1] = (uint8_t)bb;
-        ++n;
-      }
-      ntmp[i] = (uint8_t)n;
-    }
-  }
-};
-
-// A compiled codec: NP planes per group, NG groups per lane-chunk (16 dwords).
-// CSE = false: the plain networks (kernel variant 9, for A/B).
-template <class F, int K, int P, bool CSE = true>
-struct Code {
-  using Field = F;
-  static constexpr int k = K, p = P;
-  static constexpr int NP = F::kPlanes, NG = 16 / F::kPlanes;
-  static constexpr int kTemps = Planes<F, K, P, CSE>::kTemps;
-  static constexpr int kGTemps = 0;  // GF(2^8) group temporaries: run-time specialised wide codecs
-  static constexpr Planes<F, K, P, CSE> planes{};
-};
+// ------------------------------------------------------- compiled codecs
+// The code structs of the compiled codecs -- their parity rows (core.rs:430-436,
+// V * (V[0..K])^-1) and the XOR networks of those rows -- generated at build time
+// by rse_gen_tables.cpp with the generator the run-time specialisation uses
+// (rse_netgen.hpp): Bs8_10_4, Bs8_10_2, Bs16_20_8, and *Plain twins without
+// shared subexpressions (kernel variant 9, for A/B).
+#include "rse_bs_tables.inc"
 
 template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
@@ -493,31 +336,28 @@ constexpr BsDescFn rec_desc_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_desc_kernel<C, true, NS>;
   else return nullptr;
 }
-#define BS(F, FIELD, K, P)                                                      \
-  {FIELD, K, P, &Code<F, K, P>::planes.par.m[0][0],                             \
-   {{bitslice_kernel<Code<F, K, P>, false, false, false>,                        \
-     bitslice_kernel<Code<F, K, P>, true, false, false>},                         \
-    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false>},                 \
-    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, true>},                  \
-    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 3>},                             \
-    {nullptr, bitslice_dma_kernel<Code<F, K, P>, 2>},                             \
-    {nullptr, bitslice_deep_kernel<Code<F, K, P>, 2>},                            \
-    {nullptr, bitslice_deep_kernel<Code<F, K, P>, 3>},                            \
-    {nullptr, bitslice_kernel<Code<F, K, P>, true, true, false, true>},           \
-    {bitslice_kernel<Code<F, K, P>, false, true, false, false, true>,             \
-     bitslice_kernel<Code<F, K, P>, true, true, false, false, true>},             \
-    {nullptr, bitslice_kernel<Code<F, K, P, false>, true, true, false>}},         \
-   bitslice_kernel<Code<F, K, P>, true, true, false, false, false, true>,          \
-   {rec_fn<Code<F, K, P>, 1>(), rec_fn<Code<F, K, P>, 2>(), rec_fn<Code<F, K, P>, 4>(),  \
-    rec_fn<Code<F, K, P>, 8>()},                                                   \
-   {rec_fn<Code<F, K, P>, 1, false>(), rec_fn<Code<F, K, P>, 2, false>(),          \
-    rec_fn<Code<F, K, P>, 4, false>(), rec_fn<Code<F, K, P>, 8, false>()},          \
-   {rec_desc_fn<Code<F, K, P>, 1>(), rec_desc_fn<Code<F, K, P>, 2>(),             \
-    rec_desc_fn<Code<F, K, P>, 4>(), rec_desc_fn<Code<F, K, P>, 8>()}}
+#define BS(C, CP, FIELD)                                                          \
+  {FIELD, C::k, C::p, &C::rows[0][0],                                             \
+   {{bitslice_kernel<C, false, false, false>, bitslice_kernel<C, true, false, false>}, \
+    {nullptr, bitslice_kernel<C, true, true, false>},                              \
+    {nullptr, bitslice_kernel<C, true, true, true>},                               \
+    {nullptr, bitslice_dma_kernel<C, 3>},                                          \
+    {nullptr, bitslice_dma_kernel<C, 2>},                                          \
+    {nullptr, bitslice_deep_kernel<C, 2>},                                         \
+    {nullptr, bitslice_deep_kernel<C, 3>},                                         \
+    {nullptr, bitslice_kernel<C, true, true, false, true>},                        \
+    {bitslice_kernel<C, false, true, false, false, true>,                          \
+     bitslice_kernel<C, true, true, false, false, true>},                          \
+    {nullptr, bitslice_kernel<CP, true, true, false>}},                            \
+   bitslice_kernel<C, true, true, false, false, false, true>,                      \
+   {rec_fn<C, 1>(), rec_fn<C, 2>(), rec_fn<C, 4>(), rec_fn<C, 8>()},              \
+   {rec_fn<C, 1, false>(), rec_fn<C, 2, false>(), rec_fn<C, 4, false>(),          \
+    rec_fn<C, 8, false>()},                                                        \
+   {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()}}
 static const BsShape kBsShapes[] = {
-    BS(CF8, 8, 10, 4),    // BASELINE headline: galois_8 10+4
-    BS(CF8, 8, 10, 2),    // benches/bandwidth.rs 10+2
-    BS(CF16, 16, 20, 8),  // BASELINE configs[4]: galois_16 20+8
+    BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
+    BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
+    BS(Bs16_20_8, Bs16_20_8Plain, 16),  // BASELINE configs[4]: galois_16 20+8
 };
 #undef BS
 

@@ -11,12 +11,14 @@
 // v_perm in the network.  A codec type C supplies the matrices as constants:
 //   using Field = BitsF8 | BitsF16 (planes per group and their bit order);
 //   static constexpr int k, p, NP, kTemps;
-//   static constexpr ... planes.sel[o][i][q]: bit j set iff source j
-//     contributes to output plane q of coefficient (o, i).  Sources 0..15 are
-//     the input's planes; with kTemps > 0, sources 16 + t are common
-//     subexpressions of that input's network, planes.tmp[i][t] = {a, b}:
-//     source a ^ source b, t < planes.ntmp[i] (computed once per input,
-//     shared by every output plane that uses them).
+//   static constexpr ... planes.sel[o][i][q] (uint64_t): bit j set iff
+//     source j contributes to output plane q of coefficient (o, i).  Sources
+//     0..NP-1 are the input's planes (of one group); with kTemps (GF(2^16))
+//     or kGTemps (GF(2^8), per group) > 0, sources NP + t are shared
+//     subexpressions of that input's network, planes.tmp[i][t] = {a, b, c}:
+//     the XOR of sources a, b (and c unless 255), t < planes.ntmp[i]
+//     (computed once per input, shared by every output plane that uses them).
+//   All of it is generated on the host by rse_netgen.hpp.
 //
 // Lane layout: a workgroup of 256 lanes codes a 16 KiB chunk of every shard.
 // Lane t loads the 16-byte vectors t, t+256, t+512, t+768 of the chunk (each
@@ -57,30 +59,39 @@ struct BitsF16 {
 };
 
 // ------------------------------------------------------------ bit slicing
-// XOR of acc and the planes selected by M, two at a time.
-template <uint32_t M>
+// XOR of acc and the sources selected by M (bit j: source j -- an input
+// plane or a shared temporary, rse_netgen.hpp), two at a time.
+template <uint64_t M>
 __device__ __forceinline__ uint32_t xacc(uint32_t acc, const uint32_t* in) {
   if constexpr (M == 0) {
     return acc;
   } else {
-    constexpr int q0 = __builtin_ctz(M);
-    constexpr uint32_t m1 = M & (M - 1);
+    constexpr int q0 = __builtin_ctzll(M);
+    constexpr uint64_t m1 = M & (M - 1);
     if constexpr (m1 == 0) {
       return acc ^ in[q0];
     } else {
-      constexpr int q1 = __builtin_ctz(m1);
+      constexpr int q1 = __builtin_ctzll(m1);
       return xacc<m1 & (m1 - 1)>(xor3(acc, in[q0], in[q1]), in);
     }
   }
 }
-template <uint32_t M>
+template <uint64_t M>
 __device__ __forceinline__ uint32_t xinit(const uint32_t* in) {
   if constexpr (M == 0) {
     return 0u;
   } else {
-    constexpr int q0 = __builtin_ctz(M);
+    constexpr int q0 = __builtin_ctzll(M);
     return xacc<M & (M - 1)>(in[q0], in);
   }
+}
+
+// Shared temporary t of input I (rse_netgen.hpp): the XOR of two or three of
+// the input's earlier sources, one v_bitop3.
+template <class C, int I>
+__device__ __forceinline__ uint32_t temp_source(const uint32_t* src, int t) {
+  const int a = C::planes.tmp[I][t][0], b = C::planes.tmp[I][t][1], c = C::planes.tmp[I][t][2];
+  return c == 255 ? src[a] ^ src[b] : xor3(src[a], src[b], src[c == 255 ? 0 : c]);
 }
 
 // 8x8 bit transpose inside every byte lane of h[0..7] (an involution): bit b
@@ -186,7 +197,7 @@ __device__ __forceinline__ void mac_group(uint32_t (&acc)[N], const uint32_t (&p
   for (int q = 0; q < 8; ++q) src[q] = pl[G * 8 + q];
 #pragma unroll
   for (int t = 0; t < C::kGTemps; ++t)
-    if (t < C::planes.ntmp[I]) src[8 + t] = src[C::planes.tmp[I][t][0]] ^ src[C::planes.tmp[I][t][1]];
+    if (t < C::planes.ntmp[I]) src[8 + t] = temp_source<C, I>(src, t);
   // OP runs over outputs; plane q of group G of output o is acc[o * 16 + G * 8 + q]
   if constexpr (I == 0 && !ACC)
     ((acc[(OP / 8) * 16 + G * 8 + OP % 8] = xinit<C::planes.sel[OP / 8][I][OP % 8]>(src)), ...);
@@ -211,8 +222,7 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
   if constexpr (C::kTemps > 0) {
 #pragma unroll
     for (int t = 0; t < C::kTemps; ++t)
-      if (t < C::planes.ntmp[I])
-        in[16 + t] = in[C::planes.tmp[I][t][0]] ^ in[C::planes.tmp[I][t][1]];
+      if (t < C::planes.ntmp[I]) in[16 + t] = temp_source<C, I>(in, t);
   }
   if constexpr (I == 0 && !ACC)
     ((acc[OP] = xinit<C::planes.sel[OP / 16][I][OP % C::NP]>(in + (OP % 16) / C::NP * C::NP)),

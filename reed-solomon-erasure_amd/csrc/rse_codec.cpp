@@ -827,6 +827,7 @@ struct HostStripe {
   void* const* sh;         // the stripe's k + p host shards (kCode: inputs, then outputs)
   void* const* buf;        // kVerifyBuf: its p host buffer shards
   const uint8_t* present;  // kRecon*: its k + p presence flags
+  bool flat = false;       // shards are parts of ONE caller buffer (the *_flat entries)
 };
 
 // Shards one stripe's operation reads (up) and writes (down); index total + r
@@ -871,17 +872,19 @@ void host_sets(uint32_t k, uint32_t T, uint32_t p, HostOp op, bool accumulate,
 }
 
 // Copies bytes [off, off + sz) of the listed shards between the host and the
-// ring slot `dset` (shard i at dset + i * chunk): one 2D copy per run of
-// consecutive indices whose host shards are equally spaced (flat stripes),
-// one plain copy otherwise.
+// ring slot `dset` (shard i at dset + i * chunk).  Shards of one caller
+// buffer (flat): one 2D copy per run of consecutive indices whose shards are
+// equally spaced; otherwise one plain copy per shard (a 2D copy must stay
+// inside one host allocation: separate allocations that happen to be equally
+// spaced are not one buffer).
 template <class HostPtr>
 hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<uint32_t>& idx,
-                       HostPtr host, size_t off, size_t sz, hipStream_t s) {
+                       HostPtr host, size_t off, size_t sz, bool flat, hipStream_t s) {
   hipError_t e = hipSuccess;
   for (size_t a = 0; a < idx.size() && e == hipSuccess;) {
     size_t b = a + 1;
     ptrdiff_t pitch = 0;
-    if (b < idx.size() && idx[b] == idx[a] + 1) pitch = host(idx[b]) - host(idx[a]);
+    if (flat && b < idx.size() && idx[b] == idx[a] + 1) pitch = host(idx[b]) - host(idx[a]);
     if (pitch > 0 && (size_t)pitch >= sz)
       while (b < idx.size() && idx[b] == idx[b - 1] + 1 && host(idx[b]) - host(idx[b - 1]) == pitch)
         ++b;
@@ -975,7 +978,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
       return static_cast<uint8_t*>(i < T ? hs.sh[i] : hs.buf[i - T]);
     };
     if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);  // slot drained
-    if (e == hipSuccess) e = copy_shards(true, set, chunk, up, host, off, sz, hst);
+    if (e == hipSuccess) e = copy_shards(true, set, chunk, up, host, off, sz, hs.flat, hst);
     if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
     if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
     if (e != hipSuccess) break;
@@ -1006,7 +1009,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
     if (rc) break;
     e = hipEventRecord(coded[b], kst);
     if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
-    if (e == hipSuccess) e = copy_shards(false, set, chunk, down, host, off, sz, dst);
+    if (e == hipSuccess) e = copy_shards(false, set, chunk, down, host, off, sz, hs.flat, dst);
     if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
   }
   // join: the caller's stream waits for every stream, frees the ring, syncs
@@ -1540,7 +1543,7 @@ int rse_encode_host_flat(const rse_codec* c, void* stripes, size_t shard_len, si
   const size_t sb = shard_len * c->esize();
   const std::vector<void*> ptrs = flat_ptrs(c, stripes, sb, n_stripes);
   std::vector<HostStripe> list(n_stripes);
-  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr};
+  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr, true};
   return host_pipeline(c, HostOp::kEncode, list, sb, (hipStream_t)stream, nullptr);
 }
 
@@ -1580,7 +1583,7 @@ int rse_verify_host_flat(const rse_codec* c, const void* stripes, size_t shard_l
   const size_t sb = shard_len * c->esize();
   const std::vector<void*> ptrs = flat_ptrs(c, const_cast<void*>(stripes), sb, n_stripes);
   std::vector<HostStripe> list(n_stripes);
-  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr};
+  for (size_t s = 0; s < n_stripes; ++s) list[s] = HostStripe{&ptrs[s * c->total], nullptr, nullptr, true};
   std::vector<int> res(n_stripes, 0);
   const int rc = host_pipeline(c, HostOp::kVerify, list, sb, (hipStream_t)stream, res.data());
   if (rc == RSE_OK)
@@ -1629,7 +1632,7 @@ int rse_reconstruct_host_batch(const rse_codec* c, void* stripes, size_t shard_l
   const std::vector<void*> ptrs = flat_ptrs(c, stripes, sb, n_stripes);
   std::vector<HostStripe> list(n_stripes);
   for (size_t s = 0; s < n_stripes; ++s)
-    list[s] = HostStripe{&ptrs[s * T], nullptr, present + s * T};
+    list[s] = HostStripe{&ptrs[s * T], nullptr, present + s * T, true};
   return host_pipeline(c, data_only ? HostOp::kReconData : HostOp::kRecon, list, sb,
                        (hipStream_t)stream, nullptr);
 }

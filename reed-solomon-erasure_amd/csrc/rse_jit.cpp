@@ -45,6 +45,7 @@
 #include "../../include/rse_hip.h"
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
+#include "rse_netgen.hpp"
 
 extern char** environ;
 
@@ -153,119 +154,14 @@ int recon_ns(uint32_t p, int* ns) {
   return n;
 }
 
-// Greedy common-subexpression elimination over one input's XOR network.
-// rows: the source mask of every output plane (bit j: source j; the first
-// `planes` sources are the input's planes).  Repeatedly the pair of sources
-// that occurs together in the most rows (at least 3: a temporary costs one
-// v_bitop3 and saves about half of one per row that uses it, the rows
-// absorbing two sources per op) becomes a new source planes + t, up to
-// `budget` temporaries.
-struct Cse {
-  int n = 0;
-  uint8_t tmp[16][2] = {};
-};
-Cse eliminate_common_pairs(std::vector<uint32_t>& rows, int budget, int planes) {
-  Cse c;
-  while (c.n < budget && c.n < 16) {
-    const int ns = planes + c.n;
-    int best = 0, ba = -1, bb = -1;
-    for (int a = 0; a < ns; ++a)
-      for (int b = a + 1; b < ns; ++b) {
-        const uint32_t m = (1u << a) | (1u << b);
-        int cnt = 0;
-        for (uint32_t r : rows) cnt += (r & m) == m;
-        if (cnt > best) {
-          best = cnt;
-          ba = a;
-          bb = b;
-        }
-      }
-    if (best < 3) break;
-    const uint32_t m = (1u << ba) | (1u << bb);
-    for (uint32_t& r : rows)
-      if ((r & m) == m) r = (r & ~m) | (1u << ns);
-    c.tmp[c.n][0] = (uint8_t)ba;
-    c.tmp[c.n][1] = (uint8_t)bb;
-    ++c.n;
-  }
-  return c;
-}
-
-// Appends the plane-selection table and code struct `name` of p x k rows:
-// sel[o][i][q] has bit j set iff input source j feeds output plane q -- column
-// j of the bit matrix of rows[o][i] is rows[o][i] * (the element with only
-// plane j's bit set).  GF(2^16): one 16-plane group per input, `budget`
-// shared temporaries per input (kTemps).  GF(2^8): two 8-plane groups that
-// share their bit matrices, `gbudget` temporaries per input computed per
-// group (kGTemps; wide codecs, where an input feeds many outputs).
+// The code struct `name` of p x k rows (rse_netgen.hpp), inside the
+// kernels' namespace.
 void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t p,
-               const std::vector<uint16_t>& rows, int budget, int gbudget) {
-  const int np = field == 16 ? 16 : 8;
-  auto bit = [&](int q) { return field == 16 ? (q ^ 8) : q; };
-  auto mul = [&](uint16_t a, uint16_t b) {
-    return field == 16 ? Gf16Field::mul(a, b) : Gf8Field::mul(a, b);
-  };
-  if (field == 16) gbudget = 0;
-  else budget = 0;
-  std::vector<uint32_t> sel((size_t)p * k * np, 0);
-  auto at = [&](uint32_t o, uint32_t i, int q) -> uint32_t& { return sel[((size_t)o * k + i) * np + q]; };
-  for (uint32_t o = 0; o < p; ++o)
-    for (uint32_t i = 0; i < k; ++i)
-      for (int j = 0; j < np; ++j) {
-        const uint16_t col = mul(rows[o * k + i], (uint16_t)(1u << bit(j)));
-        for (int q = 0; q < np; ++q)
-          if ((col >> bit(q)) & 1u) at(o, i, q) |= 1u << j;
-      }
-  const int nt = budget > 0 ? budget : gbudget;
-  std::vector<Cse> cse(k);
-  if (nt > 0)
-    for (uint32_t i = 0; i < k; ++i) {
-      std::vector<uint32_t> r;
-      for (uint32_t o = 0; o < p; ++o)
-        for (int q = 0; q < np; ++q) r.push_back(at(o, i, q));
-      cse[i] = eliminate_common_pairs(r, nt, np);
-      size_t n = 0;
-      for (uint32_t o = 0; o < p; ++o)
-        for (int q = 0; q < np; ++q) at(o, i, q) = r[n++];
-    }
-  char buf[640];
-  std::snprintf(buf, sizeof buf,
-                "\nnamespace rse {\nnamespace {\n"
-                "struct %sPlanes {\n  uint32_t sel[%u][%u][%d];\n  uint8_t ntmp[%u];\n"
-                "  uint8_t tmp[%u][%d][2];\n};\n"
-                "struct %s {\n  using Field = %s;\n"
-                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d, kGTemps = %d;\n"
-                "  static constexpr %sPlanes planes = {{",
-                name, p, k, np, k, k, nt > 0 ? nt : 1, name, field == 16 ? "BitsF16" : "BitsF8",
-                k, p, np, 16 / np, budget > 0 ? budget : 0, gbudget > 0 ? gbudget : 0, name);
-  s += buf;
-  for (uint32_t o = 0; o < p; ++o) {
-    s += "{";
-    for (uint32_t i = 0; i < k; ++i) {
-      s += "{";
-      for (int q = 0; q < np; ++q) {
-        std::snprintf(buf, sizeof buf, "%uu,", (unsigned)at(o, i, q));
-        s += buf;
-      }
-      s += "},";
-    }
-    s += "},";
-  }
-  s += "}, {";
-  for (uint32_t i = 0; i < k; ++i) {
-    std::snprintf(buf, sizeof buf, "%d,", cse[i].n);
-    s += buf;
-  }
-  s += "}, {";
-  for (uint32_t i = 0; i < k; ++i) {
-    s += "{";
-    for (int t = 0; t < (nt > 0 ? nt : 1); ++t) {
-      std::snprintf(buf, sizeof buf, "{%d,%d},", cse[i].tmp[t][0], cse[i].tmp[t][1]);
-      s += buf;
-    }
-    s += "},";
-  }
-  s += "}};\n};\n}  // namespace\n}  // namespace rse\n";
+               const std::vector<uint16_t>& rows, int temps) {
+  const netgen::Net net = netgen::build(field, k, p, rows.data(), temps);
+  s += "\nnamespace rse {\nnamespace {\n";
+  s += netgen::emit(net, name, rows.data());
+  s += "}  // namespace\n}  // namespace rse\n";
 }
 
 // A wide codec's outputs split over the waves of one workgroup: W = ceil(p/8)
@@ -293,14 +189,15 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   if (kind == kJitWide) {
     // one code struct per wave's share of the outputs, and the kernel
     const int W = wide_waves(p);
-    const int gbudget = 16;
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, w, &o0, &n);
       std::vector<uint16_t> sub(rows.begin() + (size_t)o0 * k, rows.begin() + (size_t)(o0 + n) * k);
       char name[32];
       std::snprintf(name, sizeof name, "JitWide%d", w);
-      emit_code(s, name, field, k, n, sub, (int)get_option(13), gbudget);
+      // an input feeds many outputs here: shared temporaries in both fields
+      // (GF(2^8): per input, computed per plane group)
+      emit_code(s, name, field, k, n, sub, field == 16 ? (int)get_option(13) : 16);
     }
     char buf[512];
     std::snprintf(buf, sizeof buf,
@@ -330,7 +227,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     s += "    default: break;\n  }\n}\n";
     return s;
   }
-  emit_code(s, "JitCode", field, k, p, rows, field == 16 ? (int)get_option(13) : 0, 0);
+  emit_code(s, "JitCode", field, k, p, rows, field == 16 ? (int)get_option(13) : 0);
   char buf[512];
   if (stage == kEnc) {
     // encode/verify kernels (16 KiB and 4 KiB chunks); a later block of a wide

@@ -757,7 +757,7 @@ struct Options {
   int64_t host_h2d_streams = 2;   // host pipeline H2D streams (tools/host_e2e.py)
   int64_t jit = 1;                // run-time specialised bit-sliced kernels (rse_jit.cpp)
   int64_t jit_patterns = 1;       // ... also for repeated decode patterns
-  int64_t jit_cse = 16;           // GF(2^16) specialised networks: temporaries per input
+  int64_t jit_cse = 32;           // GF(2^16) specialised networks: temporaries per input
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
   int64_t recon_mix = 1;          // syndrome reconstruct: bit-sliced mixing (0: v_perm tables)
@@ -1096,7 +1096,7 @@ int set_option(int key, int64_t value) {
     case 8: g_opt.host_h2d_streams = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 9: g_opt.jit = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case 11: g_opt.jit_patterns = value ? 1 : 0; return 0;
-    case 13: g_opt.jit_cse = value < 0 ? 0 : value > 16 ? 16 : value; return 0;
+    case 13: g_opt.jit_cse = value < 0 ? 0 : value > 32 ? 32 : value; return 0;
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
     case 17: g_opt.recon_mix = value ? 1 : 0; return 0;

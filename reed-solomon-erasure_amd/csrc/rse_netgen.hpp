@@ -1,0 +1,204 @@
+// rse_netgen.hpp -- host-side generator of the bit-sliced XOR networks.
+//
+// Multiplying by a constant c is GF(2)-linear: an 8x8 (GF(2^8)) or 16x16
+// (GF(2^16)) bit matrix.  With the data bit-sliced (rse_bitslice_core.hpp), the
+// contribution of input i to output plane q of output o is the XOR of the input
+// planes that row q of the bit matrix of coefficient (o, i) selects: the mask
+// sel[o][i][q] (bit j = source j).  All outputs' rows of one input draw on the
+// same sources, so shared subexpressions are factored out first: temporaries
+// t = a ^ b or a ^ b ^ c of the input's sources (one v_bitop3 each, computed
+// once per input and chunk) that become new sources.
+//
+// Cost model: an output plane with w sources costs ceil(w / 2) v_bitop3
+// (acc ^ x ^ y), so replacing a pair by a temporary saves one op in exactly
+// the rows of odd weight that contain it, and replacing a triple saves one op
+// in every row that contains it.  The generator greedily adds the temporary
+// with the largest net saving (rows saved - 1 for the temporary), pairs and
+// triples alike, until none saves anything or the budget is used.  For
+// GF(2^16) 20+8 this takes the network from 5816 v_bitop3 (no temporaries)
+// past 4224 (pairs by row count, 16 temporaries; round 1) to ~3600 (32).
+//
+// Used by rse_jit.cpp for the codecs specialised at run time and by
+// rse_gen_tables.cpp, at build time, for the codecs compiled into
+// rse_bitslice.hip -- one generator, one table format, one set of kernels.
+#pragma once
+
+#include <stdint.h>
+
+#include <array>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "rse_field.hpp"
+
+namespace rse {
+namespace netgen {
+
+constexpr int kMaxTemps = 32;  // sources per mask: planes (<= 16) + temporaries <= 48 < 64
+
+struct Net {
+  int field = 8;
+  int np = 8;  // planes per group: 8 (GF(2^8), two groups per 16 dwords) or 16
+  uint32_t k = 0, p = 0;
+  int temps = 0;                                  // budget per input
+  std::vector<uint64_t> sel;                      // [o][i][q]
+  std::vector<uint8_t> ntmp;                      // [i]
+  std::vector<std::array<uint8_t, 3>> tmp;        // [i][t]: sources {a, b, c}; c = 255: a pair
+  uint64_t& at(uint32_t o, uint32_t i, int q) { return sel[((size_t)o * k + i) * np + q]; }
+  uint64_t at(uint32_t o, uint32_t i, int q) const { return sel[((size_t)o * k + i) * np + q]; }
+  // v_bitop3 count of one chunk's network (the cost model above)
+  size_t ops() const {
+    size_t n = 0;
+    for (uint32_t i = 0; i < k; ++i) n += ntmp[i];
+    for (uint64_t m : sel) n += ((size_t)__builtin_popcountll(m) + 1) / 2;
+    return n;
+  }
+};
+
+inline int popc(uint64_t m) { return __builtin_popcountll(m); }
+
+// Greedy temporaries over one input's rows (see above); returns the count and
+// fills tmp.  planes = the input's own sources (np).
+inline int factor(std::vector<uint64_t>& rows, int budget, int planes,
+                  std::array<uint8_t, 3>* tmp) {
+  int n = 0;
+  std::vector<int> c2, c3;
+  while (n < budget && n < kMaxTemps) {
+    const int ns = planes + n;
+    c2.assign((size_t)ns * ns, 0);
+    c3.assign((size_t)ns * ns * ns, 0);
+    int src[64];
+    for (uint64_t r : rows) {
+      int w = 0;
+      for (uint64_t m = r; m; m &= m - 1) src[w++] = __builtin_ctzll(m);
+      for (int x = 0; x < w; ++x)
+        for (int y = x + 1; y < w; ++y) {
+          if (w & 1) ++c2[(size_t)src[x] * ns + src[y]];
+          for (int z = y + 1; z < w; ++z) ++c3[((size_t)src[x] * ns + src[y]) * ns + src[z]];
+        }
+    }
+    int best = 0, ba = -1, bb = -1, bc = -1;
+    for (int a = 0; a < ns; ++a)
+      for (int b = a + 1; b < ns; ++b) {
+        if (c2[(size_t)a * ns + b] - 1 > best) {
+          best = c2[(size_t)a * ns + b] - 1;
+          ba = a, bb = b, bc = -1;
+        }
+        for (int c = b + 1; c < ns; ++c)
+          if (c3[((size_t)a * ns + b) * ns + c] - 1 > best) {
+            best = c3[((size_t)a * ns + b) * ns + c] - 1;
+            ba = a, bb = b, bc = c;
+          }
+      }
+    if (best <= 0) break;
+    const uint64_t m = (1ull << ba) | (1ull << bb) | (bc >= 0 ? 1ull << bc : 0ull);
+    for (uint64_t& r : rows)
+      if ((r & m) == m) r = (r & ~m) | (1ull << ns);
+    tmp[n] = {(uint8_t)ba, (uint8_t)bb, (uint8_t)(bc >= 0 ? bc : 255)};
+    ++n;
+  }
+  return n;
+}
+
+// The network of p x k rows (row-major, uint16 elements as in rse_field.hpp).
+// budget: temporaries per input (GF(2^8): per input, shared by its two plane
+// groups, which use the same bit matrices).
+inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int budget) {
+  Net net;
+  net.field = field;
+  net.np = field == 16 ? 16 : 8;
+  net.k = k;
+  net.p = p;
+  net.temps = budget < 0 ? 0 : budget > kMaxTemps ? kMaxTemps : budget;
+  net.sel.assign((size_t)p * k * net.np, 0);
+  net.ntmp.assign(k, 0);
+  net.tmp.assign((size_t)k * (net.temps > 0 ? net.temps : 1), {0, 0, 255});
+  const int np = net.np;
+  // GF(2^16) plane q < 8 is bit q of the coefficient-of-x byte (uint16 bit
+  // q + 8), q >= 8 bit q - 8 of the constant byte (rse_bitslice_core.hpp BitsF16)
+  auto bit = [&](int q) { return field == 16 ? (q ^ 8) : q; };
+  auto mul = [&](uint16_t a, uint16_t b) {
+    return field == 16 ? Gf16Field::mul(a, b) : Gf8Field::mul(a, b);
+  };
+  for (uint32_t o = 0; o < p; ++o)
+    for (uint32_t i = 0; i < k; ++i)
+      for (int j = 0; j < np; ++j) {
+        const uint16_t col = mul(rows[(size_t)o * k + i], (uint16_t)(1u << bit(j)));
+        for (int q = 0; q < np; ++q)
+          if ((col >> bit(q)) & 1u) net.at(o, i, q) |= 1ull << j;
+      }
+  if (net.temps > 0)
+    for (uint32_t i = 0; i < k; ++i) {
+      std::vector<uint64_t> r;
+      for (uint32_t o = 0; o < p; ++o)
+        for (int q = 0; q < np; ++q) r.push_back(net.at(o, i, q));
+      net.ntmp[i] = (uint8_t)factor(r, net.temps, np, &net.tmp[(size_t)i * net.temps]);
+      size_t n = 0;
+      for (uint32_t o = 0; o < p; ++o)
+        for (int q = 0; q < np; ++q) net.at(o, i, q) = r[n++];
+    }
+  return net;
+}
+
+// C++ source of code struct `name` for rse_bitslice_core.hpp:
+//   using Field; k, p, NP, NG, kTemps (GF(2^16) per-input temporaries),
+//   kGTemps (GF(2^8) per-group temporaries); planes.sel / ntmp / tmp; rows.
+inline std::string emit(const Net& net, const char* name, const uint16_t* rows) {
+  std::string s;
+  const int nt = net.temps > 0 ? net.temps : 1;
+  char buf[768];
+  std::snprintf(buf, sizeof buf,
+                "struct %sPlanes {\n  uint64_t sel[%u][%u][%d];\n  uint8_t ntmp[%u];\n"
+                "  uint8_t tmp[%u][%d][3];\n};\n"
+                "struct %s {\n  using Field = %s;\n"
+                "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d, "
+                "kGTemps = %d;\n"
+                "  static constexpr uint16_t rows[%u][%u] = {",
+                name, net.p, net.k, net.np, net.k, net.k, nt, name,
+                net.field == 16 ? "BitsF16" : "BitsF8", net.k, net.p, net.np, 16 / net.np,
+                net.field == 16 ? net.temps : 0, net.field == 16 ? 0 : net.temps, net.p, net.k);
+  s += buf;
+  for (uint32_t o = 0; o < net.p; ++o) {
+    s += "{";
+    for (uint32_t i = 0; i < net.k; ++i) {
+      std::snprintf(buf, sizeof buf, "%u,", (unsigned)rows[(size_t)o * net.k + i]);
+      s += buf;
+    }
+    s += "},";
+  }
+  std::snprintf(buf, sizeof buf, "};\n  static constexpr %sPlanes planes = {{", name);
+  s += buf;
+  for (uint32_t o = 0; o < net.p; ++o) {
+    s += "{";
+    for (uint32_t i = 0; i < net.k; ++i) {
+      s += "{";
+      for (int q = 0; q < net.np; ++q) {
+        std::snprintf(buf, sizeof buf, "%lluull,", (unsigned long long)net.at(o, i, q));
+        s += buf;
+      }
+      s += "},";
+    }
+    s += "},";
+  }
+  s += "}, {";
+  for (uint32_t i = 0; i < net.k; ++i) {
+    std::snprintf(buf, sizeof buf, "%d,", net.ntmp[i]);
+    s += buf;
+  }
+  s += "}, {";
+  for (uint32_t i = 0; i < net.k; ++i) {
+    s += "{";
+    for (int t = 0; t < nt; ++t) {
+      const auto& x = net.tmp[(size_t)i * nt + t];
+      std::snprintf(buf, sizeof buf, "{%d,%d,%d},", x[0], x[1], x[2]);
+      s += buf;
+    }
+    s += "},";
+  }
+  s += "}};\n};\n";
+  return s;
+}
+
+}  // namespace netgen
+}  // namespace rse
