@@ -201,9 +201,9 @@ int run_job(const Job& j, hipStream_t s) {
   // a wide codec's (or pattern's) rows with their one-module kernel built:
   // every whole 4 KiB chunk in one launch (each input read once, each output
   // written once), the rest of every shard below
-  if ((n_in > (size_t)kMaxIn || n_out > rse::kJitMaxOut) && !j.accumulate &&
-      j.len_bytes >= 4096 && j.stripe_stride % 16u == 0 && rse::get_option(RSE_OPT_BITSLICE) &&
-      rse::wide_eligible((uint32_t)n_in, (uint32_t)n_out) && j.n_stripes <= 0xffffffffu) {
+  if (!j.accumulate && j.len_bytes >= 4096 && j.stripe_stride % 16u == 0 &&
+      rse::get_option(RSE_OPT_BITSLICE) && rse::wide_eligible((uint32_t)n_in, (uint32_t)n_out) &&
+      j.n_stripes <= 0xffffffffu) {
     bool al = true;
     for (size_t i = 0; i < n_in; ++i) al = al && aligned16(j.in[i]);
     for (size_t r = 0; r < n_out; ++r) {
@@ -385,7 +385,8 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
 constexpr uint64_t kWideJitBytes = 1ull << 30;
 void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_t n_stripes = 1) {
   if (len_bytes < 4096 || c->jit_requested.load(std::memory_order_relaxed)) return;
-  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
+  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||
+                    rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   if (wide && !now && rse::get_option(RSE_OPT_JIT) < 2) {
     const uint64_t b = (uint64_t)len_bytes * c->total * n_stripes;
     if (c->wide_bytes.fetch_add(b, std::memory_order_relaxed) + b < kWideJitBytes) return;
@@ -1142,7 +1143,8 @@ int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const Rows rows = parity_rows(c);
-  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut;
+  const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||
+                    rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   const bool one = rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   switch (wide ? (one ? rse::jit_wide_status(c->field, (uint32_t)c->k, (uint32_t)c->p,
                                              rows.c.data(), wait != 0)

@@ -166,7 +166,10 @@ void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t
 
 // A wide codec's outputs split over the waves of one workgroup: W = ceil(p/8)
 // waves, shares as equal as possible (the waves run side by side).
-int wide_waves(uint32_t p) { return (int)((p + kJitMaxOut - 1) / kJitMaxOut); }
+int wide_waves(uint32_t p) {
+  const uint32_t per = wide_per_wave();
+  return (int)((p + per - 1) / per);
+}
 void wide_share(uint32_t p, int w, uint32_t* o0, uint32_t* n) {
   const uint32_t W = (uint32_t)wide_waves(p), base = p / W, extra = p % W;
   *o0 = w * base + std::min<uint32_t>(w, extra);
@@ -206,10 +209,10 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   // at least 2 waves per SIMD (256 VGPRs): __launch_bounds__ of a
                   // 64-thread group would give 64 VGPRs and spill
                   "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
-                  "    amdgpu_waves_per_eu(2))) void rse_jit_wide(const WideArgs a) {\n"
+                  "    amdgpu_waves_per_eu(%d))) void rse_jit_wide(const WideArgs a) {\n"
                   "  __shared__ rse::WidePlanes<%d> lds;\n"
                   "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
-                  k, p, p, 64 * W, 64 * W, W);
+                  k, p, p, 64 * W, 64 * W, wide_per_wave() <= 4 ? 3 : 2, W);
     s += buf;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     for (int w = 0; w < W; ++w) {
@@ -644,9 +647,15 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   return 1;
 }
 
+uint32_t wide_per_wave() {
+  const int64_t v = get_option(18);
+  return v >= 2 && v <= (int64_t)kJitMaxOut ? (uint32_t)v : kJitMaxOut;
+}
+
 bool wide_eligible(uint32_t k, uint32_t p) {
-  return k >= 1 && p >= 1 && (k > (uint32_t)kMaxIn || p > kJitMaxOut) &&
-         p <= kJitMaxOut * 8u && k + 2u * p <= kWideMaxPtrs;
+  const uint32_t per = wide_per_wave();
+  return k >= 1 && p >= 1 && (k > (uint32_t)kMaxIn || p > per) && p <= per * 8u &&
+         k + 2u * p <= kWideMaxPtrs;
 }
 
 int jit_register_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern) {

@@ -761,6 +761,7 @@ struct Options {
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
   int64_t recon_mix = 1;          // syndrome reconstruct: bit-sliced mixing (0: v_perm tables)
+  int64_t wide_split = 8;         // outputs per wave of wide modules
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1100,6 +1101,7 @@ int set_option(int key, int64_t value) {
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
     case 17: g_opt.recon_mix = value ? 1 : 0; return 0;
+    case 18: g_opt.wide_split = value < 2 ? 2 : value > 8 ? 8 : value; return 0;
     default: return -1;
   }
 }
@@ -1132,6 +1134,7 @@ int64_t get_option(int key) {
     case 15: return g_opt.jit_disk_cache;
     case 16: return jit_cache_hits();
     case 17: return g_opt.recon_mix;
+    case 18: return g_opt.wide_split;
     default: return -1;
   }
 }

@@ -165,6 +165,10 @@ enum JitKind { kJitCodec = 0, kJitPattern = 1, kJitBlock = 2, kJitBlockAcc = 3, 
 // kernel-argument block.
 constexpr uint32_t kWideMaxPtrs = 480;
 bool wide_eligible(uint32_t k, uint32_t p);
+// Outputs per wave of a wide module (RSE_OPT_WIDE_SPLIT, default 8): below 8,
+// codecs with more parity rows than that take wide modules too (A/B: splitting
+// a codec's outputs over 2 waves halves the accumulator VGPRs).
+uint32_t wide_per_wave();
 int jit_register_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool pattern);
 int jit_wide_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait);
 // Codes the whole 4 KiB chunks of every shard (of n_stripes stripes) with the

@@ -48,12 +48,16 @@ def main():
     ap.add_argument("--recon-mix", default="1",
                     help="comma list of RSE_OPT_RECON_MIX values (syndrome reconstruct mixing: "
                          "1 bit-sliced, 0 v_perm tables)")
+    ap.add_argument("--wide-split", type=int, default=0,
+                    help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
     args = ap.parse_args()
     lib = R._lib.load()
     if args.wide_lds >= 0:
         lib.rse_set_option(14, args.wide_lds)
+    if args.wide_split > 0:
+        lib.rse_set_option(18, args.wide_split)
     lib.rse_set_option(9, 2)  # time run-time specialised kernels, not their build
     if args.jit_cse >= 0:
         lib.rse_set_option(13, args.jit_cse)
