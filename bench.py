@@ -472,13 +472,19 @@ def other_configs(stream):
              "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),
              "parity_check_vs_reference": got == want}
         if field == 16:
+            # first uses of an erasure pattern (syndrome kernels, no decode-
+            # pattern kernel): 8 data shards lost (bit-sliced mixing) and 4
+            for lost in (8, 4):
+                erased = list(range(lost))
+                present = [i not in erased for i in range(T)]
+                rb = stripes * (k + lost) * nbytes
+                lib.rse_set_option(11, 0)
+                d[f"reconstruct_{lost}_erased_syndrome_GB_per_s"] = timed_gbps(
+                    lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
+                lib.rse_set_option(11, 1)
             erased = [0, 1, 2, 3]
             present = [i not in erased for i in range(T)]
             rb = stripes * (k + len(erased)) * nbytes
-            lib.rse_set_option(11, 0)
-            d["reconstruct_4_erased_syndrome_GB_per_s"] = timed_gbps(
-                lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
-            lib.rse_set_option(11, 1)
             old = lib.rse_get_option(9)
             lib.rse_set_option(9, 2)
             d["reconstruct_4_erased_cached_pattern_GB_per_s"] = timed_gbps(
@@ -490,7 +496,41 @@ def other_configs(stream):
         out[f"gf{field}_{k}_{p}"] = d
         del buf, v
         torch.cuda.empty_cache()
+    out["gf8_50_20"] = wide_config(stream, g)
     return out
+
+
+def wide_config(stream, g):
+    """GF(2^8) 50+20 x 1 MiB -- the widest codec of the reference's own bench
+    (benches/bandwidth.rs:128) -- on its one-module kernel (rse_jit.cpp
+    kJitWide, built by hiprtc in helper processes before timing), stripe 0's
+    parity against the reference digests of tests/golden."""
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix, last_kernel
+    lib = R_lib()
+    k, p, nbytes, stripes = 50, 20, MiB, 128
+    T = k + p
+    buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
+    v = buf.view(stripes, T, nbytes)
+    for s_ in range(stripes):
+        for i in range(k):
+            fill_splitmix(v[s_, i], SEED, shard_id(s_, i))
+    r = R.core.ReedSolomon(k, p, 8)
+    t0 = time.perf_counter()
+    kind = r.kernel_kind(wait=True)
+    build_s = time.perf_counter() - t0
+    enc = timed_gbps(lambda: r.encode_flat(buf, nbytes, stripes), stripes * T * nbytes, stream)
+    want = g["full_size"][f"gf8_{k}_{p}_{nbytes}"]["parity_sha256"]
+    got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
+    d = {"workload": f"gf8 {k}+{p} x 1 MiB, {stripes} stripes/launch", "kernels": kind,
+         "kernel": last_kernel(), "build_seconds": round(build_s, 1),
+         "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
+         "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),
+         "parity_check_vs_reference": got == want}
+    del buf, v
+    torch.cuda.empty_cache()
+    return d
 
 
 def R_lib():

@@ -144,7 +144,9 @@ def generated():
 
     # Full-size configurations (BASELINE.json configs): parity digests.
     full = {}
-    for (k, p, n) in [(10, 2, 1 << 20), (10, 4, 16 << 20)]:
+    # 50+20: the widest configuration of the reference's own bench
+    # (benches/bandwidth.rs:128), at the 1 MiB shards of the README table
+    for (k, p, n) in [(10, 2, 1 << 20), (10, 4, 16 << 20), (50, 20, 1 << 20)]:
         cc = O.Codec(8, k, p)
         rr = np.ascontiguousarray(cc.matrix()[k:])
         data = [O.splitmix_bytes(SEED, s, n) for s in range(k)]
