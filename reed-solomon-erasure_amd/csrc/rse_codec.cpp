@@ -735,6 +735,32 @@ int host_code(int field, const Rows& rows, const void* const* in, void* const* o
 
 // host: the shards are in host memory (rse_encode_sep_host): same validation,
 // then the host pipeline instead of device launches.
+// n_stripes flat stripes that share one erasure pattern (reconstruct, or
+// reconstruct_data: the wasm ABI, wasm/src/lib.rs:57-73): planned once on the
+// host (with the LRU), then coded by the pattern's own kernel if it has one,
+// else the bit-sliced syndrome kernel, the table kernels for the rest.
+int flat_reconstruct(const rse_codec* c, uint8_t* base, size_t shard_len, size_t n_stripes,
+                     const uint8_t* present, bool data_only, hipStream_t s) {
+  if (n_stripes == 0) return RSE_OK;
+  const size_t sb = shard_len * c->esize();
+  std::vector<void*> ptrs(c->total);
+  std::vector<size_t> lens(c->total, shard_len);
+  for (size_t i = 0; i < c->total; ++i) ptrs[i] = base + i * sb;
+  ReconPlan plan;
+  int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, data_only, plan);
+  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  const uint64_t stride = (uint64_t)c->total * sb;
+  if (pattern_kernel(c, plan, sb)) {
+    ++g_pattern_launches;
+    return run_plan_tail(c, plan, 0, stride, n_stripes, s);
+  }
+  size_t done = 0;
+  rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(ptrs.data()), present,
+                            data_only, sb, stride, n_stripes, s, &done);
+  if (rc) return rc;
+  return run_plan_tail(c, plan, done, stride, n_stripes, s);
+}
+
 int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* data_lens,
                     size_t n_data, void* const* parity, const size_t* parity_lens,
                     size_t n_parity, hipStream_t s, bool host = false) {
@@ -1294,24 +1320,8 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
                               size_t n_stripes, const uint8_t* present, rse_stream_t stream) {
   RSE_ON_STREAM(stream);
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
-  if (n_stripes == 0) return RSE_OK;
-  const size_t sb = shard_len * c->esize();
-  uint8_t* base = static_cast<uint8_t*>(stripes);
-  std::vector<void*> ptrs(c->total);
-  std::vector<size_t> lens(c->total, shard_len);
-  for (size_t i = 0; i < c->total; ++i) ptrs[i] = base + i * sb;
-  ReconPlan plan;
-  int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, true, plan);
-  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
-  if (pattern_kernel(c, plan, sb)) {
-    ++g_pattern_launches;
-    return run_plan_tail(c, plan, 0, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream);
-  }
-  size_t done = 0;
-  rc = bitslice_reconstruct(c, reinterpret_cast<const uint8_t* const*>(ptrs.data()), present, true,
-                            sb, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream, &done);
-  if (rc) return rc;
-  return run_plan_tail(c, plan, done, (uint64_t)c->total * sb, n_stripes, (hipStream_t)stream);
+  return flat_reconstruct(c, static_cast<uint8_t*>(stripes), shard_len, n_stripes, present, true,
+                          (hipStream_t)stream);
 }
 
 // Many stripes, each with its own erasure pattern, in two launches: the plan
@@ -1335,6 +1345,32 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   }
   uint8_t* base = static_cast<uint8_t*>(stripes);
   hipStream_t st = (hipStream_t)stream;
+  // Runs of consecutive stripes with one erasure pattern (a lost disk: every
+  // stripe misses the same shards) go through the shared-pattern path: one
+  // plan per run, and the pattern's own kernel once it has one (core.rs:
+  // 697-731 caches the pattern; used twice, it is specialised), instead of a
+  // plan and a mixing per stripe.  Used when the runs are long (at most one
+  // run per 16 stripes on average).
+  {
+    std::vector<std::pair<size_t, size_t>> runs;  // [first, count)
+    for (size_t s0 = 0; s0 < n_stripes;) {
+      size_t s1 = s0 + 1;
+      while (s1 < n_stripes && std::memcmp(present + s1 * T, present + s0 * T, T) == 0) ++s1;
+      runs.emplace_back(s0, s1 - s0);
+      if (runs.size() * 16 > n_stripes) break;
+      s0 = s1;
+    }
+    size_t covered = 0;
+    for (auto& r : runs) covered += r.second;
+    if (covered == n_stripes && runs.size() * 16 <= n_stripes) {
+      for (auto& r : runs) {
+        const int rc = flat_reconstruct(c, base + r.first * T * sb, shard_len, r.second,
+                                        present + r.first * T, data_only != 0, st);
+        if (rc) return rc;
+      }
+      return RSE_OK;
+    }
+  }
   const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
   // 1. whole 16 KiB chunks on the bit-sliced syndrome kernels (compiled or

@@ -464,3 +464,41 @@ def test_encode_sep_and_single_host_match_oracle(R, small_chunks, field, k, p):
     with pytest.raises(R.RSError) as ei:
         r.encode_single_host(k, hs)
     assert ei.value.error == R.Error.InvalidIndex
+
+
+# ------------------------------------------ reconstruct_batch, shared patterns
+@pytest.mark.parametrize("field,k,p,lost", [(8, 10, 4, (0, 1)), (16, 20, 8, (0, 1, 2, 3, 4, 5, 6, 7)),
+                                            (8, 12, 4, (3, 13))])
+def test_reconstruct_batch_shared_pattern_runs(R, field, k, p, lost):
+    """A lost disk: every stripe of a batch misses the same shards.  Long runs
+    of one pattern take the shared-pattern path (one plan; the pattern's own
+    kernel under RSE_OPT_JIT 2) and give the oracle's bytes; two runs of
+    different patterns too."""
+    lib = R._lib.load()
+    rng = np.random.default_rng(91 + k)
+    T, es, n, stripes = k + p, field // 8, 16384 + 4096 + 64, 32
+    oc = O.Codec(field, k, p)
+    flat = np.zeros((stripes, T, n * es), np.uint8)
+    for s in range(stripes):
+        sh = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(sh)
+        flat[s] = np.stack(sh)
+    second = tuple(i for i in range(T) if i not in lost)[:len(lost)]
+    old = lib.rse_get_option(9)
+    try:
+        lib.rse_set_option(9, 2)
+        for runs in ((lost,), (lost, second)):
+            pres = np.ones((stripes, T), bool)
+            for s in range(stripes):
+                pres[s, list(runs[(s * len(runs)) // stripes])] = False
+            work = flat.copy()
+            work[~pres] = 0
+            d = torch.from_numpy(work.reshape(-1)).cuda()
+            r = R.core.ReedSolomon(k, p, field)
+            p0 = lib.rse_get_option(12)
+            r.reconstruct_batch(d, n, stripes, pres, data_only=False)
+            torch.cuda.synchronize()
+            assert lib.rse_get_option(12) - p0 == len(runs)  # one pattern kernel per run
+            assert (d.cpu().numpy().reshape(stripes, T, -1) == flat).all()
+    finally:
+        lib.rse_set_option(9, old)
