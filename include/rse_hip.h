@@ -295,6 +295,11 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_WIDE_SPLIT 18       /* outputs per wave of the one-module kernels (2..8, default 8):
                                        a codec with more parity rows than this (but <= 8 x this)
                                        is coded by W waves sharing each input chunk */
+#define RSE_OPT_WIDE_BALANCE 19     /* 1 (default): W at least 4 (p >= 4) and a power of two, so a
+                                       CU's 4 SIMDs hold equally many waves of the wide kernels;
+                                       0: W = ceil(p / split) */
+#define RSE_OPT_WIDE_OCCUPANCY 20   /* minimum waves per SIMD the wide kernels are compiled for:
+                                       0 (default) = 2, or 2..4 */
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */

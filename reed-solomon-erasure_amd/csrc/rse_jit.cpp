@@ -164,11 +164,33 @@ void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t
   s += "}  // namespace\n}  // namespace rse\n";
 }
 
-// A wide codec's outputs split over the waves of one workgroup: W = ceil(p/8)
-// waves, shares as equal as possible (the waves run side by side).
+// A wide codec's outputs split over the waves of one workgroup, shares as
+// equal as possible (the waves run side by side): W = ceil(p / 8) waves, or
+// with RSE_OPT_WIDE_BALANCE (default), for p >= 4, at least 4 and a power of
+// two.  A CU's 4 SIMDs then hold equally many of the workgroups' waves (3-wave
+// workgroups two to a CU leave two SIMDs with a single wave, which issues VALU
+// every 4 cycles at best), and the smaller shares need fewer registers, so
+// more waves fit.  Same-box A/B (profiles/r02_wide4/): GF(2^8) 50+20 3.72 TB/s
+// in 4 waves vs 3.37 in 3; 10+16 5.07 in 4 vs 4.92 in 2; GF(2^16) 40+12 4.29
+// vs 4.18 in 2; 100+30 2.63 in 4 vs 2.54 in 8.
 int wide_waves(uint32_t p) {
   const uint32_t per = wide_per_wave();
-  return (int)((p + per - 1) / per);
+  int w = (int)((p + per - 1) / per);
+  if (get_option(19) != 0 && p >= 4) {
+    int b = 4;
+    while (b < w) b *= 2;
+    if ((uint32_t)b <= p) w = b;
+  }
+  return w;
+}
+
+// Waves per SIMD the wide kernel is compiled for (a lower bound: the compiler
+// may use up to 256 VGPRs).  2 by default: asking for 3 makes the scheduler
+// spill (GF(2^8) 50+20 in 4 waves: 168 VGPRs and 25 spills at 3, 156 and none
+// at 2 -- which runs 3 waves per SIMD all the same).
+int wide_waves_per_eu(uint32_t) {
+  const int64_t o = get_option(20);  // RSE_OPT_WIDE_OCCUPANCY
+  return o ? (int)o : 2;
 }
 void wide_share(uint32_t p, int w, uint32_t* o0, uint32_t* n) {
   const uint32_t W = (uint32_t)wide_waves(p), base = p / W, extra = p % W;
@@ -200,7 +222,8 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       std::snprintf(name, sizeof name, "JitWide%d", w);
       // an input feeds many outputs here: shared temporaries in both fields
       // (GF(2^8): per input, computed per plane group)
-      emit_code(s, name, field, k, n, sub, field == 16 ? (int)get_option(13) : 16);
+      emit_code(s, name, field, k, n, sub,
+                field == 16 ? (int)get_option(13) : std::min(16, (int)get_option(13)));
     }
     char buf[512];
     std::snprintf(buf, sizeof buf,
@@ -212,7 +235,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   "    amdgpu_waves_per_eu(%d))) void rse_jit_wide(const WideArgs a) {\n"
                   "  __shared__ rse::WidePlanes<%d> lds;\n"
                   "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
-                  k, p, p, 64 * W, 64 * W, wide_per_wave() <= 4 ? 3 : 2, W);
+                  k, p, p, 64 * W, 64 * W, wide_waves_per_eu(p), W);
     s += buf;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     for (int w = 0; w < W; ++w) {

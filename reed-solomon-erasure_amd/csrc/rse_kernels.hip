@@ -762,6 +762,8 @@ struct Options {
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
   int64_t recon_mix = 1;          // syndrome reconstruct: bit-sliced mixing (0: v_perm tables)
   int64_t wide_split = 8;         // outputs per wave of wide modules
+  int64_t wide_balance = 1;       // wide modules: waves per workgroup rounded to 2, 4, 8
+  int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1102,6 +1104,8 @@ int set_option(int key, int64_t value) {
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
     case 17: g_opt.recon_mix = value ? 1 : 0; return 0;
     case 18: g_opt.wide_split = value < 2 ? 2 : value > 8 ? 8 : value; return 0;
+    case 19: g_opt.wide_balance = value ? 1 : 0; return 0;
+    case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;
     default: return -1;
   }
 }
@@ -1135,6 +1139,8 @@ int64_t get_option(int key) {
     case 16: return jit_cache_hits();
     case 17: return g_opt.recon_mix;
     case 18: return g_opt.wide_split;
+    case 19: return g_opt.wide_balance;
+    case 20: return g_opt.wide_occupancy;
     default: return -1;
   }
 }

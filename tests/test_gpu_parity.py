@@ -1146,9 +1146,26 @@ def test_bench_ranks_rehearsal(ranks, extras):
 
 
 # (field, k, p, modules): one wide module (p <= 64, k + 2p <= 480), or
-# blocks of 8 outputs x 32 inputs beyond that
+# blocks of 8 outputs x 32 inputs beyond that.  Waves per workgroup
+# (rse_jit.cpp wide_waves): 1 for p < 4, else 4 (p <= 32) or 8 (10+40: shares
+# of 5; 4+17: 5/4/4/4).
 WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
-               (8, 4, 66, 9)]
+               (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9)]
+
+
+def test_wide_codec_unbalanced_waves(R):
+    """RSE_OPT_WIDE_BALANCE 0: W = ceil(p / 8) waves (2 for 7+11, shares 6/5)
+    instead of 4; same bytes.  A codec no other test builds (modules are keyed
+    by rows, not options)."""
+    lib = R._lib.load()
+    old = lib.rse_get_option(19)
+    try:
+        assert lib.rse_set_option(19, 0) == 0
+        test_wide_codec_kernels(R, 8, 7, 11, 1)
+        from reed_solomon_erasure.core import last_kernel
+        assert last_kernel().startswith("bitslice-wide gf8 7+11 w2"), last_kernel()
+    finally:
+        lib.rse_set_option(19, old)
 
 
 @pytest.mark.parametrize("field,k,p,modules", WIDE_CODECS)

@@ -52,8 +52,14 @@ def main():
                     help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="rse_set_option(KEY, VALUE) before the codec is created (repeatable)")
     args = ap.parse_args()
     lib = R._lib.load()
+    for kv in args.set:
+        key, val = (int(x) for x in kv.split("="))
+        if lib.rse_set_option(key, val) != 0:
+            sys.exit(f"unknown option {key}")
     if args.wide_lds >= 0:
         lib.rse_set_option(14, args.wide_lds)
     if args.wide_split > 0:
