@@ -147,18 +147,18 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_dma_kerne
     dma_inputs<C, D, 0>(acc, ring, ring_ptr, c * C::k, c > 0, s_ops);
     store_outputs<C, true>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {
-      atomicOr(a.mismatch + (blockIdx.x + c * gridDim.x) / chunks_per_stripe, 1u);
+      flag_mismatch(a.mismatch + (blockIdx.x + c * gridDim.x) / chunks_per_stripe);
       diff = false;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
-  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+  if (mode != kStore && diff) flag_mismatch(a.mismatch);
 }
 
-template <class C, bool NT, int NS, bool MIXB = true>
+template <class C, bool NT, int NS, int MIX>
 __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_body<C, NT, NS, MIXB>(a, chunks_per_stripe);
+  bitslice_recon_body<C, NT, NS, MIX>(a, chunks_per_stripe);
 }
 
 template <class C, bool NT, int NS>
@@ -305,6 +305,7 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
   d.synd = synd;
   d.sigma = sigma;
   d.n_out = o;
+  set_horner_masks(d, field);
 }
 
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
@@ -321,14 +322,14 @@ struct BsShape {
                       // write-through (sc1) stores ([8][0] sc1, [8][1] sc1 nt), 9 = 1
                       // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
   BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
-  BsRecFn rec[4];     // sigma rows NS = 1, 2, 4, 8 (nullptr above p); non-temporal
-  BsRecFn rec_tab[4]; // the same with the e x e mixing on v_perm tables (RSE_OPT_RECON_MIX 0)
+  BsRecFn rec[3][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
+                      // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
 };
 
-template <class C, int NS, bool MIXB = true>
+template <class C, int NS, int MIX>
 constexpr BsRecFn rec_fn() {
-  if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS, MIXB>;
+  if constexpr (NS <= C::p) return bitslice_recon_kernel<C, true, NS, MIX>;
   else return nullptr;
 }
 template <class C, int NS>
@@ -350,9 +351,9 @@ constexpr BsDescFn rec_desc_fn() {
      bitslice_kernel<C, true, true, false, false, true>},                          \
     {nullptr, bitslice_kernel<CP, true, true, false>}},                            \
    bitslice_kernel<C, true, true, false, false, false, true>,                      \
-   {rec_fn<C, 1>(), rec_fn<C, 2>(), rec_fn<C, 4>(), rec_fn<C, 8>()},              \
-   {rec_fn<C, 1, false>(), rec_fn<C, 2, false>(), rec_fn<C, 4, false>(),          \
-    rec_fn<C, 8, false>()},                                                        \
+   {{rec_fn<C, 1, 0>(), rec_fn<C, 2, 0>(), rec_fn<C, 4, 0>(), rec_fn<C, 8, 0>()},  \
+    {rec_fn<C, 1, 1>(), rec_fn<C, 2, 1>(), rec_fn<C, 4, 1>(), rec_fn<C, 8, 1>()},  \
+    {rec_fn<C, 1, 2>(), rec_fn<C, 2, 2>(), rec_fn<C, 4, 2>(), rec_fn<C, 8, 2>()}}, \
    {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
@@ -469,13 +470,12 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
       if (parity_rows[i] != sh.m[i]) return hipSuccess;
     int slot = -1;
     for (int q = 0; q < 4 && slot < 0; ++q)
-      if (sh.rec[q] && (1u << q) >= need) slot = q;
+      if (sh.rec[0][q] && (1u << q) >= need) slot = q;
     if (slot < 0) return hipSuccess;
-    const bool mixb = get_option(17) != 0;
-    note_kernel("bitslice-recon gf%d %u+%u ns%d %s", field, k, p, 1 << slot,
-                mixb ? "mix-bitsliced" : "mix-tables");
-    hipLaunchKernelGGL(mixb ? sh.rec[slot] : sh.rec_tab[slot], dim3((uint32_t)gx), dim3(kBsBlock),
-                       0, stream, a, cps);
+    const int mix = (int)get_option(17);
+    static const char* const kMixName[3] = {"mix-tables", "mix-chain", "mix-horner"};
+    note_kernel("bitslice-recon gf%d %u+%u ns%d %s", field, k, p, 1 << slot, kMixName[mix]);
+    hipLaunchKernelGGL(sh.rec[mix][slot], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     count_bitslice_launch();

@@ -366,11 +366,11 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
     code_inputs<C, NT, SB, XC, 0, S, ACC>(acc, cur, a, off, next_off);
     store_outputs<C, NT, WT, S>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
-      atomicOr(a.mismatch + c / chunks_per_stripe, 1u);
+      flag_mismatch(a.mismatch + c / chunks_per_stripe);
       diff = false;
     }
   }
-  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+  if (mode != kStore && diff) flag_mismatch(a.mismatch);
 }
 
 // Inputs I.. of one chunk with D inputs in flight: input I + D is loaded
@@ -409,11 +409,11 @@ __device__ __forceinline__ void bitslice_body_deep(const CodeArgs& a, uint64_t c
     code_inputs_deep<C, NT, D, 0>(acc, buf, a, off);
     store_outputs<C, NT>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {
-      atomicOr(a.mismatch + stripe, 1u);
+      flag_mismatch(a.mismatch + stripe);
       diff = false;
     }
   }
-  if (mode != kStore && diff) atomicOr(a.mismatch, 1u);
+  if (mode != kStore && diff) flag_mismatch(a.mismatch);
 }
 
 // ------------------------------------------------------------ wide codecs
@@ -441,11 +441,11 @@ __device__ __forceinline__ void wide_body(const A& a) {
     code_inputs<C, false, true, false, 0, 1024u, false, A>(acc, cur, a, off, ~0ull);
     store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
     if (h.per_stripe && diff) {
-      atomicOr(h.mismatch + stripe, 1u);
+      flag_mismatch(h.mismatch + stripe);
       diff = false;
     }
   }
-  if (mode != kStore && diff) atomicOr(h.mismatch, 1u);
+  if (mode != kStore && diff) flag_mismatch(h.mismatch);
 }
 
 // wide_body with the slicing shared through LDS: in round R, wave WI (of W)
@@ -526,11 +526,11 @@ __device__ __forceinline__ void wide_body_lds(const A& a, WidePlanes<W>& lds) {
     wide_rounds<C, W, WI, 0, A>(acc, cur, a, off, lds, g, lane);
     store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
     if (h.per_stripe && diff) {
-      atomicOr(h.mismatch + stripe, 1u);
+      flag_mismatch(h.mismatch + stripe);
       diff = false;
     }
   }
-  if (mode != kStore && diff) atomicOr(h.mismatch, 1u);
+  if (mode != kStore && diff) flag_mismatch(h.mismatch);
 }
 
 // ------------------------------------------------------------ reconstruct
@@ -795,9 +795,190 @@ __device__ __forceinline__ void recon_mix_bitsliced(const BsReconArgs& a,
   }
 }
 
+// The e x e mixing of a reconstruct kernel (RSE_OPT_RECON_MIX):
+//  kReconMixTables  v_perm tables in LDS after un-slicing (round 1);
+//  kReconMixChain   bit-sliced doubling chains above 4 syndrome rows, tables
+//                   below (round 2: +11 % at 8 rows);
+//  kReconMixHorner  bit-sliced Horner's rule (below), any number of rows.
+constexpr int kReconMixTables = 0, kReconMixChain = 1, kReconMixHorner = 2;
+constexpr int kReconMixDefault = kReconMixHorner;
+constexpr bool recon_mix_tables(int ns, int mix) {
+  return mix == kReconMixTables || (mix == kReconMixChain && ns <= 4);
+}
+
+// ---- Horner mixing (rse_kernels.hpp: the basis, BsReconArgs::hm) ----------
+// Output o = sum_r w[o][r] s_r, evaluated by Horner's rule over the basis
+// coordinates i (high to low) of the w[o][r]:
+//   v = z * v ^ (XOR of the syndromes s_r whose w[o][r] has coordinate i)
+// with the row set of step j in byte j of hm[o].  Multiplying by z moves plane
+// q of a group to q + 1 and XORs the group's top plane into the taps; it is
+// fused into the first row group's selection (new plane q = old plane q - 1
+// ^ the selected sources, one v_bitop3).  For each pair of rows {2t, 2t + 1}
+// the XOR d_t is precomputed, so a pair adds at most one source and a group
+// of two pairs (a nibble of the step's mask) at most two: one op per plane
+// per group, the nibble picking the case by a scalar branch.  No per-row y
+// chains (the doubling chains of recon_mix_bitsliced) and one output live at
+// a time: ~(NS / 4) x 16 + 4 ops per step, NB steps per output.
+template <class F>
+struct HornerF;
+template <>
+struct HornerF<BitsF8> {
+  static constexpr int N = 8;  // planes per group = coordinates
+  static constexpr uint32_t taps = kHornerTaps8;
+};
+template <>
+struct HornerF<BitsF16> {
+  static constexpr int N = 16;
+  static constexpr uint32_t taps = kHornerTaps16;
+};
+
+// Plane masks of the GF(2^16) basis conversions (plane q <-> element bit q ^ 8).
+constexpr uint64_t to_b_planes(int i) {  // z-coordinate plane i from element planes
+  uint64_t m = 0;
+  for (int j = 0; j < 16; ++j)
+    if ((kHornerBasis16.to_b[i] >> j) & 1u) m |= 1ull << (j ^ 8);
+  return m;
+}
+constexpr uint64_t from_b_planes(int q) {  // element plane q from z-coordinate planes
+  return kHornerBasis16.from_b[q ^ 8];
+}
+template <int... I>
+__device__ __forceinline__ void to_basis16(uint32_t* pl, int_seq<int, I...>) {
+  uint32_t in[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) in[q] = pl[q];
+  ((pl[I] = xinit<to_b_planes(I)>(in)), ...);
+}
+template <int... I>
+__device__ __forceinline__ void from_basis16(uint32_t* pl, int_seq<int, I...>) {
+  uint32_t in[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) in[q] = pl[q];
+  ((pl[I] = xinit<from_b_planes(I)>(in)), ...);
+}
+
+// Source of pair P selected by SEL (1: row 2P, 2: row 2P + 1, 3: d_P), or none.
+template <int SEL, int P, int NS>
+constexpr bool h_has() {
+  return (SEL == 1 && 2 * P < NS) || (SEL >= 2 && 2 * P + 1 < NS);
+}
+template <int SEL, int P, int NS, int ND>
+__device__ __forceinline__ const uint32_t* h_src(const uint32_t (&s)[NS * 16],
+                                                 const uint32_t (&d)[ND][16]) {
+  if constexpr (SEL == 1 && 2 * P < NS) return &s[2 * P * 16];
+  else if constexpr (SEL == 2 && 2 * P + 1 < NS) return &s[(2 * P + 1) * 16];
+  else if constexpr (SEL == 3 && 2 * P + 1 < NS) return d[P];
+  else return nullptr;
+}
+
+// v = (SH ? z * v : v) ^ the sources of nibble NIB of row group G.
+template <class F, bool SH, int NIB, int G, int NS, int ND>
+__device__ __forceinline__ void h_case(uint32_t (&v)[16], const uint32_t (&s)[NS * 16],
+                                       const uint32_t (&d)[ND][16]) {
+  constexpr int N = HornerF<F>::N;
+  constexpr bool hasA = h_has<NIB & 3, 2 * G, NS>(), hasB = h_has<(NIB >> 2) & 3, 2 * G + 1, NS>();
+  if constexpr (!SH && !hasA && !hasB) return;
+  const uint32_t* A = h_src<NIB & 3, 2 * G, NS, ND>(s, d);
+  const uint32_t* B = h_src<(NIB >> 2) & 3, 2 * G + 1, NS, ND>(s, d);
+  uint32_t n[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = q % N;
+    uint32_t t[4];
+    int c = 0;
+    t[c++] = SH ? v[i == 0 ? q + N - 1 : q - 1] : v[q];
+    if (SH && ((HornerF<F>::taps >> i) & 1u)) t[c++] = v[q - i + N - 1];
+    if constexpr (hasA) t[c++] = A[q];
+    if constexpr (hasB) t[c++] = B[q];
+    uint32_t x = t[0];
+    if (c == 2) x ^= t[1];
+    if (c >= 3) x = xor3(x, t[1], t[2]);
+    if (c == 4) x ^= t[3];
+    n[q] = x;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    v[q] = n[q];
+    asm volatile("" : "+v"(v[q]));  // a real branch per case, not selects
+  }
+}
+
+template <class F, bool SH, int G, int NS, int ND>
+__device__ __forceinline__ void h_group(uint32_t (&v)[16], const uint32_t (&s)[NS * 16],
+                                        const uint32_t (&d)[ND][16], uint32_t nib) {
+#define RSE_HCASE(n) \
+  case n:            \
+    h_case<F, SH, n, G, NS, ND>(v, s, d); \
+    break;
+  switch (nib) {
+    RSE_HCASE(0) RSE_HCASE(1) RSE_HCASE(2) RSE_HCASE(3)
+    RSE_HCASE(4) RSE_HCASE(5) RSE_HCASE(6) RSE_HCASE(7)
+    RSE_HCASE(8) RSE_HCASE(9) RSE_HCASE(10) RSE_HCASE(11)
+    RSE_HCASE(12) RSE_HCASE(13) RSE_HCASE(14) RSE_HCASE(15)
+    default: break;
+  }
+#undef RSE_HCASE
+}
+
+// The mixing of recon_chunk by Horner's rule on the sliced rows acc (converted
+// in place to the basis for GF(2^16)); each output un-sliced once and stored.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t (&acc)[NS * 16],
+                                                 uint64_t off) {
+  using F = typename C::Field;
+  constexpr int NB = HornerF<F>::N;
+  constexpr int ND = NS / 2 > 0 ? NS / 2 : 1;
+  const uint32_t n_out = __builtin_amdgcn_readfirstlane(a.n_out);
+  const uint32_t sigma = __builtin_amdgcn_readfirstlane(a.sigma);
+  if constexpr (NB == 16) {
+#pragma unroll
+    for (int r = 0; r < NS; ++r)
+      if ((sigma >> r) & 1u) to_basis16(&acc[r * 16], make_int_seq<16>{});
+  }
+  uint32_t d[ND][16];
+#pragma unroll
+  for (int t = 0; t < NS / 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[t][q] = acc[2 * t * 16 + q] ^ acc[(2 * t + 1) * 16 + q];
+#pragma unroll 1
+  for (uint32_t o = 0; o < n_out; ++o) {
+    // (readfirstlane returns int: widen through uint32_t, not sign-extended)
+    auto word = [&](int q) { return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.hm[o][q]); };
+    uint64_t lo = word(0) | word(1) << 32;
+    uint64_t hi = word(2) | word(3) << 32;
+    uint32_t v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = 0u;
+    // (the fused shift writes a second register set; the case joins cost
+    // 8 v_mov_b64 per step to move it back -- a tied in-place asm form and a
+    // one-step lag of rows 4..7 were probed and the copies stayed)
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      const uint32_t m = (uint32_t)lo & 0xFFu;
+      lo = (lo >> 8) | (hi << 56);
+      hi >>= 8;
+      h_group<F, true, 0, NS, ND>(v, acc, d, m & 15u);
+      if constexpr (NS > 4) h_group<F, false, 1, NS, ND>(v, acc, d, m >> 4);
+    }
+    const int32_t os = __builtin_amdgcn_readfirstlane(a.out_sigma[o]);
+#pragma unroll
+    for (int r = 0; r < NS; ++r)
+      if (os == r) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] ^= acc[r * 16 + q];
+      }
+    if constexpr (NB == 16) from_basis16(v, make_int_seq<16>{});
+    u32x4 x[4];
+    unslice<F>(v, x);
+    uint8_t* dst = a.out[o];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stv<NT>(dst + off + j * (kBsBlock * 16), x[j]);
+  }
+}
+
 // One 16 KiB chunk of one stripe: off is the lane's byte offset from the
-// argument block's shard pointers.
-template <class C, bool NT, int NS, bool MIXB = true>
+// argument block's shard pointers.  MIX: the e x e mixing (kReconMix*).
+template <class C, bool NT, int NS, int MIX>
 __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* tq,
                                             const uint32_t* tt2, uint64_t off) {
   using F = typename C::Field;
@@ -810,7 +991,10 @@ __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* t
   u32x4 cur[4];
   load4<NT>(cur, recon_ptr(a, C::k, first) + off);
   recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
-  if constexpr (MIXB) {  // the mixing on the sliced syndromes (recon_mix_bitsliced)
+  if constexpr (MIX == kReconMixHorner) {
+    recon_mix_horner<C, NT, NS>(a, acc, off);
+    return;
+  } else if constexpr (!recon_mix_tables(NS, MIX)) {  // the mixing on the sliced syndromes
     // outputs per pass: NS rows + G outputs + the y pair within the VGPR
     // budget of the launch bounds (3 waves/SIMD up to NS = 2, else 2)
     recon_mix_bitsliced<C, NT, NS, (NS <= 4 ? NS : 2)>(a, acc, off);  // (probed: G = 4 at NS = 8 spills)
@@ -867,22 +1051,15 @@ struct ReconLds {
 
 // Reconstruct body: one argument block for every stripe of the launch.
 // Launch bounds: kBsBlock lanes, NS > 4 ? 2 : 3 waves/SIMD.
-// Which mixing a reconstruct kernel uses: bit-sliced for NS > 4 (up to 8
-// syndromes: +11 % at GF(2^16) 20+8 with 8 data shards lost), v_perm tables
-// in LDS below (with 3 waves/SIMD they are as fast or faster there:
-// profiles/r02_mix_*.log).  MIXB = false forces the tables (A/B).
-template <int NS, bool MIXB>
-constexpr bool kMixBitsliced = MIXB && NS > 4;
-
-template <class C, bool NT, int NS, bool MIXB = true>
+template <class C, bool NT, int NS, int MIX>
 __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
                                                     uint64_t chunks_per_stripe) {
   const uint64_t total = chunks_per_stripe * a.n_stripes;
-  if constexpr (kMixBitsliced<NS, MIXB>) {
+  if constexpr (!recon_mix_tables(NS, MIX)) {
     for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
       const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-      recon_chunk<C, NT, NS, true>(a, nullptr, nullptr,
-                                   stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
+      recon_chunk<C, NT, NS, MIX>(a, nullptr, nullptr,
+                                  stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
     }
     return;
   }
@@ -893,25 +1070,25 @@ __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
   __syncthreads();
   for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    recon_chunk<C, NT, NS, false>(a, tq, tt2,
-                                  stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
+    recon_chunk<C, NT, NS, MIX>(a, tq, tt2,
+                                stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u);
   }
 }
 
 // Reconstruct body over per-stripe argument blocks (descs[s], written by the
 // device planner of rse_reconstruct_batch: every stripe its own erasure
 // pattern).  A workgroup rebuilds its mixing tables when its stripe changes.
-template <class C, bool NT, int NS, bool MIXB = true>
+template <class C, bool NT, int NS, int MIX = kReconMixDefault>
 __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __restrict__ descs,
                                                          uint64_t chunks_per_stripe,
                                                          uint64_t n_stripes) {
-  if constexpr (kMixBitsliced<NS, MIXB>) {
+  if constexpr (!recon_mix_tables(NS, MIX)) {
     const uint64_t total = chunks_per_stripe * n_stripes;
     for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
       const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
       const BsReconArgs& a = descs[stripe];
       if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
-      recon_chunk<C, NT, NS, true>(a, nullptr, nullptr, chunk * kBsChunk + threadIdx.x * 16u);
+      recon_chunk<C, NT, NS, MIX>(a, nullptr, nullptr, chunk * kBsChunk + threadIdx.x * 16u);
     }
     return;
   }
@@ -930,7 +1107,7 @@ __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __re
       __syncthreads();
       built = stripe;
     }
-    recon_chunk<C, NT, NS, false>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
+    recon_chunk<C, NT, NS, MIX>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
   }
 }
 

@@ -294,7 +294,7 @@ __global__ void compare_kernel(const uint8_t* a, const uint8_t* b, size_t len, u
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
        i += (size_t)gridDim.x * blockDim.x)
     diff |= a[i] != b[i];
-  if (diff) atomicOr(mm, 1u);
+  if (diff) *reinterpret_cast<volatile uint32_t*>(mm) = 1u;  // as rse_device.hpp flag_mismatch
 }
 
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mismatch,
@@ -304,14 +304,16 @@ hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32
   return hipGetLastError();
 }
 
-// Per-thread, per-device verdict words for run_check: a device array the
-// kernels OR into and a pinned host copy, allocated once and grown on demand
-// (verify is synchronous, so a thread's buffers are free again when it
-// returns).  Deliberately never freed: a thread_local destructor could run
-// after the HIP runtime has shut down.
+// Per-thread, per-device verdict words for run_check, in pinned host memory
+// mapped into the device (fine-grained, coherent): the check kernels store 1
+// into them directly (rse_device.hpp flag_mismatch), so a verify is one
+// launch and one synchronisation -- no memset or D2H copy of the verdict.
+// Allocated once and grown on demand (verify is synchronous, so a thread's
+// words are free again when it returns).  Deliberately never freed: a
+// thread_local destructor could run after the HIP runtime has shut down.
 struct CheckWords {
-  uint32_t* d = nullptr;
-  uint32_t* h = nullptr;
+  uint32_t* h = nullptr;  // host view
+  uint32_t* d = nullptr;  // device view of the same words
   size_t words = 0;
 };
 
@@ -325,17 +327,17 @@ hipError_t check_words(size_t words, CheckWords** out) {
   CheckWords& w = per_dev[dev];
   if (w.words < words) {
     const size_t n = std::max<size_t>(words, 256);
-    uint32_t *d = nullptr, *h = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&d), n * sizeof(uint32_t));
+    uint32_t *h = nullptr, *d = nullptr;
+    e = hipHostMalloc(reinterpret_cast<void**>(&h), n * sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return e;
-    e = hipHostMalloc(reinterpret_cast<void**>(&h), n * sizeof(uint32_t), hipHostMallocDefault);
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
     if (e != hipSuccess) {
-      (void)hipFree(d);
+      (void)hipHostFree(h);
       return e;
     }
-    if (w.d) (void)hipFree(w.d);  // the previous call has synchronised
-    if (w.h) (void)hipHostFree(w.h);
-    w = CheckWords{d, h, n};
+    if (w.h) (void)hipHostFree(w.h);  // the previous call has synchronised
+    w = CheckWords{h, d, n};
   }
   *out = &w;
   return hipSuccess;
@@ -347,18 +349,16 @@ int run_check(Job j, hipStream_t s, int* ok) {
   const size_t words = j.per_stripe ? j.n_stripes : 1;
   CheckWords* w = nullptr;
   RSE_HIP(check_words(words, &w));
-  RSE_HIP(hipMemsetAsync(w->d, 0, words * sizeof(uint32_t), s));
+  std::memset(w->h, 0, words * sizeof(uint32_t));  // no kernel of this thread uses them now
   j.mismatch = w->d;
   int rc = run_job(j, s);
-  if (rc != RSE_OK) {
-    // kernels already queued may still OR into this thread's words: drain
-    // them before the words can be reused by the thread's next verify
-    (void)hipStreamSynchronize(s);
-    return rc;
-  }
-  RSE_HIP(hipMemcpyAsync(w->h, w->d, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  RSE_HIP(hipStreamSynchronize(s));
-  for (size_t i = 0; i < words; ++i) ok[i] = w->h[i] == 0 ? 1 : 0;
+  // kernels already queued may still store into this thread's words: drain
+  // them before the words can be reused by the thread's next verify
+  const hipError_t se = hipStreamSynchronize(s);
+  if (rc != RSE_OK) return rc;
+  RSE_HIP(se);
+  for (size_t i = 0; i < words; ++i)
+    ok[i] = reinterpret_cast<volatile uint32_t*>(w->h)[i] == 0 ? 1 : 0;
   return RSE_OK;
 }
 
@@ -646,6 +646,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
     a.par[R[t]] = shards[k + R[t]];
   }
   for (size_t r : M) a.sigma |= 1u << r;
+  rse::set_horner_masks(a, c->field);
   a.stripe_stride = stripe_stride;
   std::vector<uint16_t> rows(p * k);
   for (size_t r = 0; r < p; ++r)

@@ -133,11 +133,19 @@ __device__ __forceinline__ uint32_t* mismatch_word(const CodeArgs& a, uint64_t s
   return a.mismatch + ((a.per_stripe && a.stripe_stride) ? soff / a.stripe_stride : 0u);
 }
 
-// One atomic per wave that saw a difference, on the word of stripe offset soff.
+// A check kernel's verdict: any nonzero word means a mismatch, so lanes that
+// find one store 1 (a plain vector store, idempotent: no atomic needed).  The
+// word may be in pinned host memory (rse_codec.cpp run_check), where a PCIe
+// atomic would need platform support.
+__device__ __forceinline__ void flag_mismatch(uint32_t* p) {
+  *reinterpret_cast<volatile uint32_t*>(p) = 1u;
+}
+
+// One store per wave that saw a difference, on the word of stripe offset soff.
 __device__ __forceinline__ void flag_mismatch(bool diff, const CodeArgs& a, uint64_t soff) {
   const unsigned long long m = __ballot(diff);
   if (m != 0ull && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
-    atomicOr(mismatch_word(a, soff), 1u);
+    flag_mismatch(mismatch_word(a, soff));
 }
 
 __device__ __forceinline__ uint32_t opaque_zero() {
@@ -147,6 +155,7 @@ __device__ __forceinline__ uint32_t opaque_zero() {
 }
 
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
 __device__ __forceinline__ void pin(uint4& v) {
   pin(v.x);
   pin(v.y);

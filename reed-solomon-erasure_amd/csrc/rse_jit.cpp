@@ -277,7 +277,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     std::snprintf(buf, sizeof buf,
                   "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
                   "    const rse::BsReconArgs a, uint64_t cps) {\n"
-                  "  rse::bitslice_recon_body<rse::JitCode, true, %d>(a, cps);\n}\n",
+                  "  rse::bitslice_recon_body<rse::JitCode, true, %d, rse::kReconMixDefault>(a, cps);\n}\n",
                   ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
     s += buf;
     std::snprintf(buf, sizeof buf,

@@ -181,7 +181,7 @@ __device__ __forceinline__ void gf8_code_impl(const CodeArgs& a, uint32_t stripe
       if (mode != kCheck) a.out[r][off] = (uint8_t)acc[r];
       if (mode != kStore) diff |= (uint8_t)acc[r] != a.cmp[r][off];
     }
-    if (mode != kStore && diff) atomicOr(mismatch_word(a, soff), 1u);
+    if (mode != kStore && diff) flag_mismatch(mismatch_word(a, soff));
   }
   }  // stripe loop
 }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
       if (mode != kStore)
         diff |= ((uint8_t)oh[r] != a.cmp[r][off]) || ((uint8_t)ol[r] != a.cmp[r][off + 1]);
     }
-    if (mode != kStore && diff) atomicOr(mismatch_word(a, soff), 1u);
+    if (mode != kStore && diff) flag_mismatch(mismatch_word(a, soff));
   }
   }  // stripe loop
 }
@@ -760,7 +760,7 @@ struct Options {
   int64_t jit_cse = 32;           // GF(2^16) specialised networks: temporaries per input
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
-  int64_t recon_mix = 1;          // syndrome reconstruct: bit-sliced mixing (0: v_perm tables)
+  int64_t recon_mix = 2;          // syndrome reconstruct mixing: 2 Horner, 1 doubling chains, 0 tables
   int64_t wide_split = 8;         // outputs per wave of wide modules
   int64_t wide_balance = 1;       // wide modules: waves per workgroup rounded to 2, 4, 8
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
@@ -1102,7 +1102,7 @@ int set_option(int key, int64_t value) {
     case 13: g_opt.jit_cse = value < 0 ? 0 : value > 32 ? 32 : value; return 0;
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
-    case 17: g_opt.recon_mix = value ? 1 : 0; return 0;
+    case 17: g_opt.recon_mix = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case 18: g_opt.wide_split = value < 2 ? 2 : value > 8 ? 8 : value; return 0;
     case 19: g_opt.wide_balance = value ? 1 : 0; return 0;
     case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;

@@ -72,7 +72,106 @@ struct BsReconArgs {
   uint32_t n_out;
   int32_t out_sigma[kMaxOut];     // sigma row XORed into output o, -1 for none
   uint16_t w[kMaxOut][kMaxOut];   // [o][r], zero unless r is in R
+  // Horner masks of w (set_horner_masks, rows r < 8): byte j of hm[o] (byte
+  // j % 4 of word j / 4) has bit r set iff coordinate NB - 1 - j of w[o][r]
+  // in the Horner basis is 1 (NB = 8 / 16 coordinates for GF(2^8) / GF(2^16)).
+  uint32_t hm[kMaxOut][4];
 };
+
+// ---- Horner mixing basis ----------------------------------------------------
+// The run-time e x e mixing of the syndrome reconstruct multiplies sliced
+// syndromes by run-time constants with Horner's rule over the coordinates c_i
+// of a constant c in a polynomial basis {1, z, .., z^(NB-1)}:
+//   c * s = (..((c_{NB-1} s) z + c_{NB-2} s) z + ..) z + c_0 s,
+// so that multiplying the accumulator by z is a rotation of its planes plus
+// 3 XORs of the top plane (the taps of z's minimal polynomial).
+//  GF(2^8):  z = 2, the generator of build.rs (x^8 = x^4 + x^3 + x^2 + 1):
+//            the standard basis, no conversion.
+//  GF(2^16): z = 0x4815, a root of z^16 + z^6 + z^2 + z + 1 (an irreducible
+//            pentanomial): sliced syndromes are converted into z-coordinates
+//            (to_b) and the mixed outputs back (from_b), 16 x 16 bit matrices.
+constexpr uint32_t kHornerTaps8 = (1u << 4) | (1u << 3) | (1u << 2);
+constexpr uint32_t kHornerZ16 = 0x4815u;
+constexpr uint32_t kHornerTaps16 = (1u << 6) | (1u << 2) | (1u << 1);
+
+constexpr uint32_t hb_mul8(uint32_t a, uint32_t b) {  // GF(2^8) modulo 0x11D (build.rs:11)
+  uint32_t r = 0;
+  for (int i = 0; i < 8; ++i) {
+    if ((b >> i) & 1u) r ^= a;
+    a <<= 1;
+    if (a & 0x100u) a ^= 0x11Du;
+  }
+  return r;
+}
+constexpr uint32_t hb_mul16(uint32_t a, uint32_t b) {  // galois_16.rs:146-162
+  const uint32_t a1 = a >> 8, a0 = a & 0xFFu, b1 = b >> 8, b0 = b & 0xFFu;
+  const uint32_t hh = hb_mul8(a1, b1);
+  const uint32_t x = hb_mul8(a1, b0) ^ hb_mul8(a0, b1) ^ hb_mul8(2u, hh);
+  return (x << 8) | (hb_mul8(a0, b0) ^ hb_mul8(128u, hh));
+}
+
+struct HornerBasis16 {
+  uint16_t to_b[16];    // coordinate i of element e: parity(e & to_b[i])
+  uint16_t from_b[16];  // bit j of an element: parity(coordinates & from_b[j])
+  bool ok;              // z^16 = z^6 + z^2 + z + 1 and the powers are a basis
+};
+constexpr HornerBasis16 make_horner_basis16() {
+  HornerBasis16 h{};
+  uint32_t zp[17] = {};
+  zp[0] = 1;
+  for (int i = 0; i < 16; ++i) zp[i + 1] = hb_mul16(zp[i], kHornerZ16);
+  uint32_t rel = zp[16] ^ 1u;
+  for (int i = 1; i < 16; ++i)
+    if ((kHornerTaps16 >> i) & 1u) rel ^= zp[i];
+  for (int j = 0; j < 16; ++j)
+    for (int i = 0; i < 16; ++i)
+      if ((zp[i] >> j) & 1u) h.from_b[j] |= (uint16_t)(1u << i);
+  // to_b = from_b^-1: Gauss-Jordan on [from_b | I] (bit 16 + j of row j)
+  uint32_t m[16] = {};
+  for (int j = 0; j < 16; ++j) m[j] = h.from_b[j] | (1u << (16 + j));
+  bool full = true;
+  for (int col = 0; col < 16; ++col) {
+    int piv = col;
+    while (piv < 16 && !((m[piv] >> col) & 1u)) ++piv;
+    if (piv == 16) {
+      full = false;
+      break;
+    }
+    const uint32_t t = m[piv];
+    m[piv] = m[col];
+    m[col] = t;
+    for (int r = 0; r < 16; ++r)
+      if (r != col && ((m[r] >> col) & 1u)) m[r] ^= m[col];
+  }
+  for (int i = 0; i < 16; ++i) h.to_b[i] = (uint16_t)(m[i] >> 16);
+  h.ok = full && rel == 0;
+  return h;
+}
+constexpr HornerBasis16 kHornerBasis16 = make_horner_basis16();
+static_assert(kHornerBasis16.ok, "z must be a root of the pentanomial and generate GF(2^16)");
+
+// Coordinates of c in the Horner basis of the field.
+__host__ __device__ inline uint32_t horner_coords(int field, uint32_t c) {
+  if (field == 8) return c & 0xFFu;
+  constexpr HornerBasis16 hb = make_horner_basis16();
+  uint32_t r = 0;
+  for (int i = 0; i < 16; ++i) r |= (uint32_t)__builtin_parity(c & hb.to_b[i]) << i;
+  return r;
+}
+
+// BsReconArgs::hm from w, synd and n_out (after those are final).
+__host__ __device__ inline void set_horner_masks(BsReconArgs& a, int field) {
+  const int nb = field == 8 ? 8 : 16;
+  for (int o = 0; o < kMaxOut; ++o)
+    for (int q = 0; q < 4; ++q) a.hm[o][q] = 0;
+  for (uint32_t o = 0; o < a.n_out && o < (uint32_t)kMaxOut; ++o)
+    for (int r = 0; r < 8; ++r) {
+      if (!((a.synd >> r) & 1u)) continue;
+      const uint32_t co = horner_coords(field, a.w[o][r]);
+      for (int j = 0; j < nb; ++j)
+        if ((co >> (nb - 1 - j)) & 1u) a.hm[o][j >> 2] |= 1u << (8 * (j & 3) + r);
+    }
+}
 
 // Header of a wide codec's argument block (rse_jit.cpp kJitWide).  The block
 // is the header followed by the k input, p output and p compare pointers

@@ -686,6 +686,50 @@ def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
             assert (got[s_, i] == full[i]).all(), (s_, i)
 
 
+@pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4)])
+def test_reconstruct_every_mixing_mode(R, field, k, p):
+    """The three e x e mixings of the syndrome reconstruct (RSE_OPT_RECON_MIX
+    0 v_perm tables, 1 doubling chains, 2 Horner's rule -- the default) give
+    the oracle's bytes on the same patterns: every syndrome row in use (rows
+    4..7 of the Horner masks set bit 31 of their mask words), data plus
+    parity lost, single erasures, and random patterns with both methods."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    es = field // 8
+    nbytes = 16384 * 2
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(77 + field)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    patterns = [list(range(p)), list(range(p - 1)) + [k], [0], [k - 1],
+                list(range(p - 2)) + [k, k + p - 1], [1, k + 1]]
+    patterns += [sorted(rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False).tolist())
+                 for _ in range(6)]
+    names = {0: "mix-tables", 1: "mix-chain", 2: "mix-horner"}
+    jp = lib.rse_get_option(11)
+    lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
+    try:
+        for mix in (2, 1, 0):
+            assert lib.rse_set_option(17, mix) == 0
+            for erased in patterns:
+                present = [i not in erased for i in range(k + p)]
+                tb = [dev(x).reshape(shape) for x in full]
+                for e in erased:
+                    tb[e].fill_(0x5A)
+                r.reconstruct(list(zip(tb, present)))
+                torch.cuda.synchronize()
+                if any(e < k for e in erased):
+                    assert names[mix] in last_kernel(), (mix, erased, last_kernel())
+                for i in erased:
+                    assert (host(tb[i]).reshape(-1) == full[i]).all(), (mix, erased, i)
+    finally:
+        lib.rse_set_option(17, 2)
+        lib.rse_set_option(11, jp)
+
+
 JIT_CODECS = [(8, 12, 4), (8, 6, 3), (8, 4, 2), (8, 32, 8), (8, 1, 1), (8, 17, 5),
               (16, 10, 4), (16, 4, 2), (16, 6, 7)]
 

@@ -19,8 +19,13 @@ __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void probe_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
   bitslice_body<C, true, SB, false>(a, chunks_per_stripe);
 }
+template <class C, int NS>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void rprobe(const BsReconArgs a,
+                                                                  uint64_t chunks_per_stripe) {
+  bitslice_recon_body<C, true, NS, kReconMixDefault>(a, chunks_per_stripe);
+}
 }  // namespace
-void* probe_fns[] = {(void*)probe_kernel<Bs16_20_8, false>, (void*)probe_kernel<Bs8_10_4, true>};
+void* probe_fns[] = {(void*)probe_kernel<Bs16_20_8, false>, (void*)probe_kernel<Bs8_10_4, true>, (void*)rprobe<Bs16_20_8, 8>, (void*)rprobe<Bs16_20_8, 4>, (void*)rprobe<Bs8_10_4, 4>};
 }  // namespace rse
 EOF
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 --offload-device-only -I"$PKG/csrc" \

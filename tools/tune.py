@@ -45,9 +45,9 @@ def main():
                          "kernels; the run-time builds are waited for)")
     ap.add_argument("--jit-cse", type=int, default=-1,
                     help="RSE_OPT_JIT_CSE for run-time specialised GF(2^16) modules (-1: default)")
-    ap.add_argument("--recon-mix", default="1",
+    ap.add_argument("--recon-mix", default="2",
                     help="comma list of RSE_OPT_RECON_MIX values (syndrome reconstruct mixing: "
-                         "1 bit-sliced, 0 v_perm tables)")
+                         "2 Horner, 1 doubling chains, 0 v_perm tables)")
     ap.add_argument("--wide-split", type=int, default=0,
                     help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
