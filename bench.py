@@ -639,13 +639,38 @@ def extra_legs(r, v, k, p, L, n_stripes, stream):
         dbuf.copy_(hflat, non_blocking=True)
     torch.cuda.synchronize()
     raw_h2d = hflat.numel() / ((time.perf_counter() - t0) / reps) / 1e9
-    del dbuf
+    # ... and the ceiling of the encode's own traffic: plain copies of the data
+    # shards up and the parity shards down at the same time (two streams)
+    hv = hflat.view(ns, k + p, L)
+    dv = dbuf.view(ns, k + p, L)
+    hpar = torch.empty((ns, p, L), dtype=torch.uint8).pin_memory()
+    up, down = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def duplex():  # per stripe: each copy is one contiguous block
+        with torch.cuda.stream(up):
+            for s_ in range(ns):
+                dv[s_, :k].copy_(hv[s_, :k], non_blocking=True)
+        with torch.cuda.stream(down):
+            for s_ in range(ns):
+                hpar[s_].copy_(dv[s_, k:], non_blocking=True)
+    duplex()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        duplex()
+    torch.cuda.synchronize()
+    dt_raw = (time.perf_counter() - t0) / reps
+    del dbuf, hpar
     out["end_to_end_pinned_host_flat"] = {
         "what": f"rse_encode_host_flat, {ns} stripes from pinned host memory, one "
                 "H2D/kernel/D2H pipeline",
         "MB_per_s": round(ns * (k + p) * L / dt / MiB, 1),
         "GB_per_s_pcie_h2d": round(ns * k * L / dt / 1e9, 1),
-        "raw_pinned_h2d_copy_GB_per_s": round(raw_h2d, 1), "parity_matches_device": ok}
+        "raw_pinned_h2d_copy_GB_per_s": round(raw_h2d, 1),
+        "raw_pinned_duplex_MB_per_s": round(ns * (k + p) * L / dt_raw / MiB, 1),
+        "raw_pinned_duplex_what": "plain copies of the same data shards H2D and parity "
+                                  "shards D2H at once (the encode's traffic, no kernel)",
+        "parity_matches_device": ok}
     # the decode direction from host memory: data shards 0 and 1 of every
     # stripe lost; only the k valid shards go up, only the 2 rebuilt come back
     want = hflat.view(ns, k + p, L)[:, :2].clone()

@@ -909,6 +909,7 @@ template <class HostPtr>
 hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<uint32_t>& idx,
                        HostPtr host, size_t off, size_t sz, bool flat, hipStream_t s) {
   hipError_t e = hipSuccess;
+  if (!rse::get_option(RSE_OPT_HOST_COPY_2D)) flat = false;
   for (size_t a = 0; a < idx.size() && e == hipSuccess;) {
     size_t b = a + 1;
     ptrdiff_t pitch = 0;

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--hog-gib", type=int, default=0,
                     help="allocate this much extra device memory first (the bench holds 112 GiB)")
     ap.add_argument("--chunks", default="1024,2048,4096,8192,16384")
+    ap.add_argument("--streams", default="1,2,3", help="RSE_OPT_HOST_H2D_STREAMS values")
+    ap.add_argument("--copy2d", default="1,0", help="RSE_OPT_HOST_COPY_2D values")
     args = ap.parse_args()
     hog = torch.empty(args.hog_gib << 30, dtype=torch.uint8, device="cuda") if args.hog_gib else None
     if os.environ.get("RSE_E2E_JIT_FIRST"):  # a hiprtc build in this process beforehand
@@ -72,22 +74,38 @@ def main():
             hh.copy_(d, non_blocking=True)
     t = timed(both, args.reps)
     print(f"raw H2D+D2H concurrent {2 * n / t / 1e9:6.1f} GB/s total")
+    hv, dv = h.view(S, k + p, L), dd.view(S, k + p, L)
+    hpar = torch.empty((S, p, L), dtype=torch.uint8).pin_memory()
+
+    def duplex():  # the encode's own traffic: data shards up, parity down
+        with torch.cuda.stream(s1):
+            for s_ in range(S):
+                dv[s_, :k].copy_(hv[s_, :k], non_blocking=True)
+        with torch.cuda.stream(s2):
+            for s_ in range(S):
+                hpar[s_].copy_(dv[s_, k:], non_blocking=True)
+    t = timed(duplex, args.reps)
+    print(f"raw duplex (data up, parity down) {S * (k + p) * L / t / 1e9:6.1f} GB/s data+parity "
+          f"(H2D {S * k * L / t / 1e9:5.1f})")
     best = None
-    for chunk in [int(x) for x in args.chunks.split(",")]:
-        for nh in (1, 2, 3):
+    for c2, chunk, nh in [(c2, c, n) for c2 in (int(x) for x in args.copy2d.split(","))
+                          for c in (int(x) for x in args.chunks.split(","))
+                          for n in (int(x) for x in args.streams.split(","))]:
+            lib.rse_set_option(21, c2)
             lib.rse_set_option(7, chunk)
             lib.rse_set_option(8, nh)
             h.view(S, k + p, L)[:, k:].zero_()
             t = timed(lambda: r.encode_host_flat(h, L, S), args.reps)
             ok = torch.equal(h.view(S, k + p, L)[:, k:], want)
             rate = S * (k + p) * L / t
-            print(f"pipeline chunk={chunk:5d} KiB h2d_streams={nh}  {rate / 1e9:6.1f} GB/s data+parity "
+            print(f"pipeline 2d={c2} chunk={chunk:5d} KiB h2d_streams={nh}  {rate / 1e9:6.1f} GB/s data+parity "
                   f"(H2D {S * k * L / t / 1e9:5.1f} GB/s)  parity_ok={ok}", flush=True)
             if ok and (best is None or rate > best[0]):
-                best = (rate, chunk, nh)
-    print(f"best: chunk={best[1]} KiB h2d_streams={best[2]} {best[0] / 1e9:.1f} GB/s")
+                best = (rate, chunk, nh, c2)
+    print(f"best: 2d={best[3]} chunk={best[1]} KiB h2d_streams={best[2]} {best[0] / 1e9:.1f} GB/s")
     lib.rse_set_option(7, 4096)
     lib.rse_set_option(8, 2)
+    lib.rse_set_option(21, 1)
     del hog
 
 
