@@ -265,13 +265,13 @@ def gather(values, world, rank, device):
 
 def host_leg(r, v, k, p, L, stream, world, rank, coll_dev):
     """Host-memory encode on every rank at once (multi-GPU host bandwidth,
-    SURVEY 8f): each rank streams 4 of its stripes from pinned host memory
+    SURVEY 8f): each rank streams 8 of its stripes from pinned host memory
     through its GPU; the job rate is all ranks' bytes over the slowest rank."""
     import torch
     import torch.distributed as dist
-    ns = min(4, v.shape[0])
+    ns = min(8, v.shape[0])
     hflat = v[:ns].reshape(-1).cpu().pin_memory()
-    r.encode_host_flat(hflat, L, ns)  # warm
+    r.encode_host_flat(hflat, L, ns)  # warm (first use of the buffer, the pipeline's resources)
     reps = 3
     if world > 1:
         dist.barrier()

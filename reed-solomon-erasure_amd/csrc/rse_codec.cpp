@@ -941,6 +941,70 @@ struct HostCode {
   bool accumulate;
 };
 
+// The pipeline's streams, events and device ring, kept per thread and device
+// between calls (creating 4 streams, 12 events and a ring of up to hundreds of
+// MiB per call cost milliseconds: a one-stripe 10+4 x 16 MiB host encode ran
+// at 21 GB/s against 54 for eight).  A call leaves them idle (it synchronises
+// the caller's stream, which waits for every pipeline stream).  Grown on
+// demand; deliberately never freed (a thread_local destructor could run after
+// the HIP runtime has shut down).
+struct PipeRes {
+  int nh = 0, ring = 0;
+  std::vector<hipStream_t> st;
+  std::vector<hipEvent_t> h2d, coded, d2h;
+  hipEvent_t start = nullptr;
+  uint8_t* dbuf = nullptr;
+  size_t dbytes = 0;
+};
+
+hipError_t pipe_res(int nh, int ring, size_t dbytes, PipeRes** out) {
+  constexpr int kMaxDev = 64;
+  thread_local PipeRes per_dev[kMaxDev];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+  PipeRes& r = per_dev[dev];
+  if (r.nh != nh || r.ring != ring) {
+    for (auto& q : r.st) (void)hipStreamDestroy(q);
+    for (auto* ev : {&r.h2d, &r.coded, &r.d2h})
+      for (auto& q : *ev) (void)hipEventDestroy(q);
+    r.st.clear();
+    r.h2d.clear();
+    r.coded.clear();
+    r.d2h.clear();
+    r.nh = r.ring = 0;
+    for (int i = 0; i < nh + 2 && e == hipSuccess; ++i) {
+      hipStream_t q = nullptr;
+      e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+      if (e == hipSuccess) r.st.push_back(q);
+    }
+    for (auto* ev : {&r.h2d, &r.coded, &r.d2h})
+      for (int i = 0; i < ring && e == hipSuccess; ++i) {
+        hipEvent_t q = nullptr;
+        e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
+        if (e == hipSuccess) ev->push_back(q);
+      }
+    if (e != hipSuccess) return e;
+    r.nh = nh;
+    r.ring = ring;
+  }
+  if (!r.start) {
+    e = hipEventCreateWithFlags(&r.start, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  if (r.dbytes < dbytes) {
+    if (r.dbuf) (void)hipFree(r.dbuf);  // idle: the previous call synchronised
+    r.dbuf = nullptr;
+    r.dbytes = 0;
+    e = hipMalloc(reinterpret_cast<void**>(&r.dbuf), dbytes);
+    if (e != hipSuccess) return e;
+    r.dbytes = dbytes;
+  }
+  *out = &r;
+  return hipSuccess;
+}
+
 // Runs `op` over `bytes` of every shard of every stripe (codec ops: `c`;
 // kCode: `code`).  verify ops: ok[s] receives stripe s's verdict.
 int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& stripes,
@@ -958,20 +1022,15 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   const size_t T = low ? k + code->rows->n_out : c->total;
   const size_t p = T - k, es = field == RSE_FIELD_GF16 ? 2 : 1;
   const size_t nbuf = T + (op == HostOp::kVerifyBuf ? p : 0);  // shards per slot
-  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H
-  std::vector<hipStream_t> st(nh + 2, nullptr);
-  std::vector<hipEvent_t> h2d(ring, nullptr), coded(ring, nullptr), d2h(ring, nullptr);
-  uint8_t* dbuf = nullptr;
+  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H (cached: PipeRes)
+  PipeRes* res = nullptr;
+  hipError_t e = pipe_res(nh, ring, ring * nbuf * chunk, &res);
+  if (e != hipSuccess) return dev_fail(e);
+  const std::vector<hipStream_t>& st = res->st;
+  const std::vector<hipEvent_t>&h2d = res->h2d, &coded = res->coded, &d2h = res->d2h;
+  hipEvent_t start = res->start;
+  uint8_t* dbuf = res->dbuf;
   uint32_t *dwords = nullptr, *hwords = nullptr;
-  hipEvent_t start = nullptr;
-  hipError_t e = hipSuccess;
-  for (auto& q : st)
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
-  for (auto* ev : {&h2d, &coded, &d2h})
-    for (auto& q : *ev)
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dbuf), ring * nbuf * chunk, user);
   if (verify) {  // one mismatch word per stripe
     const size_t wb = stripes.size() * sizeof(uint32_t);
     if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&dwords), wb, user);
@@ -1051,19 +1110,14 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   if (verify && dwords && hwords && e == hipSuccess && e2 == hipSuccess && rc == RSE_OK)
     e2 = hipMemcpyAsync(hwords, dwords, stripes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         user);
-  if (dbuf) (void)hipFreeAsync(dbuf, user);
   if (dwords) (void)hipFreeAsync(dwords, user);
   const hipError_t e3 = hipStreamSynchronize(user);
   if (e2 == hipSuccess) e2 = e3;
+  if (e2 != hipSuccess || e != hipSuccess || rc != RSE_OK)
+    for (auto& q : st) (void)hipStreamSynchronize(q);  // idle before the next call reuses them
   if (verify && ok && hwords && e == hipSuccess && e2 == hipSuccess && rc == RSE_OK)
     for (size_t s = 0; s < stripes.size(); ++s) ok[s] = hwords[s] == 0 ? 1 : 0;
   if (hwords) (void)hipHostFree(hwords);
-  for (auto* ev : {&h2d, &coded, &d2h})
-    for (auto& q : *ev)
-      if (q) (void)hipEventDestroy(q);
-  for (auto& q : st)
-    if (q) (void)hipStreamDestroy(q);
-  if (start) (void)hipEventDestroy(start);
   if (rc) return rc;
   if (e != hipSuccess) return dev_fail(e);
   if (e2 != hipSuccess) return dev_fail(e2);
