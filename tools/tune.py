@@ -36,6 +36,7 @@ def main():
                     help="batch: rse_reconstruct_batch, every stripe its own random pattern "
                          "of len(--erase) erased shards")
     ap.add_argument("--variants", type=int, default=1)
+    ap.add_argument("--variant-list", default="", help="comma list of variants (overrides --variants)")
     ap.add_argument("--bitslice", default="1", help="comma list of RSE_OPT_BITSLICE values")
     ap.add_argument("--shapes", default="", help="gx:gy,gx:gy,... (default: built-in list)")
     ap.add_argument("--erase", default="0,1", help="reconstruct: erased shard indices")
@@ -122,8 +123,10 @@ def main():
     pats = [int(x) for x in args.patterns.split(",")] if args.op != "encode" else [1]
     nts = (0, 1) if not args.nt_only else (1,)
     mixes = [int(x) for x in args.recon_mix.split(",")]
+    vlist = ([int(x) for x in args.variant_list.split(",")] if args.variant_list
+             else list(range(args.variants)))
     configs = [(nt, gx, gy, var, bs, pat, mx) for mx in mixes for pat in pats for bs in bss
-               for var in range(args.variants) for nt in nts for gx, gy in shapes]
+               for var in vlist for nt in nts for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
