@@ -158,7 +158,7 @@ int recon_ns(uint32_t p, int* ns) {
 // kernels' namespace.
 void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t p,
                const std::vector<uint16_t>& rows, int temps) {
-  const netgen::Net net = netgen::build(field, k, p, rows.data(), temps);
+  const netgen::Net net = netgen::build(field, k, p, rows.data(), temps, get_option(23) != 0);
   s += "\nnamespace rse {\nnamespace {\n";
   s += netgen::emit(net, name, rows.data());
   s += "}  // namespace\n}  // namespace rse\n";
@@ -253,7 +253,10 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     s += "    default: break;\n  }\n}\n";
     return s;
   }
-  emit_code(s, "JitCode", field, k, p, rows, field == 16 ? (int)get_option(13) : 0);
+  // GF(2^8) temporaries only above 4 outputs (2 waves/SIMD: room for them; at
+  // 3 waves/SIMD the extra live sources would cost spills)
+  emit_code(s, "JitCode", field, k, p, rows,
+            field == 16 ? (int)get_option(13) : p > 4 ? std::min(16, (int)get_option(13)) : 0);
   char buf[512];
   if (stage == kEnc) {
     // encode/verify kernels (16 KiB and 4 KiB chunks); a later block of a wide
