@@ -303,9 +303,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        0 (default) = 2, or 2..4 */
 #define RSE_OPT_HOST_COPY_2D 21     /* host pipeline (*_host_flat): 1 (default) one 2D copy per run of
                                        equally spaced shards of the caller buffer, 0 one copy per shard */
-#define RSE_OPT_JIT_EXACT8 23       /* GF(2^8) networks built after: 1 (default) temporaries chosen by
-                                       exact fewest-source decompositions (rse_netgen.hpp factor8), 0 the
-                                       pair/triple greedy (A/B) */
+#define RSE_OPT_JIT_EXACT 23        /* run-time networks built after: 1 (default) temporaries chosen by
+                                       exact fewest-source decompositions (rse_netgen.hpp factor8 /
+                                       factor16), 0 the pair/triple greedy (A/B) */
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */

@@ -765,7 +765,7 @@ struct Options {
   int64_t wide_balance = 1;       // wide modules: waves per workgroup rounded to 2, 4, 8
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
   int64_t host_copy_2d = 1;       // host pipeline: 2D copies for runs of a flat buffer's shards
-  int64_t jit_exact8 = 1;         // GF(2^8) run-time networks: exact-decomposition temporaries
+  int64_t jit_exact = 1;          // run-time networks: exact-decomposition temporaries
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1109,7 +1109,7 @@ int set_option(int key, int64_t value) {
     case 19: g_opt.wide_balance = value ? 1 : 0; return 0;
     case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;
     case 21: g_opt.host_copy_2d = value ? 1 : 0; return 0;
-    case 23: g_opt.jit_exact8 = value ? 1 : 0; return 0;
+    case 23: g_opt.jit_exact = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1146,7 +1146,7 @@ int64_t get_option(int key) {
     case 19: return g_opt.wide_balance;
     case 20: return g_opt.wide_occupancy;
     case 21: return g_opt.host_copy_2d;
-    case 23: return g_opt.jit_exact8;
+    case 23: return g_opt.jit_exact;
     default: return -1;
   }
 }

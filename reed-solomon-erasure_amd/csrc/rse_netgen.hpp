@@ -16,7 +16,10 @@
 // with the largest net saving (rows saved - 1 for the temporary), pairs and
 // triples alike, until none saves anything or the budget is used.  For
 // GF(2^16) 20+8 this takes the network from 5816 v_bitop3 (no temporaries)
-// past 4224 (pairs by row count, 16 temporaries; round 1) to ~3600 (32).
+// past 4224 (pairs by row count, 16 temporaries; round 1) to 3592 (32).
+// The default since is factor8 / factor16 below: the same greedy, but every
+// row re-expressed by its exact fewest-source decomposition over the current
+// sources (3144 for 20+8).
 //
 // Used by rse_jit.cpp for the codecs specialised at run time and by
 // rse_gen_tables.cpp, at build time, for the codecs compiled into
@@ -171,12 +174,93 @@ inline int factor8(std::vector<uint64_t>& rows, int budget, std::array<uint8_t, 
   return n;
 }
 
+// GF(2^16): the same with a 65536-entry D.  Candidates are the XORs of two or
+// three current sources (one v_bitop3); a row's new cost needs only D[r] and
+// D[r ^ m].  A decomposition follows D downhill (a source s with
+// D[x ^ s] = D[x] - 1; minimality rules out reusing one).  For GF(2^16) 20+8
+// 3144 ops per chunk against 3592 for factor(); 40+12 in 3-output shares
+// 10728 against 11806.
+inline int factor16(std::vector<uint64_t>& rows, int budget, std::array<uint8_t, 3>* tmp) {
+  std::vector<uint8_t> d(65536, 0xFF), nd(65536);
+  d[0] = 0;
+  std::vector<uint32_t> src;
+  auto add = [&](uint32_t m) {
+    for (uint32_t x = 0; x < 65536; ++x) {
+      const int via = d[x ^ m] == 0xFF ? 0xFF : d[x ^ m] + 1;
+      nd[x] = (uint8_t)std::min<int>(d[x], via);
+    }
+    d.swap(nd);
+    src.push_back(m);
+  };
+  for (int j = 0; j < 16; ++j) add(1u << j);
+  auto decompose = [&](uint32_t x) {
+    uint64_t used = 0;
+    while (x) {
+      bool step = false;
+      for (size_t j = 0; j < src.size() && !step; ++j)
+        if (!((used >> j) & 1u) && d[x ^ src[j]] + 1 == d[x]) {
+          used |= 1ull << j;
+          x ^= src[j];
+          step = true;
+        }
+      if (!step) break;  // cannot happen: d is exact
+    }
+    return used;
+  };
+  std::vector<std::pair<uint32_t, int>> rc;  // distinct rows and their counts
+  {
+    std::vector<uint32_t> v;
+    for (uint64_t r : rows) v.push_back((uint32_t)(r & 0xFFFFu));
+    std::sort(v.begin(), v.end());
+    for (size_t i = 0; i < v.size();) {
+      size_t j = i;
+      while (j < v.size() && v[j] == v[i]) ++j;
+      if (v[i]) rc.push_back({v[i], (int)(j - i)});
+      i = j;
+    }
+  }
+  auto cost_with = [&](uint32_t m) {
+    int c = 0;
+    for (const auto& [r, n] : rc) c += n * ((std::min<int>(d[r], d[r ^ m] + 1) + 1) / 2);
+    return c;
+  };
+  int n = 0, cur = cost_with(0);
+  while (n < budget && n < kMaxTemps) {
+    int best = 0;
+    uint32_t bm = 0;
+    const size_t ns = src.size();
+    auto eval = [&](uint32_t m) {
+      if (d[m] < 2) return;  // zero or already a source
+      const int save = cur - cost_with(m) - 1;
+      if (save > best) {
+        best = save;
+        bm = m;
+      }
+    };
+    for (size_t a = 0; a < ns; ++a)
+      for (size_t b = a + 1; b < ns; ++b) {
+        eval(src[a] ^ src[b]);
+        for (size_t c = b + 1; c < ns; ++c) eval(src[a] ^ src[b] ^ src[c]);
+      }
+    if (!bm) break;
+    const uint64_t parts = decompose(bm);
+    int a[3], w = 0;
+    for (uint64_t q = parts; q && w < 3; q &= q - 1) a[w++] = __builtin_ctzll(q);
+    tmp[n] = {(uint8_t)a[0], (uint8_t)a[1], (uint8_t)(w == 3 ? a[2] : 255)};
+    add(bm);
+    cur = cost_with(0);
+    ++n;
+  }
+  for (uint64_t& r : rows) r = decompose((uint32_t)(r & 0xFFFFu));
+  return n;
+}
+
 // The network of p x k rows (row-major, uint16 elements as in rse_field.hpp).
 // budget: temporaries per input (GF(2^8): per input, shared by its two plane
-// groups, which use the same bit matrices).  exact8: GF(2^8) temporaries by
-// factor8 (default) instead of factor (A/B).
+// groups, which use the same bit matrices).  exact: temporaries by factor8 /
+// factor16 (default) instead of factor (A/B).
 inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int budget,
-                 bool exact8 = true) {
+                 bool exact = true) {
   Net net;
   net.field = field;
   net.np = field == 16 ? 16 : 8;
@@ -205,9 +289,9 @@ inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int bu
       std::vector<uint64_t> r;
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) r.push_back(net.at(o, i, q));
-      net.ntmp[i] = (uint8_t)(field == 8 && exact8
-                                  ? factor8(r, net.temps, &net.tmp[(size_t)i * net.temps])
-                                         : factor(r, net.temps, np, &net.tmp[(size_t)i * net.temps]));
+      std::array<uint8_t, 3>* t = &net.tmp[(size_t)i * net.temps];
+      net.ntmp[i] = (uint8_t)(!exact ? factor(r, net.temps, np, t)
+                              : field == 8 ? factor8(r, net.temps, t) : factor16(r, net.temps, t));
       size_t n = 0;
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) net.at(o, i, q) = r[n++];
