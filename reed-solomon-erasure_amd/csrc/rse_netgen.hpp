@@ -257,8 +257,8 @@ inline int factor16(std::vector<uint64_t>& rows, int budget, std::array<uint8_t,
 
 // The network of p x k rows (row-major, uint16 elements as in rse_field.hpp).
 // budget: temporaries per input (GF(2^8): per input, shared by its two plane
-// groups, which use the same bit matrices).  exact: temporaries by factor8 /
-// factor16 (default) instead of factor (A/B).
+// groups, which use the same bit matrices).  exact: per input, the cheaper of
+// factor8 / factor16 and factor (default); otherwise factor alone (A/B).
 inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int budget,
                  bool exact = true) {
   Net net;
@@ -290,8 +290,25 @@ inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int bu
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) r.push_back(net.at(o, i, q));
       std::array<uint8_t, 3>* t = &net.tmp[(size_t)i * net.temps];
-      net.ntmp[i] = (uint8_t)(!exact ? factor(r, net.temps, np, t)
-                              : field == 8 ? factor8(r, net.temps, t) : factor16(r, net.temps, t));
+      net.ntmp[i] = (uint8_t)factor(r, net.temps, np, t);
+      if (exact) {  // the exact factoring, unless the greedy did better on this input
+        std::vector<uint64_t> r2;
+        for (uint32_t o = 0; o < p; ++o)
+          for (int q = 0; q < np; ++q) r2.push_back(net.at(o, i, q));
+        std::vector<std::array<uint8_t, 3>> t2((size_t)net.temps);
+        const int n2 = field == 8 ? factor8(r2, net.temps, t2.data())
+                                  : factor16(r2, net.temps, t2.data());
+        auto cost = [](const std::vector<uint64_t>& v, int n) {
+          size_t c = (size_t)n;
+          for (uint64_t m : v) c += ((size_t)__builtin_popcountll(m) + 1) / 2;
+          return c;
+        };
+        if (cost(r2, n2) <= cost(r, net.ntmp[i])) {
+          r.swap(r2);
+          for (int x = 0; x < n2; ++x) t[x] = t2[(size_t)x];
+          net.ntmp[i] = (uint8_t)n2;
+        }
+      }
       size_t n = 0;
       for (uint32_t o = 0; o < p; ++o)
         for (int q = 0; q < np; ++q) net.at(o, i, q) = r[n++];
