@@ -53,9 +53,12 @@ def main():
                     help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
+    ap.add_argument("--hog-gib", type=int, default=0,
+                    help="allocate this much device memory first (the bench holds 112 GiB)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="rse_set_option(KEY, VALUE) before the codec is created (repeatable)")
     args = ap.parse_args()
+    hog = torch.empty(args.hog_gib << 30, dtype=torch.uint8, device="cuda") if args.hog_gib else None
     lib = R._lib.load()
     for kv in args.set:
         key, val = (int(x) for x in kv.split("="))
