@@ -947,7 +947,10 @@ struct HostCode {
 // at 21 GB/s against 54 for eight).  A call leaves them idle (it synchronises
 // the caller's stream, which waits for every pipeline stream).  Grown on
 // demand; deliberately never freed (a thread_local destructor could run after
-// the HIP runtime has shut down).
+// the HIP runtime has shut down).  Only rings up to kPipeRingKeep are kept, so
+// a service's worker threads hold at most that much HBM each; a larger ring
+// (wide codecs, big chunks) is allocated for the call and freed after it.
+constexpr size_t kPipeRingKeep = size_t(512) << 20;
 struct PipeRes {
   int nh = 0, ring = 0;
   std::vector<hipStream_t> st;
@@ -993,7 +996,7 @@ hipError_t pipe_res(int nh, int ring, size_t dbytes, PipeRes** out) {
     e = hipEventCreateWithFlags(&r.start, hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
-  if (r.dbytes < dbytes) {
+  if (r.dbytes < dbytes && dbytes <= kPipeRingKeep) {
     if (r.dbuf) (void)hipFree(r.dbuf);  // idle: the previous call synchronised
     r.dbuf = nullptr;
     r.dbytes = 0;
@@ -1030,6 +1033,12 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   const std::vector<hipEvent_t>&h2d = res->h2d, &coded = res->coded, &d2h = res->d2h;
   hipEvent_t start = res->start;
   uint8_t* dbuf = res->dbuf;
+  uint8_t* call_ring = nullptr;  // a ring too big to keep: this call's own
+  if (res->dbytes < ring * nbuf * chunk) {
+    e = hipMallocAsync(reinterpret_cast<void**>(&call_ring), ring * nbuf * chunk, user);
+    if (e != hipSuccess) return dev_fail(e);
+    dbuf = call_ring;
+  }
   uint32_t *dwords = nullptr, *hwords = nullptr;
   if (verify) {  // one mismatch word per stripe
     const size_t wb = stripes.size() * sizeof(uint32_t);
@@ -1111,6 +1120,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
     e2 = hipMemcpyAsync(hwords, dwords, stripes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         user);
   if (dwords) (void)hipFreeAsync(dwords, user);
+  if (call_ring) (void)hipFreeAsync(call_ring, user);
   const hipError_t e3 = hipStreamSynchronize(user);
   if (e2 == hipSuccess) e2 = e3;
   if (e2 != hipSuccess || e != hipSuccess || rc != RSE_OK)
