@@ -158,13 +158,13 @@ __device__ __forceinline__ void unslice(uint32_t (&pl)[16], u32x4 (&v)[4]) {
 
 template <bool NT>
 __device__ __forceinline__ u32x4 ldv(const uint8_t* p) {
-  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  const gptr<const u32x4> q = (gptr<const u32x4>)(p);
   if constexpr (NT) return __builtin_nontemporal_load(q);
   else return *q;
 }
 template <bool NT>
 __device__ __forceinline__ void stv(uint8_t* p, u32x4 v) {
-  u32x4* q = reinterpret_cast<u32x4*>(p);
+  const gptr<u32x4> q = (gptr<u32x4>)(p);
   if constexpr (NT) __builtin_nontemporal_store(v, q);
   else *q = v;
 }

@@ -104,24 +104,34 @@ __device__ __forceinline__ void write_tab(uint4* q, uint32_t* t2, int idx, const
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// Shard accesses go through global-address-space pointers. Shard pointers read
+// from memory (the per-stripe descriptors of reconstruct_batch and of the
+// table path's batched reconstruct) are generic pointers, which the compiler
+// otherwise accesses with flat_load/flat_store: both counters to wait on and no
+// global addressing. Shards are always device-visible global memory.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+
 // 16-byte global access.  NT = non-temporal (streaming) hint: every shard byte
 // is touched exactly once, so there is nothing to keep in L2/MALL.
 template <bool NT = false>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
   if constexpr (NT) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    const u32x4 v = __builtin_nontemporal_load((gptr<const u32x4>)(p));
     return make_uint4(v.x, v.y, v.z, v.w);
   } else {
-    return *reinterpret_cast<const uint4*>(p);
+    const u32x4 v = *(gptr<const u32x4>)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 template <bool NT = false>
 __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
   if constexpr (NT) {
     const u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+    __builtin_nontemporal_store(w, (gptr<u32x4>)(p));
   } else {
-    *reinterpret_cast<uint4*>(p) = v;
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    *(gptr<u32x4>)(p) = w;
   }
 }
 __device__ __forceinline__ bool ne4(uint4 a, uint4 b) {

@@ -53,6 +53,9 @@ def main():
                     help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
+    ap.add_argument("--batch-cycle", type=int, default=0,
+                    help="batch: stripes alternate between this many fixed patterns "
+                         "(rotations of --erase) instead of random ones (0)")
     ap.add_argument("--hog-gib", type=int, default=0,
                     help="allocate this much device memory first (the bench holds 112 GiB)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
@@ -104,7 +107,10 @@ def main():
     rng = np.random.default_rng(5)
     batch_present = np.ones((S, k + p), bool)
     for s_ in range(S):
-        batch_present[s_, rng.choice(k + p, len(erased), replace=False)] = False
+        if args.batch_cycle:
+            batch_present[s_, [(e + s_ % args.batch_cycle) % (k + p) for e in erased]] = False
+        else:
+            batch_present[s_, rng.choice(k + p, len(erased), replace=False)] = False
 
     def op():
         if args.op == "encode":
