@@ -32,10 +32,11 @@ constexpr int kBsDefaultVariant8 = 1, kBsDefaultVariant16 = 0;
 // shared subexpressions (kernel variant 9, for A/B).
 #include "rse_bs_tables.inc"
 
-template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false>
+template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false,
+          bool CE = false>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
-  bitslice_body<C, NT, SB, XC, XM, WT, W4>(a, chunks_per_stripe);
+  bitslice_body<C, NT, SB, XC, XM, WT, W4, false, CE>(a, chunks_per_stripe);
 }
 
 template <class C, int D>
@@ -322,6 +323,8 @@ struct BsShape {
                       // write-through (sc1) stores ([8][0] sc1, [8][1] sc1 nt), 9 = 1
                       // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
   BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
+  BsFn chk;           // the default variant for the check modes (verify): the
+                      // stored parity loaded before un-slicing (store_outputs CE)
   BsRecFn rec[3][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
                       // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
@@ -351,6 +354,7 @@ constexpr BsDescFn rec_desc_fn() {
      bitslice_kernel<C, true, true, false, false, true>},                          \
     {nullptr, bitslice_kernel<CP, true, true, false>}},                            \
    bitslice_kernel<C, true, true, false, false, false, true>,                      \
+   bitslice_kernel<C, true, C::NP == 8, false, false, false, false, true>,         \
    {{rec_fn<C, 1, 0>(), rec_fn<C, 2, 0>(), rec_fn<C, 4, 0>(), rec_fn<C, 8, 0>()},  \
     {rec_fn<C, 1, 1>(), rec_fn<C, 2, 1>(), rec_fn<C, 4, 1>(), rec_fn<C, 8, 1>()},  \
     {rec_fn<C, 1, 2>(), rec_fn<C, 2, 2>(), rec_fn<C, 4, 2>(), rec_fn<C, 8, 2>()}}, \
@@ -389,6 +393,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                                      : (field == 16 ? kBsDefaultVariant16 : kBsDefaultVariant8);
     f16 = sh.fn[v][nt ? 1 : 0];
     if (!f16) f16 = sh.fn[v][1];
+    if (a.mode != kStore && vopt < 0 && nt) f16 = sh.chk;
     vopt_used = v;
     f4 = sh.w4;
     compiled = true;

@@ -248,8 +248,12 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
 // (kStore), compare them with the stored parity (kCheck), or both.
 // A: the argument block (CodeArgs, or a wide codec's WideArgs: O0 is then the
 // first output of the wave's share).
+// CE: check modes load the stored parity before un-slicing, which then covers
+// part of its latency (a one-stripe verify: 60 -> 52 us per 10+4 x 16 MiB
+// call).  A separate instantiation for the check kernels: in the store-mode
+// kernel the reordered code cost the headline encode 1.2 % (same box A/B).
 template <class C, bool NT, bool WT = false, uint32_t S = kBsBlock * 16, int O0 = 0,
-          class A = CodeArgs>
+          class A = CodeArgs, bool CE = false>
 __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const A& a,
                                               uint64_t off, uint32_t mode, bool& diff) {
 #pragma unroll
@@ -257,6 +261,8 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
     uint32_t pl[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) pl[q] = acc[o * 16 + q];
+    u32x4 w[4];
+    if (CE && mode != kStore) load4<NT, S>(w, a.cmp[O0 + o] + off);
     u32x4 v[4];
     unslice<typename C::Field>(pl, v);
 #pragma unroll
@@ -264,8 +270,8 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
       const uint64_t o16 = off + j * S;
       if (mode != kCheck) stv_policy<NT, WT>(a.out[O0 + o] + o16, v[j]);
       if (mode != kStore) {
-        const u32x4 w = ldv<NT>(a.cmp[O0 + o] + o16);
-        diff |= (w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w);
+        if (!CE) w[j] = ldv<NT>(a.cmp[O0 + o] + o16);
+        diff |= (w[j].x != v[j].x) | (w[j].y != v[j].y) | (w[j].z != v[j].z) | (w[j].w != v[j].w);
       }
     }
   }
@@ -323,7 +329,7 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 //      loaded and sliced into the accumulators first -- the blocks of a wide
 //      codec's parity matrix, input chunk after input chunk (rse_jit.cpp).
 template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false,
-          bool ACC = false>
+          bool ACC = false, bool CE = false>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
   static_assert(!(XC && W4), "cross-chunk prefetch is for 16 KiB chunks");
   static_assert(!(XC && ACC), "cross-chunk prefetch is for store mode");
@@ -364,7 +370,7 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
       }
     }
     code_inputs<C, NT, SB, XC, 0, S, ACC>(acc, cur, a, off, next_off);
-    store_outputs<C, NT, WT, S>(acc, a, off, mode, diff);
+    store_outputs<C, NT, WT, S, 0, CodeArgs, CE>(acc, a, off, mode, diff);
     if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
       flag_mismatch(a.mismatch + c / chunks_per_stripe);
       diff = false;
