@@ -1081,6 +1081,14 @@ __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
   }
 }
 
+// A stripe's descriptor through the constant address space: the planner wrote
+// it before this kernel, nothing writes it during, so its fields can be scalar
+// loads (through a generic pointer they were vector loads + readfirstlane).
+__device__ __forceinline__ const BsReconArgs& desc_at(const BsReconArgs* descs, uint64_t s) {
+  using CPtr = const __attribute__((address_space(4))) BsReconArgs*;
+  return *(const BsReconArgs*)((CPtr)descs + s);
+}
+
 // Reconstruct body over per-stripe argument blocks (descs[s], written by the
 // device planner of rse_reconstruct_batch: every stripe its own erasure
 // pattern).  A workgroup rebuilds its mixing tables when its stripe changes.
@@ -1092,7 +1100,7 @@ __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __re
     const uint64_t total = chunks_per_stripe * n_stripes;
     for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
       const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-      const BsReconArgs& a = descs[stripe];
+      const BsReconArgs& a = desc_at(descs, stripe);
       if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
       recon_chunk<C, NT, NS, MIX>(a, nullptr, nullptr, chunk * kBsChunk + threadIdx.x * 16u);
     }
@@ -1105,7 +1113,7 @@ __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __re
   const uint64_t total = chunks_per_stripe * n_stripes;
   for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
     const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
-    const BsReconArgs& a = descs[stripe];
+    const BsReconArgs& a = desc_at(descs, stripe);
     if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
     if (stripe != built) {
       __syncthreads();  // every lane is done with the previous stripe's tables
