@@ -196,7 +196,10 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
 // the grid codes stripe y with its own shard pointers and coefficient rows.
 template <bool NT>
 __global__ __launch_bounds__(kBlock, 3) void gf8_code_desc_kernel(const CodeArgs* __restrict__ descs) {
-  const CodeArgs& a = descs[blockIdx.y];
+  // through the constant address space: scalar loads of the descriptor's fields
+  // (written by the planner kernel before this one, never during it)
+  using CPtr = const __attribute__((address_space(4))) CodeArgs*;
+  const CodeArgs& a = *(const CodeArgs*)((CPtr)descs + blockIdx.y);
   if (a.n_out == 0) return;  // uniform: nothing missing in this stripe
   gf8_code_impl<8, kMaxOut, false, NT, 1>(a, 0, 1);
 }
