@@ -76,6 +76,82 @@ def init_dist(args):
     return world, rank, local
 
 
+def collective_timeout_s() -> float:
+    return float(os.environ.get("RSE_BENCH_COLLECTIVE_TIMEOUT", "300"))
+
+
+def init_collective(world: int, rank: int, local: int, rehearsal: bool) -> str:
+    """Joins the process group and proves it with one all-reduce, or ends this
+    rank with a non-zero status -- never a hang.  RCCL ("nccl") with one GPU
+    per rank; gloo for the one-GPU rehearsal and on a host without a GPU.  The
+    rendezvous and the first collective run under a deadline
+    (RSE_BENCH_COLLECTIVE_TIMEOUT, default 300 s): a rank whose peers never
+    arrive, or whose RCCL init or first all-reduce fails, exits with status 4
+    (an error) or 5 (the deadline) after saying so, so the driver sees every
+    rank fail instead of waiting forever."""
+    import datetime
+    import threading
+
+    import torch
+    import torch.distributed as dist
+    backend = "gloo" if rehearsal or not torch.cuda.is_available() else "nccl"
+    timeout = collective_timeout_s()
+
+    def expire():
+        print(f"rank {rank}/{world}: {backend} rendezvous or first all-reduce not done after "
+              f"{timeout:.0f} s; exiting", file=sys.stderr, flush=True)
+        os._exit(5)
+
+    dog = threading.Timer(timeout, expire)
+    dog.daemon = True
+    dog.start()
+    try:
+        kw = {"timeout": datetime.timedelta(seconds=timeout)}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        t = torch.ones(1, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        if int(t.item()) != world:
+            raise RuntimeError(f"all-reduce of ones gave {t.item()}, not {world}")
+    except Exception as e:  # noqa: BLE001 -- any failure ends the rank
+        print(f"rank {rank}/{world}: {backend} init failed: {e!r}", file=sys.stderr, flush=True)
+        os._exit(4)
+    finally:
+        dog.cancel()
+    return backend
+
+
+def device_identity(local: int) -> dict:
+    """What this rank computes on: the GPU's PCI address and UUID (so a
+    multi-GPU line shows N ranks on N distinct GPUs), or the host CPU."""
+    import torch
+    if not torch.cuda.is_available():
+        return {"device": "cpu", "host": os.uname().nodename, "pid": os.getpid()}
+    p = torch.cuda.get_device_properties(local)
+    pci = None
+    if hasattr(p, "pci_bus_id"):
+        pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    uuid = getattr(p, "uuid", None)
+    return {"device": f"cuda:{local}", "name": p.name, "pci": pci,
+            "uuid": str(uuid) if uuid is not None else None}
+
+
+def collective_info(world: int, local: int, rehearsal: bool) -> dict:
+    """What the collective saw: backend, world size, and every rank's device
+    (gathered), with whether they are all distinct GPUs."""
+    ident = device_identity(local)
+    if world == 1:
+        return {"backend": None, "world_size": 1, "rank_devices": [ident],
+                "distinct_gpus": ident["device"] != "cpu", "rehearsal": rehearsal}
+    import torch.distributed as dist
+    ids = [None] * world
+    dist.all_gather_object(ids, ident)
+    keys = {(i.get("pci"), i.get("uuid")) for i in ids if i["device"] != "cpu"}
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "rank_devices": ids, "distinct_gpus": len(keys) == world, "rehearsal": rehearsal}
+
+
 def reduce_timing(elapsed: float, world: int, device=None) -> float:
     """Job time = the slowest rank's timed region (all_reduce MAX).  The only
     collective in the benchmark; stripes never cross ranks."""
@@ -303,11 +379,9 @@ def main(argv=None):
         local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_collective(world, rank, local, rehearsal)
     coll_dev = None if rehearsal else "cuda"
+    coll = collective_info(world, local, rehearsal)
     import reed_solomon_erasure as R
     from reed_solomon_erasure.core import fill_splitmix, last_kernel
 
@@ -402,6 +476,7 @@ def main(argv=None):
                 "kernel": kernel, "kernel_id": kernel_id,
                 "kernel_ms_per_launch": round(mean_ms, 4),
                 "kernel_ms_per_launch_per_rank": [round(x, 4) for x in rank_ms],
+                "kernel_ms_per_launch_min_max": [round(min(rank_ms), 4), round(max(rank_ms), 4)],
                 "algorithmic_bytes_per_launch": int(per_launch_bytes)}
         cpu = {}
         if world == 1 and not args.no_cpu:
@@ -419,6 +494,7 @@ def main(argv=None):
                        "parity_check_vs_reference": check,
                        "parity_check_per_rank": [int(x) for x in verdicts],
                        "parity_checked_stripes_rank0": checked},
+            "collective": coll,
             "roofline": roof, "cpu_baseline": cpu.get("cpu_baseline"),
         }
         for key in ("cpu_baseline_legs", "cpu_host"):

@@ -8,7 +8,9 @@
  * native FFI kernel reedsolomon_gal_mul(_xor) (simd_c/reedsolomon.h:30-42).
  *
  * Conventions (mirroring the reference; see INTEGRATION.md for the Rust binding):
- *  - Shards are DEVICE pointers (HBM) unless the function name ends in _host.
+ *  - Shards are DEVICE pointers (HBM) unless the function name ends in _host;
+ *    the Field/FFI slice hooks (rse_gal_mul*, rse_gf8/gf16_mul_slice) take
+ *    host or device memory.
  *  - Lengths are in field ELEMENTS, like Rust slice lengths: bytes for GF(2^8),
  *    2-byte [u8;2] elements ({coefficient of x, constant}, galois_16.rs:49-51)
  *    for GF(2^16).
@@ -184,24 +186,38 @@ int rse_code_shards(int field, const uint8_t *rows, size_t n_out, size_t n_in,
 int rse_code_shards_host(int field, const uint8_t *rows, size_t n_out, size_t n_in,
                          const void *const *inputs, void *const *outputs, size_t len,
                          int accumulate, rse_stream_t stream);
-/* galois_8 mul_slice / mul_slice_xor (galois_8.rs:291-327) on device memory:
- * out = c*in (or out ^= c*in) over GF(2^8), asynchronous on `stream`. */
+/* The Field/FFI slice hooks below take in/out WHEREVER THEY LIVE, as the
+ * reference's callers do (they pass host slices): the library asks the runtime
+ * (hipPointerGetAttributes) where each buffer is.
+ *  - in and out both device memory of one device (hipMalloc, managed): the
+ *    kernel, asynchronous on `stream`;
+ *  - either in host memory (pageable, pinned or registered): the host
+ *    pipeline -- H2D, kernel, D2H -- synchronous: out holds the result on
+ *    return.  Pinned memory overlaps the copies; pageable memory works.
+ * galois_8 mul_slice / mul_slice_xor (galois_8.rs:291-327): out = c*in (or
+ * out ^= c*in) over GF(2^8). */
 int rse_gf8_mul_slice(uint8_t c, const void *in, void *out, size_t len, int xor_into,
                       rse_stream_t stream);
 /* The reference FFI kernel itself, same signature and contract:
  * reedsolomon_gal_mul / reedsolomon_gal_mul_xor (simd_c/reedsolomon.h:30-42,
  * bound at galois_8.rs:267-283).  low/high are the coefficient's 16-entry
- * nibble tables (MUL_TABLE_LOW/HIGH[c], build.rs:75-94; host memory), in/out
- * DEVICE memory.  Returns the bytes processed -- always len (no scalar tail
- * for the caller to finish, galois_8.rs:301-304) -- or 0 on error.  Runs on
- * the null stream and returns when done, as the CPU kernel does. */
+ * nibble tables (MUL_TABLE_LOW/HIGH[c], build.rs:75-94; host memory); in/out
+ * host or device memory as above.  Returns when out holds the result, as the
+ * CPU kernel does, having waited only for its own work (a library stream, not
+ * the whole device).  Returns the bytes processed: len (no scalar tail for
+ * the caller to finish, galois_8.rs:301-304), or 0 on a device failure with
+ * nothing written (rse_last_device_error says why).  On host slices a 0 lets
+ * the reference's tail loop do the whole slice on the CPU, which is correct;
+ * a caller passing DEVICE slices must treat 0 (for len > 0) as an error and
+ * never run a host tail on them. */
 size_t rse_gal_mul(const uint8_t *low, const uint8_t *high, const uint8_t *in, uint8_t *out,
                    size_t len);
 size_t rse_gal_mul_xor(const uint8_t *low, const uint8_t *high, const uint8_t *in, uint8_t *out,
                        size_t len);
 /* galois_16's Field::mul_slice / mul_slice_add (the trait defaults,
- * lib.rs:99-118) on device memory: c is one [u8;2] element {coefficient of x,
- * constant}; len counts elements.  add_into = 0: out = c*in, 1: out += c*in. */
+ * lib.rs:99-118), host or device memory as above: c is one [u8;2] element
+ * {coefficient of x, constant}; len counts elements.  add_into = 0:
+ * out = c*in, 1: out += c*in. */
 int rse_gf16_mul_slice(const uint8_t *c, const void *in, void *out, size_t len, int add_into,
                        rse_stream_t stream);
 
@@ -309,6 +325,10 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */
+#define RSE_OPT_SCRATCH_LIVE 24     /* read-only: per-call device resource sets (verdict words, library
+                                       stream, host-pipeline streams/events/ring) in existence, leased or
+                                       idle.  Calls lease one from a process-wide pool that keeps at most 4
+                                       idle per device, so threads that come and go leave nothing behind */
 /* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */

@@ -304,42 +304,185 @@ hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32
   return hipGetLastError();
 }
 
-// Per-thread, per-device verdict words for run_check, in pinned host memory
-// mapped into the device (fine-grained, coherent): the check kernels store 1
-// into them directly (rse_device.hpp flag_mismatch), so a verify is one
-// launch and one synchronisation -- no memset or D2H copy of the verdict.
-// Allocated once and grown on demand (verify is synchronous, so a thread's
-// words are free again when it returns).  Deliberately never freed: a
-// thread_local destructor could run after the HIP runtime has shut down.
-struct CheckWords {
-  uint32_t* h = nullptr;  // host view
-  uint32_t* d = nullptr;  // device view of the same words
+// ------------------------------------------------------------- scratch pool
+// The device resources of the synchronous calls, kept between calls because
+// creating them per call costs milliseconds (a one-stripe 10+4 x 16 MiB host
+// encode ran at 21 GB/s against 54 for eight before they were kept):
+//  * verify verdict words, in pinned host memory mapped into the device
+//    (fine-grained, coherent): the check kernels store 1 into them directly
+//    (rse_device.hpp flag_mismatch), so a verify is one launch and one
+//    synchronisation -- no memset or D2H copy of the verdict;
+//  * a library-owned stream for calls that must wait for their own work only
+//    (rse_gal_mul: the reference kernel returns when done);
+//  * the host pipeline's streams, events and device ring.
+// A call leases one Scratch of its device from a process-wide pool and
+// returns it idle when it has synchronised, so a Scratch is never shared by
+// two calls at once.  The pool keeps at most kIdleScratch idle ones per device
+// and destroys the surplus on return: threads that come and go (a service's
+// or Python's thread pool) leave nothing behind, and a burst of N concurrent
+// calls holds N leases only while it lasts.  Rings above kPipeRingKeep
+// (wide codecs, big chunks) are never kept: such a call allocates its own.
+// The pool itself is never destroyed (a static destructor could run after
+// the HIP runtime has shut down); idle resources end with the process.
+constexpr int kMaxDev = 64;
+constexpr size_t kIdleScratch = 4;
+constexpr size_t kPipeRingKeep = size_t(512) << 20;
+
+struct Scratch {
+  int dev = 0;
+  uint32_t* wh = nullptr;  // verdict words, host view
+  uint32_t* wd = nullptr;  // device view of the same words
   size_t words = 0;
+  hipStream_t own = nullptr;
+  int nh = 0, ring = 0;  // host pipeline: nh H2D streams + kernel + D2H
+  std::vector<hipStream_t> st;
+  std::vector<hipEvent_t> h2d, coded, d2h;
+  hipEvent_t start = nullptr;
+  uint8_t* dbuf = nullptr;
+  size_t dbytes = 0;
 };
 
-hipError_t check_words(size_t words, CheckWords** out) {
-  constexpr int kMaxDev = 64;
-  thread_local CheckWords per_dev[kMaxDev];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
-  CheckWords& w = per_dev[dev];
-  if (w.words < words) {
-    const size_t n = std::max<size_t>(words, 256);
-    uint32_t *h = nullptr, *d = nullptr;
-    e = hipHostMalloc(reinterpret_cast<void**>(&h), n * sizeof(uint32_t),
-                      hipHostMallocMapped | hipHostMallocCoherent);
+void drop_pipe_streams(Scratch& s) {
+  for (auto& q : s.st) (void)hipStreamDestroy(q);
+  for (auto* ev : {&s.h2d, &s.coded, &s.d2h})
+    for (auto& q : *ev) (void)hipEventDestroy(q);
+  s.st.clear();
+  s.h2d.clear();
+  s.coded.clear();
+  s.d2h.clear();
+  s.nh = s.ring = 0;
+}
+
+void destroy_scratch(Scratch* s) {  // idle: its last call synchronised
+  drop_pipe_streams(*s);
+  if (s->start) (void)hipEventDestroy(s->start);
+  if (s->own) (void)hipStreamDestroy(s->own);
+  if (s->dbuf) (void)hipFree(s->dbuf);
+  if (s->wh) (void)hipHostFree(s->wh);
+  delete s;
+}
+
+struct ScratchPool {
+  std::mutex mu;
+  std::vector<Scratch*> idle[kMaxDev];
+  std::atomic<int64_t> live{0};  // Scratch objects in existence (tests: RSE_OPT_SCRATCH_LIVE)
+};
+ScratchPool& scratch_pool() {
+  static ScratchPool& p = *new ScratchPool;
+  return p;
+}
+
+// One Scratch of the current device for the duration of a call.
+class Lease {
+ public:
+  Lease() = default;
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+  ~Lease() {
+    if (!s_) return;
+    ScratchPool& pool = scratch_pool();
+    {
+      std::lock_guard<std::mutex> g(pool.mu);
+      auto& idle = pool.idle[s_->dev];
+      if (idle.size() < kIdleScratch) {
+        idle.push_back(s_);
+        return;
+      }
+    }
+    --pool.live;
+    destroy_scratch(s_);
+  }
+  hipError_t acquire() {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    ScratchPool& pool = scratch_pool();
+    {
+      std::lock_guard<std::mutex> g(pool.mu);
+      auto& idle = pool.idle[dev];
+      if (!idle.empty()) {
+        s_ = idle.back();
+        idle.pop_back();
+        return hipSuccess;
+      }
+    }
+    s_ = new Scratch;
+    s_->dev = dev;
+    ++pool.live;
+    return hipSuccess;
+  }
+  Scratch* operator->() const { return s_; }
+  Scratch* get() const { return s_; }
+
+ private:
+  Scratch* s_ = nullptr;
+};
+
+hipError_t lease_words(Scratch* s, size_t words) {
+  if (s->words >= words) return hipSuccess;
+  const size_t n = std::max<size_t>(words, 256);
+  uint32_t *h = nullptr, *d = nullptr;
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), n * sizeof(uint32_t),
+                               hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return e;
+  e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return e;
+  }
+  if (s->wh) (void)hipHostFree(s->wh);  // idle: the previous call has synchronised
+  s->wh = h;
+  s->wd = d;
+  s->words = n;
+  return hipSuccess;
+}
+
+hipError_t lease_own_stream(Scratch* s, hipStream_t* out) {
+  if (!s->own) {
+    const hipError_t e = hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  *out = s->own;
+  return hipSuccess;
+}
+
+// The host pipeline's streams and events for (nh, ring), and a kept ring of
+// dbytes if that is at most kPipeRingKeep.
+hipError_t lease_pipe(Scratch* r, int nh, int ring, size_t dbytes) {
+  hipError_t e = hipSuccess;
+  if (r->nh != nh || r->ring != ring) {
+    drop_pipe_streams(*r);
+    for (int i = 0; i < nh + 2 && e == hipSuccess; ++i) {
+      hipStream_t q = nullptr;
+      e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+      if (e == hipSuccess) r->st.push_back(q);
+    }
+    for (auto* ev : {&r->h2d, &r->coded, &r->d2h})
+      for (int i = 0; i < ring && e == hipSuccess; ++i) {
+        hipEvent_t q = nullptr;
+        e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
+        if (e == hipSuccess) ev->push_back(q);
+      }
     if (e != hipSuccess) {
-      (void)hipHostFree(h);
+      drop_pipe_streams(*r);
       return e;
     }
-    if (w.h) (void)hipHostFree(w.h);  // the previous call has synchronised
-    w = CheckWords{h, d, n};
+    r->nh = nh;
+    r->ring = ring;
   }
-  *out = &w;
+  if (!r->start) {
+    e = hipEventCreateWithFlags(&r->start, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  if (r->dbytes < dbytes && dbytes <= kPipeRingKeep) {
+    if (r->dbuf) (void)hipFree(r->dbuf);  // idle: the previous call synchronised
+    r->dbuf = nullptr;
+    r->dbytes = 0;
+    e = hipMalloc(reinterpret_cast<void**>(&r->dbuf), dbytes);
+    if (e != hipSuccess) return e;
+    r->dbytes = dbytes;
+  }
   return hipSuccess;
 }
 
@@ -347,18 +490,20 @@ hipError_t check_words(size_t words, CheckWords** out) {
 // ok[0], or ok[s] for every stripe when j.per_stripe.
 int run_check(Job j, hipStream_t s, int* ok) {
   const size_t words = j.per_stripe ? j.n_stripes : 1;
-  CheckWords* w = nullptr;
-  RSE_HIP(check_words(words, &w));
-  std::memset(w->h, 0, words * sizeof(uint32_t));  // no kernel of this thread uses them now
-  j.mismatch = w->d;
+  Lease lease;
+  RSE_HIP(lease.acquire());
+  RSE_HIP(lease_words(lease.get(), words));
+  uint32_t* wh = lease->wh;
+  std::memset(wh, 0, words * sizeof(uint32_t));  // leased: no kernel uses them now
+  j.mismatch = lease->wd;
   int rc = run_job(j, s);
-  // kernels already queued may still store into this thread's words: drain
-  // them before the words can be reused by the thread's next verify
+  // kernels already queued may still store into the words: drain them before
+  // the lease returns them to the pool
   const hipError_t se = hipStreamSynchronize(s);
   if (rc != RSE_OK) return rc;
   RSE_HIP(se);
   for (size_t i = 0; i < words; ++i)
-    ok[i] = reinterpret_cast<volatile uint32_t*>(w->h)[i] == 0 ? 1 : 0;
+    ok[i] = reinterpret_cast<volatile uint32_t*>(wh)[i] == 0 ? 1 : 0;
   return RSE_OK;
 }
 
@@ -732,7 +877,7 @@ int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens
 }
 
 int host_code(int field, const Rows& rows, const void* const* in, void* const* out, size_t len_bytes,
-              bool accumulate, hipStream_t s);
+              bool accumulate, hipStream_t s, bool any_mem = false);
 
 // host: the shards are in host memory (rse_encode_sep_host): same validation,
 // then the host pipeline instead of device launches.
@@ -907,7 +1052,8 @@ void host_sets(uint32_t k, uint32_t T, uint32_t p, HostOp op, bool accumulate,
 // spaced are not one buffer).
 template <class HostPtr>
 hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<uint32_t>& idx,
-                       HostPtr host, size_t off, size_t sz, bool flat, hipStream_t s) {
+                       HostPtr host, size_t off, size_t sz, bool flat, bool any_mem,
+                       hipStream_t s) {
   hipError_t e = hipSuccess;
   if (!rse::get_option(RSE_OPT_HOST_COPY_2D)) flat = false;
   for (size_t a = 0; a < idx.size() && e == hipSuccess;) {
@@ -924,7 +1070,10 @@ hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<
     const size_t rows = b - a;
     if (rows == 1)
       e = hipMemcpyAsync(h2d ? d : h, h2d ? h : d, sz,
-                         h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s);
+                         any_mem ? hipMemcpyDefault
+                         : h2d   ? hipMemcpyHostToDevice
+                                 : hipMemcpyDeviceToHost,
+                         s);
     else if (h2d)
       e = hipMemcpy2DAsync(d, chunk, h, (size_t)pitch, sz, rows, hipMemcpyHostToDevice, s);
     else
@@ -934,79 +1083,15 @@ hipError_t copy_shards(bool h2d, uint8_t* dset, size_t chunk, const std::vector<
   return e;
 }
 
-// The low-level op (rse_code_shards_host): rows over n_in inputs.
+// The low-level op (rse_code_shards_host): rows over n_in inputs.  any_mem:
+// some of the caller's buffers may be device memory (the Field/FFI hooks on
+// mixed arguments), so the copies let the runtime infer their direction.
 struct HostCode {
   int field;
   const Rows* rows;
   bool accumulate;
+  bool any_mem = false;
 };
-
-// The pipeline's streams, events and device ring, kept per thread and device
-// between calls (creating 4 streams, 12 events and a ring of up to hundreds of
-// MiB per call cost milliseconds: a one-stripe 10+4 x 16 MiB host encode ran
-// at 21 GB/s against 54 for eight).  A call leaves them idle (it synchronises
-// the caller's stream, which waits for every pipeline stream).  Grown on
-// demand; deliberately never freed (a thread_local destructor could run after
-// the HIP runtime has shut down).  Only rings up to kPipeRingKeep are kept, so
-// a service's worker threads hold at most that much HBM each; a larger ring
-// (wide codecs, big chunks) is allocated for the call and freed after it.
-constexpr size_t kPipeRingKeep = size_t(512) << 20;
-struct PipeRes {
-  int nh = 0, ring = 0;
-  std::vector<hipStream_t> st;
-  std::vector<hipEvent_t> h2d, coded, d2h;
-  hipEvent_t start = nullptr;
-  uint8_t* dbuf = nullptr;
-  size_t dbytes = 0;
-};
-
-hipError_t pipe_res(int nh, int ring, size_t dbytes, PipeRes** out) {
-  constexpr int kMaxDev = 64;
-  thread_local PipeRes per_dev[kMaxDev];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
-  PipeRes& r = per_dev[dev];
-  if (r.nh != nh || r.ring != ring) {
-    for (auto& q : r.st) (void)hipStreamDestroy(q);
-    for (auto* ev : {&r.h2d, &r.coded, &r.d2h})
-      for (auto& q : *ev) (void)hipEventDestroy(q);
-    r.st.clear();
-    r.h2d.clear();
-    r.coded.clear();
-    r.d2h.clear();
-    r.nh = r.ring = 0;
-    for (int i = 0; i < nh + 2 && e == hipSuccess; ++i) {
-      hipStream_t q = nullptr;
-      e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
-      if (e == hipSuccess) r.st.push_back(q);
-    }
-    for (auto* ev : {&r.h2d, &r.coded, &r.d2h})
-      for (int i = 0; i < ring && e == hipSuccess; ++i) {
-        hipEvent_t q = nullptr;
-        e = hipEventCreateWithFlags(&q, hipEventDisableTiming);
-        if (e == hipSuccess) ev->push_back(q);
-      }
-    if (e != hipSuccess) return e;
-    r.nh = nh;
-    r.ring = ring;
-  }
-  if (!r.start) {
-    e = hipEventCreateWithFlags(&r.start, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-  }
-  if (r.dbytes < dbytes && dbytes <= kPipeRingKeep) {
-    if (r.dbuf) (void)hipFree(r.dbuf);  // idle: the previous call synchronised
-    r.dbuf = nullptr;
-    r.dbytes = 0;
-    e = hipMalloc(reinterpret_cast<void**>(&r.dbuf), dbytes);
-    if (e != hipSuccess) return e;
-    r.dbytes = dbytes;
-  }
-  *out = &r;
-  return hipSuccess;
-}
 
 // Runs `op` over `bytes` of every shard of every stripe (codec ops: `c`;
 // kCode: `code`).  verify ops: ok[s] receives stripe s's verdict.
@@ -1020,14 +1105,16 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   const size_t nchunks = per_stripe * stripes.size();
   const bool verify = op == HostOp::kVerify || op == HostOp::kVerifyBuf;
   const bool low = op == HostOp::kCode;
+  const bool any_mem = low && code->any_mem;
   const int field = low ? code->field : c->field;
   const size_t k = low ? code->rows->n_in : c->k;
   const size_t T = low ? k + code->rows->n_out : c->total;
   const size_t p = T - k, es = field == RSE_FIELD_GF16 ? 2 : 1;
   const size_t nbuf = T + (op == HostOp::kVerifyBuf ? p : 0);  // shards per slot
-  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H (cached: PipeRes)
-  PipeRes* res = nullptr;
-  hipError_t e = pipe_res(nh, ring, ring * nbuf * chunk, &res);
+  // streams: [0, nh) H2D, nh kernel, nh + 1 D2H (leased: Scratch)
+  Lease res;
+  hipError_t e = res.acquire();
+  if (e == hipSuccess) e = lease_pipe(res.get(), nh, ring, ring * nbuf * chunk);
   if (e != hipSuccess) return dev_fail(e);
   const std::vector<hipStream_t>& st = res->st;
   const std::vector<hipEvent_t>&h2d = res->h2d, &coded = res->coded, &d2h = res->d2h;
@@ -1075,7 +1162,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
       return static_cast<uint8_t*>(i < T ? hs.sh[i] : hs.buf[i - T]);
     };
     if (ci >= (size_t)ring) e = hipStreamWaitEvent(hst, d2h[b], 0);  // slot drained
-    if (e == hipSuccess) e = copy_shards(true, set, chunk, up, host, off, sz, hs.flat, hst);
+    if (e == hipSuccess) e = copy_shards(true, set, chunk, up, host, off, sz, hs.flat, any_mem, hst);
     if (e == hipSuccess) e = hipEventRecord(h2d[b], hst);
     if (e == hipSuccess) e = hipStreamWaitEvent(kst, h2d[b], 0);
     if (e != hipSuccess) break;
@@ -1106,7 +1193,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
     if (rc) break;
     e = hipEventRecord(coded[b], kst);
     if (e == hipSuccess) e = hipStreamWaitEvent(dst, coded[b], 0);
-    if (e == hipSuccess) e = copy_shards(false, set, chunk, down, host, off, sz, hs.flat, dst);
+    if (e == hipSuccess) e = copy_shards(false, set, chunk, down, host, off, sz, hs.flat, any_mem, dst);
     if (e == hipSuccess) e = hipEventRecord(d2h[b], dst);
   }
   // join: the caller's stream waits for every stream, frees the ring, syncs
@@ -1136,13 +1223,13 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
 
 // rows x host inputs -> host outputs through the pipeline (kCode).
 int host_code(int field, const Rows& rows, const void* const* in, void* const* out, size_t len_bytes,
-              bool accumulate, hipStream_t s) {
+              bool accumulate, hipStream_t s, bool any_mem) {
   std::vector<void*> ptrs(rows.n_in + rows.n_out);
   for (size_t i = 0; i < rows.n_in; ++i) ptrs[i] = const_cast<void*>(in[i]);
   for (size_t o = 0; o < rows.n_out; ++o) ptrs[rows.n_in + o] = out[o];
   for (void* q : ptrs)
     if (!q) return RSE_ERR_INVALID_ARGUMENT;
-  const HostCode hc{field, &rows, accumulate};
+  const HostCode hc{field, &rows, accumulate, any_mem};
   return host_pipeline(nullptr, HostOp::kCode, {HostStripe{ptrs.data(), nullptr, nullptr}},
                        len_bytes, s, nullptr, &hc);
 }
@@ -1152,6 +1239,84 @@ std::vector<void*> flat_ptrs(const rse_codec* c, void* base, size_t sb, size_t n
   std::vector<void*> ptrs(n_stripes * c->total);
   for (size_t i = 0; i < ptrs.size(); ++i) ptrs[i] = static_cast<uint8_t*>(base) + i * sb;
   return ptrs;
+}
+
+// Makes `dev` current for a scope (dev < 0: no change) and restores the
+// caller's device.
+class OnDevice {
+ public:
+  explicit OnDevice(int dev) {
+    int cur = 0;
+    if (dev < 0 || hipGetDevice(&cur) != hipSuccess || cur == dev) return;
+    if (hipSetDevice(dev) == hipSuccess) prev_ = cur;
+  }
+  ~OnDevice() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  OnDevice(const OnDevice&) = delete;
+  OnDevice& operator=(const OnDevice&) = delete;
+
+ private:
+  int prev_ = -1;
+};
+
+// Where a caller buffer lives.  True for device memory (hipMalloc'd or
+// managed) and sets *dev; false for host memory -- pageable (unknown to the
+// runtime), pinned or registered.
+bool device_memory(const void* p, int* dev) {
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof a);
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // an unregistered host pointer is not an error here
+    return false;
+  }
+  if (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged) return false;
+  *dev = a.device;
+  return true;
+}
+
+// The Field/FFI slice hooks (galois_8.rs:291-327 mul_slice(_xor) over
+// reedsolomon_gal_mul(_xor); galois_16's Field::mul_slice(_add), lib.rs:99-118):
+// out (+)= c * in over len elements, wherever the caller's slices live -- the
+// reference's callers pass host slices.
+//  * in and out in device memory of one device: the kernel, asynchronous on
+//    `stream`; with `sync`, on a leased library stream of that device, waited
+//    for (only this call's work, not the whole device).
+//  * either in host memory: the host pipeline (H2D, kernel, D2H; synchronous),
+//    on `stream` or, with `sync`, a leased library stream.  A side that is
+//    device memory is copied device to device by the same pipeline.
+int mul_slice_any(int field, const uint8_t* coef, const void* in, void* out, size_t len,
+                  bool acc, hipStream_t stream, bool sync) {
+  if (!coef || (len && (!in || !out))) return RSE_ERR_INVALID_ARGUMENT;
+  if (len == 0) return RSE_OK;
+  int din = -1, dout = -1;
+  const bool di = device_memory(in, &din), dd = device_memory(out, &dout);
+  Rows r;
+  r.n_out = r.n_in = 1;
+  r.c.assign(1, field == RSE_FIELD_GF16 ? (uint16_t)((coef[0] << 8) | coef[1]) : coef[0]);
+  const size_t bytes = len * (field == RSE_FIELD_GF16 ? 2 : 1);
+  std::unique_ptr<OnStreamDevice> on_stream;
+  std::unique_ptr<OnDevice> on_dev;
+  if (sync) on_dev.reset(new OnDevice(dd ? dout : din));  // the data's device
+  else on_stream.reset(new OnStreamDevice(stream));
+  Lease lease;
+  if (sync) {
+    RSE_HIP(lease.acquire());
+    RSE_HIP(lease_own_stream(lease.get(), &stream));
+  }
+  if (di && dd && din == dout) {
+    const uint8_t* ins[1] = {static_cast<const uint8_t*>(in)};
+    uint8_t* outs[1] = {static_cast<uint8_t*>(out)};
+    Job j{field, &r, ins, outs, nullptr, bytes, rse::kStore, acc, nullptr, 0, 1};
+    const int rc = run_job(j, stream);
+    const hipError_t e = sync ? hipStreamSynchronize(stream) : hipSuccess;
+    if (rc) return rc;
+    RSE_HIP(e);
+    return RSE_OK;
+  }
+  const void* ins[1] = {in};
+  void* outs[1] = {out};
+  return host_code(field, r, ins, outs, bytes, acc, stream, di || dd);
 }
 
 }  // namespace
@@ -1538,9 +1703,7 @@ int rse_code_shards(int field, const uint8_t* rows, size_t n_out, size_t n_in,
 
 int rse_gf8_mul_slice(uint8_t c, const void* in, void* out, size_t len, int xor_into,
                       rse_stream_t stream) {
-  const void* ins[1] = {in};
-  void* outs[1] = {out};
-  return rse_code_shards(RSE_FIELD_GF8, &c, 1, 1, ins, outs, len, xor_into, stream);
+  return mul_slice_any(RSE_FIELD_GF8, &c, in, out, len, xor_into != 0, (hipStream_t)stream, false);
 }
 
 int rse_code_shards_host(int field, const uint8_t* rows, size_t n_out, size_t n_in,
@@ -1591,27 +1754,26 @@ int rse_encode_single_sep_host(const rse_codec* c, size_t i_data, const void* si
                                 (hipStream_t)stream, true);
 }
 
+// low[n] = c * n and high[n] = c * (n << 4) (build.rs:75-94), so c = low[1].
+// Synchronous on a library stream, like the CPU kernel; 0 on error (nothing
+// written; rse_last_device_error tells why).
 size_t rse_gal_mul(const uint8_t* low, const uint8_t* high, const uint8_t* in, uint8_t* out,
                    size_t len) {
-  // low[n] = c * n and high[n] = c * (n << 4) (build.rs:75-94), so c = low[1]
   if (!low || !high || (len && (!in || !out))) return 0;
-  if (rse_gf8_mul_slice(low[1], in, out, len, 0, nullptr) != RSE_OK) return 0;
-  return hipDeviceSynchronize() == hipSuccess ? len : 0;
+  return mul_slice_any(RSE_FIELD_GF8, &low[1], in, out, len, false, nullptr, true) == RSE_OK ? len
+                                                                                            : 0;
 }
 
 size_t rse_gal_mul_xor(const uint8_t* low, const uint8_t* high, const uint8_t* in, uint8_t* out,
                        size_t len) {
   if (!low || !high || (len && (!in || !out))) return 0;
-  if (rse_gf8_mul_slice(low[1], in, out, len, 1, nullptr) != RSE_OK) return 0;
-  return hipDeviceSynchronize() == hipSuccess ? len : 0;
+  return mul_slice_any(RSE_FIELD_GF8, &low[1], in, out, len, true, nullptr, true) == RSE_OK ? len
+                                                                                           : 0;
 }
 
 int rse_gf16_mul_slice(const uint8_t* c, const void* in, void* out, size_t len, int add_into,
                        rse_stream_t stream) {
-  if (!c) return RSE_ERR_INVALID_ARGUMENT;
-  const void* ins[1] = {in};
-  void* outs[1] = {out};
-  return rse_code_shards(RSE_FIELD_GF16, c, 1, 1, ins, outs, len, add_into, stream);
+  return mul_slice_any(RSE_FIELD_GF16, c, in, out, len, add_into != 0, (hipStream_t)stream, false);
 }
 
 int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
@@ -1746,7 +1908,9 @@ int rse_set_option(int key, int64_t value) {
 }
 
 int64_t rse_get_option(int key) {
-  return key == RSE_OPT_PATTERN_LAUNCHES ? g_pattern_launches : rse::get_option(key);
+  if (key == RSE_OPT_PATTERN_LAUNCHES) return g_pattern_launches;
+  if (key == RSE_OPT_SCRATCH_LIVE) return scratch_pool().live.load();
+  return rse::get_option(key);
 }
 
 int rse_fill_splitmix(void* dst, size_t nbytes, uint64_t seed, uint64_t shard_id,

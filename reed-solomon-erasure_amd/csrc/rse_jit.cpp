@@ -379,18 +379,41 @@ constexpr int kMaxBuilders = 8;
 std::atomic<pid_t> g_child[kMaxBuilders];
 std::atomic<bool> g_unloading{false};
 
+// The helper's source and output files live in a directory private to this
+// process (mkdtemp: mode 0700, a fresh name), inside the cache directory when
+// there is one (so a finished code object is renamed into the cache on the
+// same file system), else in $TMPDIR or /tmp.  Nobody else can plant a
+// symlink or swap a file in it between the write and the load.  "" if it
+// cannot be made (the builds then run hiprtc in process).  Never destroyed,
+// like cache_dir(); removed (when empty) by the Worker destructor.
+const std::string& private_dir() {
+  static const std::string& dir = *new std::string([] {
+    std::string base = cache_dir();
+    if (base.empty()) {
+      const char* t = std::getenv("TMPDIR");
+      base = t && *t ? t : "/tmp";
+    }
+    std::string tmpl = base + "/rse_jit.XXXXXX";
+    return mkdtemp(&tmpl[0]) ? tmpl : std::string();
+  }());
+  return dir;
+}
+
 // Builds src with the helper process (thread slot `slot`); false if it could
-// not run (the caller falls back to hiprtc in process).
+// not run or did not finish cleanly (the caller falls back to hiprtc in
+// process).  Only the helper's two clean outcomes are final: exit 0 with a
+// code object, or exit 1 (the source does not compile, which hiprtc in
+// process would repeat).  A helper that cannot start on this system (exit
+// 127), dies on a signal or reports an I/O error (exit 2) hands the build
+// back -- except at unload, when the build threads kill their helpers on
+// purpose and the build completes as failed.
 bool build_with_helper(const std::string& src, const std::string& key, int slot, Compiled* out) {
   const std::string& helper = helper_path();
   if (helper.empty()) return false;
-  std::string dir = cache_dir();
-  if (dir.empty()) {
-    const char* t = std::getenv("TMPDIR");
-    dir = t ? t : "/tmp";
-  }
-  char tag[64];
-  std::snprintf(tag, sizeof tag, ".%d.%d", (int)getpid(), slot);
+  const std::string& dir = private_dir();
+  if (dir.empty()) return false;
+  char tag[32];
+  std::snprintf(tag, sizeof tag, ".%d", slot);
   const std::string src_path = dir + "/" + key + tag + ".hip";
   const std::string out_path = dir + "/" + key + tag + ".co";
   if (!write_file(src_path, src)) return false;
@@ -412,17 +435,18 @@ bool build_with_helper(const std::string& src, const std::string& key, int slot,
   } while (w < 0 && errno == EINTR);
   g_child[slot].store(0);
   unlink(src_path.c_str());
-  if (w == pid && WIFEXITED(status) && WEXITSTATUS(status) == 0 && read_file(out_path, &out->code)) {
+  const bool exited = w == pid && WIFEXITED(status);
+  if (exited && WEXITSTATUS(status) == 0 && read_file(out_path, &out->code)) {
     out->ok = true;
     if (cache_dir().empty() || get_option(15) == 0 ||
         rename(out_path.c_str(), (cache_dir() + "/" + key + ".co").c_str()) != 0)
       unlink(out_path.c_str());
-  } else {
-    unlink(out_path.c_str());
-    out->log = "rse_jitc failed";
-    if (w == pid && WIFEXITED(status) && WEXITSTATUS(status) == 2) return false;  // I/O: retry here
+    return true;
   }
-  return true;
+  unlink(out_path.c_str());
+  out->code.clear();
+  out->log = "rse_jitc failed";
+  return (exited && WEXITSTATUS(status) == 1) || g_unloading.load();
 }
 
 // In-process hiprtc (no helper, or it could not run).
@@ -518,6 +542,7 @@ class Worker {
       if (pid_t pid = c.load()) kill(pid, SIGKILL);
     for (auto& t : th_)
       if (t.joinable()) t.join();
+    if (!th_.empty() && !private_dir().empty()) rmdir(private_dir().c_str());  // empty by now
     std::lock_guard<std::mutex> g(g_mu);
     for (int q = 0; q < kQueues; ++q) {
       for (Entry* e : g_jobs[q])

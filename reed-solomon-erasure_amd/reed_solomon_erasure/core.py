@@ -452,6 +452,29 @@ def _host_elems(s, field: int) -> int:
     return n if field == 8 else n // 2
 
 
+def _any_ptr(s) -> int:
+    """Address of a shard wherever it lives: a device tensor, a CPU tensor or a
+    numpy array (the Field/FFI slice hooks route by memory type)."""
+    if isinstance(s, torch.Tensor) and s.is_cuda:
+        _elems(s, 8)
+        return s.data_ptr()
+    return _host_ptr(s)
+
+
+def _any_elems(s, field: int) -> int:
+    if isinstance(s, torch.Tensor) and s.is_cuda:
+        return _elems(s, field)
+    return _host_elems(s, field)
+
+
+def _any_stream(*bufs):
+    """torch's current stream of the first device buffer, else of the current device."""
+    for b in bufs:
+        if isinstance(b, torch.Tensor) and b.is_cuda:
+            return _stream(b)
+    return _stream()
+
+
 def _host_arrays(shards, field):
     n = len(shards)
     pa = (ctypes.c_void_p * max(1, n))(*[_host_ptr(s) for s in shards])
@@ -543,20 +566,36 @@ def _check_multi(lens: List[int]) -> None:  # macros.rs:144-155
             raise RSError(Error.IncorrectShardSize)
 
 
-def code_shards(field: int, rows, inputs: ShardList, outputs: ShardList,
-                accumulate: bool = False) -> None:
-    """The fused kernel itself: outputs[r] (+)= sum_i rows[r][i] * inputs[i]
-    (core.rs:481-509 code_some_slices when accumulate is False)."""
-    n_out, n_in = len(outputs), len(inputs)
+def _row_bytes(field: int, rows, n_out: int, n_in: int) -> List[int]:
     flat = []
     for r in range(n_out):
         for i in range(n_in):
             v = int(rows[r][i])
             flat += [v >> 8, v & 0xFF] if field == 16 else [v & 0xFF]
+    return flat
+
+
+def _same_len(lens: List[int]) -> int:
+    """The C entry takes one length for every input and output: refuse a
+    shorter buffer before the library reads or writes past its end (the
+    reference's mul_slice asserts equal lengths, lib.rs:100)."""
+    if not lens:
+        return 0
+    if any(n != lens[0] for n in lens):
+        raise RSError(Error.IncorrectShardSize)
+    return lens[0]
+
+
+def code_shards(field: int, rows, inputs: ShardList, outputs: ShardList,
+                accumulate: bool = False) -> None:
+    """The fused kernel itself: outputs[r] (+)= sum_i rows[r][i] * inputs[i]
+    (core.rs:481-509 code_some_slices when accumulate is False)."""
+    n_out, n_in = len(outputs), len(inputs)
+    flat = _row_bytes(field, rows, n_out, n_in)
     rb = (ctypes.c_uint8 * max(1, len(flat)))(*flat)
     ip = (ctypes.c_void_p * max(1, n_in))(*[_dev(t) for t in inputs])
     op = (ctypes.c_void_p * max(1, n_out))(*[_dev(t) for t in outputs])
-    n = _elems(inputs[0], field) if n_in else 0
+    n = _same_len([_elems(t, field) for t in list(inputs) + list(outputs)])
     _raise(_lib.rse_code_shards(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
                                 _stream(inputs[0] if n_in else None)))
 
@@ -566,15 +605,11 @@ def code_shards_host(field: int, rows, inputs: Sequence, outputs: Sequence,
     """code_shards() on HOST inputs/outputs (the code_some_slices hook,
     core.rs:481-490): pipelined through the GPU, synchronous."""
     n_out, n_in = len(outputs), len(inputs)
-    flat = []
-    for r in range(n_out):
-        for i in range(n_in):
-            v = int(rows[r][i])
-            flat += [v >> 8, v & 0xFF] if field == 16 else [v & 0xFF]
+    flat = _row_bytes(field, rows, n_out, n_in)
     rb = (ctypes.c_uint8 * max(1, len(flat)))(*flat)
     ip = (ctypes.c_void_p * max(1, n_in))(*[_host_ptr(t) for t in inputs])
     op = (ctypes.c_void_p * max(1, n_out))(*[_host_ptr(t) for t in outputs])
-    n = _host_elems(inputs[0], field) if n_in else 0
+    n = _same_len([_host_elems(t, field) for t in list(inputs) + list(outputs)])
     _raise(_lib.rse_code_shards_host(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
                                      _stream()))
 

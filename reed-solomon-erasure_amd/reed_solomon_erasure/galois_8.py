@@ -1,7 +1,5 @@
 """GF(2^8) backend (galois_8.rs): type aliases of the codec over the 8-bit field."""
-import ctypes
-
-from .core import ReedSolomon as _RS, ShardByShard as _SBS, _dev, _lib, _raise, _stream
+from .core import ReedSolomon as _RS, ShardByShard as _SBS, _any_elems, _any_ptr, _any_stream, _lib, _raise
 
 FIELD = 8
 ORDER = 256
@@ -20,7 +18,11 @@ ShardByShard = _SBS
 
 
 def mul_slice(c: int, input, out) -> None:
-    """galois_8::mul_slice (galois_8.rs:291-308): out = c * input (device tensors)."""
+    """galois_8::mul_slice (galois_8.rs:291-308): out = c * input.
+
+    input/out may be device tensors (asynchronous on torch's current stream)
+    or host memory -- CPU tensors or numpy arrays, as the reference's callers
+    pass -- which go through the host pipeline and are done on return."""
     _mul(c, input, out, 0)
 
 
@@ -30,7 +32,8 @@ def mul_slice_xor(c: int, input, out) -> None:
 
 
 def _mul(c, input, out, xor):
-    if input.numel() != out.numel():  # lib.rs:100 assert_eq!
+    n = _any_elems(input, 8)
+    if n != _any_elems(out, 8):  # lib.rs:100 assert_eq!
         raise ValueError("input and out must have the same length")
-    _raise(_lib.rse_gf8_mul_slice(c & 0xFF, _dev(input), _dev(out), input.numel(), xor,
-                                  _stream(input)))
+    _raise(_lib.rse_gf8_mul_slice(c & 0xFF, _any_ptr(input), _any_ptr(out), n, xor,
+                                  _any_stream(input, out)))

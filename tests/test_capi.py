@@ -272,3 +272,15 @@ def test_exit_not_blocked_by_a_build(tmp_path):
     assert out.returncode == 0 and out.stdout.strip() == "bye", out.stderr[-2000:]
     assert time.time() - t0 < 60
     assert list(tmp_path.iterdir()) == []
+
+
+def test_code_shards_refuses_unequal_lengths():
+    """rse_code_shards(_host) take ONE length for every input and output: the
+    Python mirror refuses a shorter buffer before the library could read or
+    write past its end (lib.rs:100 asserts equal lengths)."""
+    a = np.zeros(64, np.uint8)
+    b = np.zeros(63, np.uint8)
+    for ins, outs in [([a, b], [a]), ([a], [b]), ([a], [a, b]), ([b, a], [a, a])]:
+        with pytest.raises(RSError) as ei:
+            R.core.code_shards_host(8, [[1] * len(ins)] * len(outs), ins, outs)
+        assert ei.value.error == Error.IncorrectShardSize

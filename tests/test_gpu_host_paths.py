@@ -253,6 +253,125 @@ def test_gal_mul_ffi_contract(R):
             assert (d_out.cpu().numpy() == O.gf8_mul_slice(c, x)).all()
 
 
+def _u8p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _host_buf(a, kind):
+    """A host copy of `a`: a numpy (pageable) array, or a pinned CPU tensor
+    (its numpy view shares the pinned memory)."""
+    if kind == "pageable":
+        return a.copy()
+    return torch.from_numpy(a.copy()).pin_memory().numpy()
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+def test_gal_mul_ffi_on_host_slices(R, kind):
+    """rse_gal_mul(_xor) exactly as galois_8.rs:291-327 calls
+    reedsolomon_gal_mul(_xor): HOST slices (simd_c/reedsolomon.h:30-42), the
+    coefficient's MUL_TABLE_LOW/HIGH rows, bytes done returned.  Every length
+    0..130 (the SIMD kernel's tails), 34, and 1 MiB; out equals the oracle's
+    mul_slice(_xor), so the reference's tail loop would have nothing to do."""
+    lib = R._lib.load()
+    _, _, _, low, high = O.gf8_tables()
+    rng = np.random.default_rng(71)
+    lens = list(range(0, 131)) + [34, 1 << 20]
+    for n in lens:
+        cs = (0, 1, 2, 29, 142, 255) if n in (34, 1 << 20) else (int(rng.integers(0, 256)),)
+        x = _host_buf(rng.integers(0, 256, n, dtype=np.uint8), kind)
+        for c in cs:
+            lo, hi = np.ascontiguousarray(low[c]), np.ascontiguousarray(high[c])
+            o = _host_buf(rng.integers(0, 256, n, dtype=np.uint8), kind)
+            before = o.copy()
+            assert lib.rse_gal_mul_xor(_u8p(lo), _u8p(hi), x.ctypes.data, o.ctypes.data, n) == n
+            assert (o == before ^ O.gf8_mul_slice(c, x)).all(), (n, c)
+            assert lib.rse_gal_mul(_u8p(lo), _u8p(hi), x.ctypes.data, o.ctypes.data, n) == n
+            assert (o == O.gf8_mul_slice(c, x)).all(), (n, c)
+
+
+def test_gal_mul_ffi_mixed_memory(R):
+    """One slice in host memory and the other in HBM: routed by where each
+    lives (hipPointerGetAttributes), same bytes as the oracle."""
+    lib = R._lib.load()
+    _, _, _, low, high = O.gf8_tables()
+    rng = np.random.default_rng(73)
+    for n in (1, 130, 65_537):
+        c = int(rng.integers(1, 256))
+        lo, hi = np.ascontiguousarray(low[c]), np.ascontiguousarray(high[c])
+        x = rng.integers(0, 256, n, dtype=np.uint8)
+        o = rng.integers(0, 256, n, dtype=np.uint8)
+        d_in = torch.from_numpy(x).cuda()
+        host_out = o.copy()
+        torch.cuda.synchronize()
+        assert lib.rse_gal_mul_xor(_u8p(lo), _u8p(hi), d_in.data_ptr(), host_out.ctypes.data, n) == n
+        assert (host_out == o ^ O.gf8_mul_slice(c, x)).all()
+        d_out = torch.from_numpy(o).cuda()
+        torch.cuda.synchronize()
+        assert lib.rse_gal_mul(_u8p(lo), _u8p(hi), x.ctypes.data, d_out.data_ptr(), n) == n
+        assert (d_out.cpu().numpy() == O.gf8_mul_slice(c, x)).all()
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+def test_field_mul_slice_on_host_slices(R, kind):
+    """galois_8 mul_slice(_xor) and galois_16's Field::mul_slice(_add)
+    (lib.rs:99-118) on host slices, through the raw C ABI (as a Rust Field
+    impl binds them) and through the Python mirror."""
+    from reed_solomon_erasure import galois_8, galois_16
+    lib = R._lib.load()
+    rng = np.random.default_rng(79)
+    for n in (1, 2, 33, 130, 4096 + 3, 1 << 19):
+        x = _host_buf(rng.integers(0, 256, (n, 2), dtype=np.uint8), kind)
+        o = _host_buf(rng.integers(0, 256, (n, 2), dtype=np.uint8), kind)
+        for c in [(0, 1), (1, 0), (0xD2, 0x0F), (255, 255), (0, 0)]:
+            for add in (0, 1):
+                before = o.copy()
+                cb = (ctypes.c_uint8 * 2)(*c)
+                assert lib.rse_gf16_mul_slice(cb, x.ctypes.data, o.ctypes.data, n, add, None) == 0
+                want = np.zeros(n * 2, np.uint8)
+                O.code_some_slices(16, np.array([[c]], np.uint8), [x.reshape(-1)], [want])
+                if add:
+                    want ^= before.reshape(-1)
+                assert (o.reshape(-1) == want).all(), (n, c, add)
+        galois_16.mul_slice_add((3, 7), x, o)  # the Python mirror, same routing
+        x8 = x.reshape(-1)
+        o8 = o.reshape(-1)
+        before = o8.copy()
+        galois_8.mul_slice_xor(117, x8, o8)
+        assert (o8 == before ^ O.gf8_mul_slice(117, x8)).all()
+        assert lib.rse_gf8_mul_slice(25, x8.ctypes.data, o8.ctypes.data, x8.size, 0, None) == 0
+        assert (o8 == O.gf8_mul_slice(25, x8)).all()
+
+
+def test_scratch_pool_short_lived_threads(R):
+    """Calls lease their streams, events, verdict words and pipeline ring from
+    a process-wide pool (at most 4 idle per device): host encodes and verifies
+    on 48 short-lived threads leave neither resource sets nor HBM behind."""
+    import threading
+    lib = R._lib.load()
+    r = R.galois_8.ReedSolomon(10, 4)
+    rng = np.random.default_rng(83)
+    n = 3 << 20
+    data = [torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).pin_memory() for _ in range(10)]
+
+    def work():
+        shards = data + [torch.empty(n, dtype=torch.uint8).pin_memory() for _ in range(4)]
+        r.encode_host(shards)
+        assert r.verify_host(shards)
+
+    work()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for wave in range(12):
+        ts = [threading.Thread(target=work) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    torch.cuda.synchronize()
+    assert lib.rse_get_option(24) <= 4 + 1  # the idle cap (+ nothing leased now)
+    assert free0 - torch.cuda.mem_get_info()[0] < (256 << 20)
+
+
 def test_field_mul_slice_both_fields(R):
     from reed_solomon_erasure import galois_8, galois_16
     rng = np.random.default_rng(59)

@@ -1183,6 +1183,15 @@ def test_bench_ranks_rehearsal(ranks, extras):
     assert d["config"]["parity_check_per_rank"] == [1] * ranks
     assert d["config"]["parity_checked_stripes_rank0"] == [0, 3]
     assert len(d["roofline"]["kernel_ms_per_launch_per_rank"]) == ranks
+    lo, hi = d["roofline"]["kernel_ms_per_launch_min_max"]
+    assert 0 < lo <= hi
+    # what the collective saw: the rehearsal's gloo group of `ranks` ranks, each
+    # rank's device gathered (all on the one GPU here, so not distinct)
+    coll = d["collective"]
+    assert coll["backend"] == "gloo" and coll["world_size"] == ranks and coll["rehearsal"]
+    assert len(coll["rank_devices"]) == ranks
+    assert all(x["device"] == "cuda:0" and x["pci"] for x in coll["rank_devices"])
+    assert coll["distinct_gpus"] is False
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
     if extras:
         h = d["end_to_end_host_all_ranks"]

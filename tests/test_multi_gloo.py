@@ -41,7 +41,8 @@ def _stripe_digest(g):
 
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    assert bench.init_collective(world, rank, 0, rehearsal=False) == "gloo"  # no GPU here
+    coll = bench.collective_info(world, 0, False)
     mine = bench.stripes_for_rank(STRIPES_PER_RANK * world, rank, world)
     digests = {g: _stripe_digest(g) for g in mine}
     elapsed = 0.5 + rank  # deterministic stand-in for the timed region
@@ -51,7 +52,7 @@ def _worker(rank, world, port, q):
     verdicts = bench.gather(1 if rank else -1, world, rank, None)  # per-rank verdicts
     if rank == 0:
         q.put((t, gathered, [list(bench.stripes_for_rank(STRIPES_PER_RANK * world, r, world))
-                             for r in range(world)], verdicts))
+                             for r in range(world)], verdicts, coll))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,7 +65,7 @@ def test_two_rank_stripe_split_and_reduction():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    t, gathered, parts, verdicts = q.get(timeout=120)
+    t, gathered, parts, verdicts, coll = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -78,6 +79,10 @@ def test_two_rank_stripe_split_and_reduction():
     stripe_bytes = (K + P) * L
     v = bench.job_throughput(3, STRIPES_PER_RANK, world, stripe_bytes, t)
     assert v == pytest.approx(3 * STRIPES_PER_RANK * world * stripe_bytes / 1.5 / (1 << 20))
+    # what the collective saw: the backend, both ranks, each rank's device
+    assert coll["backend"] == "gloo" and coll["world_size"] == world
+    assert [d["pid"] for d in coll["rank_devices"]] == sorted({d["pid"] for d in coll["rank_devices"]})
+    assert len(coll["rank_devices"]) == world and coll["distinct_gpus"] is False  # CPU ranks
     # placement-independent results
     merged = {}
     for d in gathered:
@@ -115,3 +120,19 @@ def test_check_stripes_detects_a_flipped_byte():
     v[0, k + 2, 12345] ^= 1
     assert bench.check_stripes(v, range(0, 1), 1, k, p) == (0, [0])
     assert bench.check_stripes(v, range(5, 6), 1, k, p) == (-1, [])  # no digest: unchecked
+
+
+def test_missing_peer_fails_fast():
+    """A rank whose peer never joins exits non-zero within the collective
+    deadline instead of hanging (bench.init_collective)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), RSE_BENCH_COLLECTIVE_TIMEOUT="5")
+    code = "import bench; bench.init_collective(2, 0, 0, False); print('joined')"
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode in (4, 5), (out.returncode, out.stderr[-2000:])
+    assert "joined" not in out.stdout
+    assert "rank 0/2" in out.stderr
