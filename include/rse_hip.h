@@ -221,11 +221,19 @@ size_t rse_gal_mul_xor(const uint8_t *low, const uint8_t *high, const uint8_t *i
 int rse_gf16_mul_slice(const uint8_t *c, const void *in, void *out, size_t len, int add_into,
                        rse_stream_t stream);
 
-/* ---- device matrix inversion (matrix.rs:249-261 semantics) ----------- */
-/* Invert `batch` n x n GF(2^8) matrices (device memory, row-major, n <= 255),
- * one workgroup per matrix.  singular[b] = 1 for a singular matrix. */
+/* ---- device matrix inversion (matrix.rs:195-261 semantics) ----------- */
+/* Invert `batch` n x n matrices (device memory, row-major), one workgroup per
+ * matrix (Gauss-Jordan; the augmented matrix in LDS up to n = 127, else in a
+ * stream-ordered device workspace).  singular[b] = 1 for a singular matrix
+ * (matrix.rs:11-13 Error::SingularMatrix; its out[b] is left unwritten), else
+ * 0.  Asynchronous on `stream`.
+ * GF(2^8): one byte per element, n <= 255 (the field's largest codec). */
 int rse_gf8_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, size_t n,
                          size_t batch, rse_stream_t stream);
+/* GF(2^16): [u8;2] elements {coefficient of x, constant} (galois_16.rs:49-51),
+ * n <= 4096.  The decode matrices of galois_16 codecs (core.rs:697-731). */
+int rse_gf16_invert_batch(const void *d_in, void *d_out, uint32_t *d_singular, size_t n,
+                          size_t batch, rse_stream_t stream);
 
 /* ---- host-memory (end-to-end) path ----------------------------------- */
 /* The reference API's own form: shards are caller slices in HOST memory
@@ -325,6 +333,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_WIDE_LDS 14         /* wide-codec modules built after: 1 (default) each wave slices
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */
+#define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch
+                                       planned on the host (a batch past the device planner's LDS
+                                       budget: more than 8192 shards or very many erasures) */
 #define RSE_OPT_SCRATCH_LIVE 24     /* read-only: per-call device resource sets (verdict words, library
                                        stream, host-pipeline streams/events/ring) in existence, leased or
                                        idle.  Calls lease one from a process-wide pool that keeps at most 4

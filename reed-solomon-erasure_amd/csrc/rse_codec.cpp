@@ -816,6 +816,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
 }
 
 thread_local int64_t g_pattern_launches = 0;  // RSE_OPT_PATTERN_LAUNCHES
+thread_local int64_t g_host_planned = 0;      // RSE_OPT_HOST_PLANNED_STRIPES
 
 // Decode patterns used more than once (the decode-matrix LRU of
 // core.rs:697-731 counts them) get a bit-sliced kernel built at run time for
@@ -1645,37 +1646,57 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     }
   }
   if (done == sb) return RSE_OK;
-  // 2. the rest of every shard (all of it if step 1 did not apply)
-  if (c->field != RSE_FIELD_GF8 || !fits) {  // host planner, stripe by stripe
+  // 2. the rest of every shard (all of it if step 1 did not apply): planned
+  //    per stripe on the device (recon_plan_kernel: e x e syndrome inverse,
+  //    composed rows as descriptors), coded by the table kernels
+  uint32_t e_cap = 0, nout_cap = 0;
+  for (size_t s = 0; s < n_stripes; ++s) {
+    const uint8_t* pr = present + s * T;
+    uint32_t ne = 0, nmp = 0;
+    for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0 : 1;
+    if (!data_only)
+      for (size_t r = 0; r < p; ++r) nmp += pr[k + r] ? 0 : 1;
+    e_cap = std::max(e_cap, ne);
+    nout_cap = std::max(nout_cap, ne + nmp);
+  }
+  if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
+  if (T > 0xffffu ||
+      rse::recon_plan_lds((uint32_t)k, (uint32_t)T, e_cap, nout_cap) > rse::kReconPlanLdsMax) {
+    // past the device planner's LDS budget: the host planner, stripe by stripe
     std::vector<void*> ptrs(T);
     std::vector<size_t> lens(T, (sb - done) / c->esize());
     for (size_t s = 0; s < n_stripes; ++s) {
       for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb + done;
       int rc = reconstruct_impl(c, ptrs.data(), lens.data(), present + s * T, T, data_only != 0, st);
       if (rc) return rc;
+      ++g_host_planned;
     }
     return RSE_OK;
   }
-  // device planner (k x k inverse per stripe) + table kernels
-  const size_t mat_bytes = T * k, pres_off = (mat_bytes + 255) & ~size_t(255);
+  const Rows prow = parity_rows(c);
+  const size_t n_ib = (k + 31) / 32, n_ob = (nout_cap + 15) / 16;
+  const size_t per_stripe = n_ib * n_ob * sizeof(CodeArgs);
+  // stripes per planning group: descriptors of at most 256 MiB at a time
+  const size_t grp = std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per_stripe));
+  const size_t p_bytes = prow.c.size() * sizeof(uint16_t), pres_off = (p_bytes + 255) & ~size_t(255);
   const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
-  const size_t ws_bytes = desc_off + n_stripes * sizeof(CodeArgs);
-  std::vector<uint8_t> mat(mat_bytes);
-  for (size_t r = 0; r < T; ++r)
-    for (size_t j = 0; j < k; ++j) mat[r * k + j] = (uint8_t)c->mat(r, j);
   uint8_t* ws = nullptr;
-  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), ws_bytes, st));
-  hipError_t e = hipMemcpyAsync(ws, mat.data(), mat_bytes, hipMemcpyHostToDevice, st);
+  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + grp * per_stripe, st));
+  hipError_t e = hipMemcpyAsync(ws, prow.c.data(), p_bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
-    e = rse::launch_recon_batch(ws, ws + pres_off, (uint32_t)k, (uint32_t)T,
-                                data_only ? 1u : 0u, base, sb, done, sb - done,
-                                (uint32_t)n_stripes, reinterpret_cast<CodeArgs*>(ws + desc_off), st);
-  hipError_t f = hipFreeAsync(ws, st);
+  for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {
+    const size_t ng = std::min(grp, n_stripes - g0);
+    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(ws),
+                               ws + pres_off + g0 * T, (uint32_t)k, (uint32_t)T,
+                               data_only ? 1u : 0u, e_cap, nout_cap, base + g0 * T * sb, sb, done,
+                               sb - done, (uint32_t)ng, reinterpret_cast<CodeArgs*>(ws + desc_off),
+                               st);
+  }
+  const hipError_t f = hipFreeAsync(ws, st);
   if (e != hipSuccess) return dev_fail(e);
   if (f != hipSuccess) return dev_fail(f);
-  // The pageable copies above were staged before returning, but `mat` dies
+  // The pageable copies above were staged before returning, but `prow` dies
   // here: make sure the runtime is done reading it.
   RSE_HIP(hipStreamSynchronize(st));
   return RSE_OK;
@@ -1776,14 +1797,37 @@ int rse_gf16_mul_slice(const uint8_t* c, const void* in, void* out, size_t len, 
   return mul_slice_any(RSE_FIELD_GF16, c, in, out, len, add_into != 0, (hipStream_t)stream, false);
 }
 
+// Batched device inversion (matrix.rs:195-261 semantics, either field); the
+// augmented matrices go to a stream-ordered workspace when they exceed LDS.
+static int invert_batch(int field, const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
+                        size_t batch, hipStream_t st) {
+  const size_t max_n = field == RSE_FIELD_GF8 ? 255 : 4096;
+  if (!d_in || !d_out || !d_singular || n == 0 || n > max_n || batch == 0 || batch > 0x7fffffff)
+    return RSE_ERR_INVALID_ARGUMENT;
+  const size_t w = n * 2 * n * sizeof(uint16_t);
+  uint16_t* gws = nullptr;
+  if (w > rse::invert_lds_max_bytes()) RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&gws), w * batch, st));
+  hipError_t e = rse::launch_invert(field, static_cast<const uint8_t*>(d_in),
+                                    static_cast<uint8_t*>(d_out), d_singular, (uint32_t)n,
+                                    (uint32_t)batch, gws, st);
+  if (gws) {
+    const hipError_t f = hipFreeAsync(gws, st);
+    if (e == hipSuccess) e = f;
+  }
+  RSE_HIP(e);
+  return RSE_OK;
+}
+
 int rse_gf8_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
                          size_t batch, rse_stream_t stream) {
   RSE_ON_STREAM(stream);
-  if (!d_in || !d_out || !d_singular || n == 0 || n > 255 || batch == 0 || batch > 0x7fffffff)
-    return RSE_ERR_INVALID_ARGUMENT;
-  RSE_HIP(rse::launch_gf8_invert(static_cast<const uint8_t*>(d_in), static_cast<uint8_t*>(d_out),
-                                 d_singular, (uint32_t)n, (uint32_t)batch, (hipStream_t)stream));
-  return RSE_OK;
+  return invert_batch(RSE_FIELD_GF8, d_in, d_out, d_singular, n, batch, (hipStream_t)stream);
+}
+
+int rse_gf16_invert_batch(const void* d_in, void* d_out, uint32_t* d_singular, size_t n,
+                          size_t batch, rse_stream_t stream) {
+  RSE_ON_STREAM(stream);
+  return invert_batch(RSE_FIELD_GF16, d_in, d_out, d_singular, n, batch, (hipStream_t)stream);
 }
 
 int rse_encode_host(const rse_codec* c, void* const* shards, const size_t* lens, size_t n,
@@ -1910,6 +1954,7 @@ int rse_set_option(int key, int64_t value) {
 int64_t rse_get_option(int key) {
   if (key == RSE_OPT_PATTERN_LAUNCHES) return g_pattern_launches;
   if (key == RSE_OPT_SCRATCH_LIVE) return scratch_pool().live.load();
+  if (key == RSE_OPT_HOST_PLANNED_STRIPES) return g_host_planned;
   return rse::get_option(key);
 }
 

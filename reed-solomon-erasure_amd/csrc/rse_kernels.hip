@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? (NO >= 16 ? 3 : 4) : 2) void gf8
   gf8_code_impl<KC, NO, NOGUARD, NT, VPL>(a, blockIdx.y, gridDim.y);
 }
 
-// Per-stripe descriptors in HBM (written by gf8_recon_plan_kernel): row y of
+// Per-stripe descriptors in HBM (written by recon_plan_kernel): row y of
 // the grid codes stripe y with its own shard pointers and coefficient rows.
 template <bool NT>
 __global__ __launch_bounds__(kBlock, 3) void gf8_code_desc_kernel(const CodeArgs* __restrict__ descs) {
@@ -451,7 +451,8 @@ __device__ __forceinline__ void gf16_span(const CodeArgs& a, const uint4* tq, co
 }
 
 template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
-__global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(const CodeArgs a) {
+__device__ __forceinline__ void gf16_code_impl(const CodeArgs& a, uint32_t stripe0,
+                                               uint32_t stripe_step) {
   __shared__ uint4 tq[kMaxIn * NO * 4];
   __shared__ uint32_t tt2[kMaxIn * NO * 4];
 
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
   const uint64_t span = (uint64_t)kBlock * VPL;
   const uint64_t n_full = a.n_vec / span;
 
-  for (uint32_t stripe = blockIdx.y; stripe < a.n_stripes; stripe += gridDim.y) {
+  for (uint32_t stripe = stripe0; stripe < a.n_stripes; stripe += stripe_step) {
   const uint64_t soff = (uint64_t)stripe * a.stripe_stride;
 
   for (uint64_t sp = blockIdx.x; sp < n_full; sp += gridDim.x)
@@ -520,6 +521,21 @@ __global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(con
     if (mode != kStore && diff) flag_mismatch(mismatch_word(a, soff));
   }
   }  // stripe loop
+}
+
+template <int KC, int NO, bool NOGUARD, bool NT, int VPL>
+__global__ __launch_bounds__(kBlock, VPL == 1 ? 3 : 2) void gf16_code_kernel(const CodeArgs a) {
+  gf16_code_impl<KC, NO, NOGUARD, NT, VPL>(a, blockIdx.y, gridDim.y);
+}
+
+// Per-stripe (or per-block) descriptors of recon_plan_kernel, GF(2^16): row y
+// of the grid codes descriptor y (as gf8_code_desc_kernel).
+template <bool NT>
+__global__ __launch_bounds__(kBlock, 3) void gf16_code_desc_kernel(const CodeArgs* __restrict__ descs) {
+  using CPtr = const __attribute__((address_space(4))) CodeArgs*;
+  const CodeArgs& a = *(const CodeArgs*)((CPtr)descs + blockIdx.y);
+  if (a.n_out == 0) return;  // uniform: nothing to rebuild in this block
+  gf16_code_impl<4, kMaxOut, false, NT, 1>(a, 0, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -801,210 +817,276 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* dst, uin
 }
 
 // ---------------------------------------------------------------------------
-// Batched GF(2^8) Gauss-Jordan inversion, one workgroup per matrix, the
-// augmented [M | I] in LDS (matrix.rs:195-261 computes the same unique
-// inverse; pivot choice cannot change the result of an exact field).
-constexpr int kInvMax = 255;
+// Field arithmetic of the planner and inversion kernels: log/exp of GF(2^8)'s
+// generator 2 modulo 0x11D (build.rs:13-43) in LDS, exp extended to kExLen
+// entries so a sum of two logs plus 7 needs no reduction.  GF(2^16) =
+// GF(2^8)[x]/(x^2 + 2x + 128) (galois_16.rs:9-14, 146-162):
+//   (a1 x + a0)(b1 x + b0) = (a1 b0 + a0 b1 + 2 a1 b1) x + (a0 b0 + 128 a1 b1)
+// and the inverse through the norm N = a0^2 + 2 a0 a1 + 128 a1^2 (in GF(2^8)):
+//   (a1 x + a0)^-1 = (a1 / N) x + (a0 + 2 a1) / N
+// -- the same unique inverse as the reference's extended Euclid
+// (galois_16.rs:113-144; tests/test_oracle_golden.py checks all 65535).
+constexpr int kExLen = 520;
+constexpr uint32_t kTabBytes = 784;  // lg[256] + ex[kExLen], rounded to 16
 
-__device__ __forceinline__ uint32_t gmul(const uint8_t* lg, const uint8_t* ex, uint32_t a,
-                                         uint32_t b) {
-  return (a && b) ? ex[lg[a] + lg[b]] : 0u;
-}
-
-__global__ __launch_bounds__(1024) void gf8_invert_kernel(const uint8_t* in, uint8_t* out,
-                                                          uint32_t* singular, uint32_t n) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  int& s_piv = *reinterpret_cast<int*>(smem);  // 16 B slot
-  uint8_t* lg = smem + 16;    // 256
-  uint8_t* ex = smem + 272;   // 512
-  uint8_t* w = smem + 784;    // n x 2n
-  const uint32_t tid = threadIdx.x, nt = blockDim.x, w2 = 2 * n;
-  const uint8_t* m = in + (size_t)blockIdx.x * n * n;
-
-  if (tid == 0) {  // log/exp of generator 2 modulo 0x11D (build.rs:13-43)
+__device__ __forceinline__ void build_log_exp(uint8_t* lg, uint8_t* ex) {
+  if (threadIdx.x == 0) {
     uint32_t b = 1;
-    for (uint32_t l = 0; l < 255; ++l) {
-      lg[b] = (uint8_t)l;
+    for (int l = 0; l < kExLen; ++l) {
+      if (l < 255) lg[b] = (uint8_t)l;
       ex[l] = (uint8_t)b;
-      ex[l + 255] = (uint8_t)b;
       b <<= 1;
       if (b & 0x100u) b ^= 0x11Du;
+      if (l % 255 == 254) b = 1;  // 2^255 = 1
     }
     lg[0] = 0;
-    ex[510] = ex[511] = 0;
   }
-  for (uint32_t t = tid; t < n * w2; t += nt) {
-    const uint32_t r = t / w2, c = t % w2;
-    w[t] = c < n ? m[r * n + c] : (uint8_t)((c - n) == r ? 1 : 0);
-  }
-  __syncthreads();
+}
 
+struct PlanF8 {
+  static constexpr int kField = 8;
+  __device__ static uint32_t mul(const uint8_t* lg, const uint8_t* ex, uint32_t a, uint32_t b) {
+    return (a && b) ? ex[lg[a] + lg[b]] : 0u;
+  }
+  __device__ static uint32_t inv(const uint8_t* lg, const uint8_t* ex, uint32_t a) {  // a != 0
+    return ex[255 - lg[a]];
+  }
+  __device__ static uint32_t load(const uint8_t* m, size_t i) { return m[i]; }
+  __device__ static void store(uint8_t* m, size_t i, uint32_t v) { m[i] = (uint8_t)v; }
+};
+
+struct PlanF16 {
+  static constexpr int kField = 16;
+  __device__ static uint32_t mul(const uint8_t* lg, const uint8_t* ex, uint32_t a, uint32_t b) {
+    const uint32_t a1 = a >> 8, a0 = a & 0xFFu, b1 = b >> 8, b0 = b & 0xFFu;
+    uint32_t hi = 0, lo = 0;
+    if (a1 && b1) {
+      const uint32_t l = lg[a1] + lg[b1];
+      hi = ex[l + 1];  // 2 a1 b1
+      lo = ex[l + 7];  // 128 a1 b1
+    }
+    if (a1 && b0) hi ^= ex[lg[a1] + lg[b0]];
+    if (a0 && b1) hi ^= ex[lg[a0] + lg[b1]];
+    if (a0 && b0) lo ^= ex[lg[a0] + lg[b0]];
+    return (hi << 8) | lo;
+  }
+  __device__ static uint32_t inv(const uint8_t* lg, const uint8_t* ex, uint32_t a) {  // a != 0
+    const uint32_t a1 = a >> 8, a0 = a & 0xFFu;
+    uint32_t n = 0;
+    if (a0) n ^= ex[2u * lg[a0]];
+    if (a0 && a1) n ^= ex[lg[a0] + lg[a1] + 1];
+    if (a1) n ^= ex[2u * lg[a1] + 7];
+    const uint32_t li = 255u - lg[n];  // n != 0 for a != 0
+    const uint32_t c = a0 ^ (a1 ? ex[lg[a1] + 1] : 0u);
+    return ((a1 ? (uint32_t)ex[lg[a1] + li] : 0u) << 8) | (c ? ex[lg[c] + li] : 0u);
+  }
+  // [u8;2] elements {coefficient of x, constant} (galois_16.rs:49-51)
+  __device__ static uint32_t load(const uint8_t* m, size_t i) {
+    return ((uint32_t)m[2 * i] << 8) | m[2 * i + 1];
+  }
+  __device__ static void store(uint8_t* m, size_t i, uint32_t v) {
+    m[2 * i] = (uint8_t)(v >> 8);
+    m[2 * i + 1] = (uint8_t)v;
+  }
+};
+
+// Gauss-Jordan on the n x 2n augmented matrix w (row stride 2n) by the whole
+// workgroup (matrix.rs:195-261: the same unique inverse -- the pivot choice
+// cannot change the result of an exact field).  False if singular (uniform).
+template <class F>
+__device__ bool gauss_jordan(uint16_t* w, uint32_t n, const uint8_t* lg, const uint8_t* ex,
+                             int* s_piv) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x, w2 = 2 * n;
   for (uint32_t col = 0; col < n; ++col) {
     if (tid == 0) {
       int piv = -1;
       for (uint32_t r = col; r < n; ++r)
-        if (w[r * w2 + col]) { piv = (int)r; break; }
-      s_piv = piv;
+        if (w[r * w2 + col]) {
+          piv = (int)r;
+          break;
+        }
+      *s_piv = piv;
     }
     __syncthreads();
-    const int piv = s_piv;
-    if (piv < 0) {
-      if (tid == 0) singular[blockIdx.x] = 1u;
-      return;  // uniform: every thread read the same s_piv
-    }
+    const int piv = *s_piv;
+    if (piv < 0) return false;
     if ((uint32_t)piv != col) {
       for (uint32_t c = tid; c < w2; c += nt) {
-        const uint8_t t0 = w[col * w2 + c];
+        const uint16_t t0 = w[col * w2 + c];
         w[col * w2 + c] = w[piv * w2 + c];
         w[piv * w2 + c] = t0;
       }
       __syncthreads();
     }
-    const uint32_t inv = ex[255 - lg[w[col * w2 + col]]];
+    const uint32_t inv = F::inv(lg, ex, w[col * w2 + col]);
+    __syncthreads();  // every thread has read the pivot before the row is scaled
+    for (uint32_t c = tid; c < w2; c += nt)
+      w[col * w2 + c] = (uint16_t)F::mul(lg, ex, inv, w[col * w2 + c]);
     __syncthreads();
-    for (uint32_t c = tid; c < w2; c += nt) w[col * w2 + c] = (uint8_t)gmul(lg, ex, inv, w[col * w2 + c]);
-    __syncthreads();
-    // eliminate column `col` from every other row
-    for (uint32_t t = tid; t < n * w2; t += nt) {
+    for (uint32_t t = tid; t < n * w2; t += nt) {  // eliminate column `col` elsewhere
       const uint32_t r = t / w2, c = t % w2;
       if (r == col || c == col) continue;
       const uint32_t f = w[r * w2 + col];
-      if (f) w[t] ^= (uint8_t)gmul(lg, ex, f, w[col * w2 + c]);
+      if (f) w[t] ^= (uint16_t)F::mul(lg, ex, f, w[col * w2 + c]);
     }
     __syncthreads();
     for (uint32_t r = tid; r < n; r += nt)
       if (r != col) w[r * w2 + col] = 0;
     __syncthreads();
   }
-  uint8_t* o = out + (size_t)blockIdx.x * n * n;
-  for (uint32_t t = tid; t < n * n; t += nt) o[t] = w[(t / n) * w2 + n + (t % n)];
+  return true;
+}
+
+// Batched inversion, one workgroup per n x n matrix (row-major, the field's
+// element bytes), [M | I] in LDS -- or, past kInvLds, in a global workspace
+// of batch x n x 2n elements (gws).  singular[b] = 1 for a singular matrix
+// (matrix.rs:11-13 Error::SingularMatrix), and out[b] is then left unwritten.
+constexpr uint32_t kInvLds = 65536 - kTabBytes - 16;
+
+template <class F>
+__global__ __launch_bounds__(1024) void invert_kernel(const uint8_t* in, uint8_t* out,
+                                                      uint32_t* singular, uint32_t n,
+                                                      uint16_t* gws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* lg = smem;
+  uint8_t* ex = smem + 256;
+  int* s_piv = reinterpret_cast<int*>(smem + kTabBytes);
+  uint16_t* w = gws ? gws + (size_t)blockIdx.x * n * 2 * n
+                    : reinterpret_cast<uint16_t*>(smem + kTabBytes + 16);
+  const uint32_t tid = threadIdx.x, nt = blockDim.x, w2 = 2 * n;
+  const uint8_t* m = in + (size_t)blockIdx.x * n * n * (F::kField / 8);
+  build_log_exp(lg, ex);
+  for (uint32_t t = tid; t < n * w2; t += nt) {
+    const uint32_t r = t / w2, c = t % w2;
+    w[t] = (uint16_t)(c < n ? F::load(m, (size_t)r * n + c) : ((c - n) == r ? 1u : 0u));
+  }
+  __syncthreads();
+  if (!gauss_jordan<F>(w, n, lg, ex, s_piv)) {
+    if (tid == 0) singular[blockIdx.x] = 1u;
+    return;
+  }
+  uint8_t* o = out + (size_t)blockIdx.x * n * n * (F::kField / 8);
+  for (uint32_t t = tid; t < n * n; t += nt) F::store(o, t, w[(t / n) * w2 + n + (t % n)]);
   if (tid == 0) singular[blockIdx.x] = 0u;
 }
 
-// One workgroup per stripe: the reconstruct planning of core.rs:733-923 on the
-// device -- the valid/invalid partition (core.rs:801-841), the k x k inverse of
-// the valid rows (core.rs:711-722; Gauss-Jordan in LDS, the unique inverse of
-// matrix.rs:195-261), the rows that rebuild each missing data shard
-// (core.rs:850-861) and, unless data_only, each missing parity shard composed
-// over the valid inputs (core.rs:872-918, exact GF algebra) -- written as the
-// stripe's CodeArgs for gf8_code_desc_kernel.  k <= kMaxIn, p <= kMaxOut.
-__global__ __launch_bounds__(256) void gf8_recon_plan_kernel(
-    const uint8_t* __restrict__ matrix, const uint8_t* __restrict__ present, uint32_t k,
-    uint32_t total, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint64_t off,
-    uint64_t len, uint64_t n_vec, CodeArgs* descs) {
-  __shared__ uint8_t lg[256], ex[512];
-  __shared__ uint8_t valid[kMaxIn], miss[kMaxIn + kMaxOut];
-  __shared__ uint8_t w[kMaxIn][2 * kMaxIn];
-  __shared__ uint8_t drow[kMaxIn][kMaxIn];
-  __shared__ int s_nout, s_piv;
-  const uint32_t s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const uint8_t* pres = present + (size_t)s * total;
-  CodeArgs& d = descs[s];
+// ---------------------------------------------------------------------------
+// Device reconstruct planner, one workgroup per stripe, either field, any codec
+// whose batch fits the LDS budget (recon_plan_lds): the planning of
+// core.rs:733-923 for the stripe's own erasure pattern, written as CodeArgs
+// descriptors for the table kernels' descriptor variants.
+//  * valid = the first k present shards in index order (core.rs:801-841): the
+//    k - e present data shards, then R, the first e present parity rows;
+//    S = the e missing data shards; outputs = missing data, then (unless
+//    data_only) missing parity, ascending.
+//  * Only the e x e matrix A = P[R][S] is inverted (Gauss-Jordan in LDS): the
+//    k x k decode matrix of core.rs:711-722 restricted to what the outputs
+//    need.  With W[o] = A^-1 row u for missing data S_u, and
+//    W[o] = sum_u P[r][S_u] A^-1[u] for missing parity r, the composed row
+//    over the valid inputs is
+//        on parity input R_t:     W[o][t]
+//        on present data d:       [r missing: P[r][d]] + sum_t W[o][t] P[R_t][d]
+//    -- the unique linear map from the k valid shards to each output, so the
+//    bytes equal the host planner's (plan_reconstruct) and the reference's.
+//  * Descriptor (ib, ob) of a stripe codes outputs [16 ob, 16 ob + 16) from
+//    inputs [32 ib, 32 ib + 32), accumulating for ib > 0; descs[(ib * n_grp +
+//    stripe) * n_ob + ob].  A block with nothing to rebuild gets n_out = 0.
+// Layout of the dynamic LDS: tables | ints | valid[k] | miss[T] | S[e_cap] |
+// R[e_cap] | A[e_cap][2 e_cap] | W[nout_cap][e_cap] (uint16).
+template <class F>
+__global__ __launch_bounds__(256) void recon_plan_kernel(
+    const uint16_t* __restrict__ P, const uint8_t* __restrict__ present, uint32_t k, uint32_t T,
+    uint32_t data_only, uint32_t e_cap, uint8_t* base, uint64_t shard_bytes, uint64_t off,
+    uint64_t len, uint64_t n_vec, uint32_t n_grp, uint32_t n_ib, uint32_t n_ob, CodeArgs* descs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* lg = smem;
+  uint8_t* ex = smem + 256;
+  int* sc = reinterpret_cast<int*>(smem + kTabBytes);  // e, n_out, pivot, ok
+  uint16_t* valid = reinterpret_cast<uint16_t*>(smem + kTabBytes + 16);
+  uint16_t* miss = valid + k;
+  uint16_t* S = miss + T;
+  uint16_t* R = S + e_cap;
+  uint16_t* A = R + e_cap;
+  uint16_t* W = A + 2 * e_cap * e_cap;
+  const uint32_t sl = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const uint8_t* pres = present + (size_t)sl * T;
+  build_log_exp(lg, ex);
   if (tid == 0) {
-    uint32_t b = 1;
-    for (uint32_t l = 0; l < 255; ++l) {
-      lg[b] = (uint8_t)l;
-      ex[l] = ex[l + 255] = (uint8_t)b;
-      b <<= 1;
-      if (b & 0x100u) b ^= 0x11Du;
-    }
-    lg[0] = 0;
-    ex[510] = ex[511] = 0;
-    uint32_t nv = 0, nm = 0;
-    for (uint32_t row = 0; row < total; ++row) {
+    uint32_t nv = 0, ne = 0, nr = 0, nm = 0;
+    for (uint32_t row = 0; row < T; ++row) {
       if (pres[row]) {
-        if (nv < k) valid[nv++] = (uint8_t)row;
-      } else if (row < k || !data_only) {
-        miss[nm++] = (uint8_t)row;  // data first: indices ascend
+        if (nv < k) {
+          valid[nv++] = (uint16_t)row;
+          if (row >= k) R[nr++] = (uint16_t)(row - k);
+        }
+      } else if (row < k) {
+        S[ne++] = (uint16_t)row;
+        miss[nm++] = (uint16_t)row;
+      } else if (!data_only) {
+        miss[nm++] = (uint16_t)row;
       }
     }
-    s_nout = (int)nm;
-    d.n_out = nm;
-    d.n_in = k;
+    sc[0] = (int)ne;
+    sc[1] = (int)nm;
+    sc[3] = 1;
+  }
+  __syncthreads();
+  const uint32_t e = (uint32_t)sc[0], nm = (uint32_t)sc[1];
+  if (e) {  // [A | I], then A^-1 in the right half
+    const uint32_t w2 = 2 * e;
+    for (uint32_t t = tid; t < e * w2; t += nt) {
+      const uint32_t r = t / w2, c = t % w2;
+      A[t] = c < e ? P[(size_t)R[r] * k + S[c]] : (uint16_t)((c - e) == r ? 1 : 0);
+    }
+    __syncthreads();
+    if (!gauss_jordan<F>(A, e, lg, ex, &sc[2]) && tid == 0) sc[3] = 0;  // impossible for MDS
+    __syncthreads();
+    for (uint32_t t = tid; t < nm * e; t += nt) {
+      const uint32_t o = t / e, u = t % e, m = miss[o];
+      uint32_t v = 0;
+      if (m < k) {
+        v = A[o * w2 + e + u];  // outputs o < e are S in order
+      } else {
+        for (uint32_t q = 0; q < e; ++q)
+          v ^= F::mul(lg, ex, P[(size_t)(m - k) * k + S[q]], A[q * w2 + e + u]);
+      }
+      W[o * e + u] = (uint16_t)v;
+    }
+  }
+  __syncthreads();
+  const uint32_t n_out = sc[3] ? nm : 0u;  // singular: leave the stripe untouched
+  uint8_t* sbase = base + (uint64_t)sl * T * shard_bytes + off;
+  for (uint32_t b = tid; b < n_ib * n_ob; b += nt) {
+    const uint32_t ib = b / n_ob, ob = b % n_ob;
+    CodeArgs& d = descs[((size_t)ib * n_grp + sl) * n_ob + ob];
+    const uint32_t ni = k - 32 * ib < 32u ? k - 32 * ib : 32u;
+    const uint32_t no = 16 * ob < n_out ? (n_out - 16 * ob < 16u ? n_out - 16 * ob : 16u) : 0u;
+    d.n_in = ni;
+    d.n_out = no;
     d.n_stripes = 1;
     d.stripe_stride = 0;
     d.n_vec = n_vec;
     d.len = len;
     d.mismatch = nullptr;
     d.mode = kStore;
-    d.accumulate = 0;
+    d.accumulate = ib > 0 ? 1u : 0u;
     d.per_stripe = 0;
-  }
-  __syncthreads();
-  const uint32_t n_out = (uint32_t)s_nout;
-  if (n_out == 0) return;  // uniform
-  const uint8_t* sbase = base + (uint64_t)s * total * shard_bytes + off;
-  for (uint32_t i = tid; i < k; i += nt) d.in[i] = sbase + (uint64_t)valid[i] * shard_bytes;
-  for (uint32_t o = tid; o < n_out; o += nt) {
-    d.out[o] = const_cast<uint8_t*>(sbase) + (uint64_t)miss[o] * shard_bytes;
-    d.cmp[o] = nullptr;
-  }
-  // [M_valid | I] and Gauss-Jordan
-  const uint32_t w2 = 2 * k;
-  for (uint32_t t = tid; t < k * w2; t += nt) {
-    const uint32_t r = t / w2, c = t % w2;
-    w[r][c] = c < k ? matrix[valid[r] * k + c] : (uint8_t)((c - k) == r ? 1 : 0);
-  }
-  __syncthreads();
-  for (uint32_t col = 0; col < k; ++col) {
-    if (tid == 0) {
-      int piv = -1;
-      for (uint32_t r = col; r < k; ++r)
-        if (w[r][col]) { piv = (int)r; break; }
-      s_piv = piv;
+    for (uint32_t i = 0; i < ni; ++i) d.in[i] = sbase + (uint64_t)valid[32 * ib + i] * shard_bytes;
+    for (uint32_t o = 0; o < no; ++o) {
+      d.out[o] = sbase + (uint64_t)miss[16 * ob + o] * shard_bytes;
+      d.cmp[o] = nullptr;
     }
-    __syncthreads();
-    const int piv = s_piv;
-    if (piv < 0) {  // singular: impossible for this MDS code; leave the stripe untouched
-      if (tid == 0) d.n_out = 0;
-      return;
-    }
-    if ((uint32_t)piv != col) {
-      for (uint32_t c = tid; c < w2; c += nt) {
-        const uint8_t t0 = w[col][c];
-        w[col][c] = w[piv][c];
-        w[piv][c] = t0;
-      }
-      __syncthreads();
-    }
-    const uint32_t inv = ex[255 - lg[w[col][col]]];
-    __syncthreads();
-    for (uint32_t c = tid; c < w2; c += nt) w[col][c] = (uint8_t)gmul(lg, ex, inv, w[col][c]);
-    __syncthreads();
-    for (uint32_t t = tid; t < k * w2; t += nt) {
-      const uint32_t r = t / w2, c = t % w2;
-      if (r == col || c == col) continue;
-      const uint32_t f = w[r][col];
-      if (f) w[r][c] ^= (uint8_t)gmul(lg, ex, f, w[col][c]);
-    }
-    __syncthreads();
-    for (uint32_t r = tid; r < k; r += nt)
-      if (r != col) w[r][col] = 0;
-    __syncthreads();
   }
-  // data_row(j): unit vector for a present data shard (always among the valid
-  // rows), row j of the inverse for a missing one.
-  for (uint32_t t = tid; t < k * k; t += nt) {
-    const uint32_t j = t / k, i = t % k;
-    drow[j][i] = (valid[i] == j) ? 1 : 0;
-  }
-  __syncthreads();
-  for (uint32_t t = tid; t < k * k; t += nt) {
-    const uint32_t j = t / k, i = t % k;
-    bool present_j = false;
-    for (uint32_t q = 0; q < k; ++q) present_j |= valid[q] == j;
-    if (!present_j) drow[j][i] = w[j][k + i];
-  }
-  __syncthreads();
   for (uint32_t t = tid; t < n_out * k; t += nt) {
-    const uint32_t o = t / k, i = t % k, m = miss[o];
-    uint32_t v = 0;
-    if (m < k) {
-      v = drow[m][i];
+    const uint32_t o = t / k, i = t % k, v = valid[i], m = miss[o];
+    uint32_t c;
+    if (v >= k) {
+      c = W[o * e + (i - (k - e))];
     } else {
-      for (uint32_t j = 0; j < k; ++j) v ^= gmul(lg, ex, matrix[m * k + j], drow[j][i]);
+      c = m >= k ? P[(size_t)(m - k) * k + v] : 0u;
+      for (uint32_t q = 0; q < e; ++q) c ^= F::mul(lg, ex, W[o * e + q], P[(size_t)R[q] * k + v]);
     }
-    d.coef[o][i] = (uint16_t)v;
+    descs[((size_t)(i / 32) * n_grp + sl) * n_ob + o / 16].coef[o % 16][i % 32] = (uint16_t)c;
   }
 }
 
@@ -1063,33 +1145,45 @@ hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
-                              uint32_t total, uint32_t data_only, uint8_t* base,
-                              uint64_t shard_bytes, uint64_t off, uint64_t len,
-                              uint32_t n_stripes, CodeArgs* d_descs, hipStream_t stream) {
-  if (k == 0 || k > (uint32_t)kMaxIn || total - k > (uint32_t)kMaxOut || n_stripes == 0 ||
-      off + len > shard_bytes || len == 0)
+size_t recon_plan_lds(uint32_t k, uint32_t T, uint32_t e_cap, uint32_t nout_cap) {
+  return kTabBytes + 16 +
+         2 * ((size_t)k + T + 2 * (size_t)e_cap + 2 * (size_t)e_cap * e_cap + (size_t)nout_cap * e_cap);
+}
+
+hipError_t launch_recon_plan(int field, const uint16_t* d_parity, const uint8_t* d_present,
+                             uint32_t k, uint32_t T, uint32_t data_only, uint32_t e_cap,
+                             uint32_t nout_cap, uint8_t* base, uint64_t shard_bytes, uint64_t off,
+                             uint64_t len, uint32_t n_grp, CodeArgs* d_descs, hipStream_t stream) {
+  const size_t lds = recon_plan_lds(k, T, e_cap, nout_cap);
+  if (k == 0 || T <= k || nout_cap == 0 || n_grp == 0 || off + len > shard_bytes || len == 0 ||
+      lds > kReconPlanLdsMax || (field != 8 && field != 16))
     return hipErrorInvalidValue;
   const bool al = (reinterpret_cast<uintptr_t>(base + off) % 16u) == 0 && shard_bytes % 16u == 0;
   const uint64_t n_vec = al ? len / 16u : 0;
-  hipLaunchKernelGGL(gf8_recon_plan_kernel, dim3(n_stripes), dim3(256), 0, stream, d_matrix,
-                     d_present, k, total, data_only, base, shard_bytes, off, len, n_vec, d_descs);
+  const uint32_t n_ib = (k + 31) / 32, n_ob = (nout_cap + 15) / 16;
+  hipLaunchKernelGGL(field == 8 ? recon_plan_kernel<PlanF8> : recon_plan_kernel<PlanF16>,
+                     dim3(n_grp), dim3(256), lds, stream, d_parity, d_present, k, T, data_only,
+                     e_cap, base, shard_bytes, off, len, n_vec, n_grp, n_ib, n_ob, d_descs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint64_t units = n_vec ? n_vec : len + 1;
-  uint64_t gx = (2048u + n_stripes - 1) / n_stripes;
+  const uint64_t rows = (uint64_t)n_grp * n_ob;  // descriptors per input block
+  const uint64_t units = n_vec ? n_vec : (field == 8 ? len : len / 2) + 1;
+  uint64_t gx = (2048u + rows - 1) / rows;
   const uint64_t want = (units + kBlock - 1) / kBlock;
   if (gx > want) gx = want;
   if (gx < 1) gx = 1;
   void (*fn)(const CodeArgs*) =
-      g_opt.nontemporal ? gf8_code_desc_kernel<true> : gf8_code_desc_kernel<false>;
-  for (uint32_t y0 = 0; y0 < n_stripes; y0 += 65535u) {
-    const uint32_t gy = n_stripes - y0 < 65535u ? n_stripes - y0 : 65535u;
-    hipLaunchKernelGGL(fn, dim3((uint32_t)gx, gy, 1),
-                       dim3(kBlock, 1, 1), 0, stream, d_descs + y0);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
+      field == 8 ? (g_opt.nontemporal ? gf8_code_desc_kernel<true> : gf8_code_desc_kernel<false>)
+                 : (g_opt.nontemporal ? gf16_code_desc_kernel<true> : gf16_code_desc_kernel<false>);
+  note_kernel("table-desc gf%d %u+%u", field, k, T - k);
+  for (uint32_t ib = 0; ib < n_ib; ++ib)  // later input blocks accumulate: stream order
+    for (uint64_t y0 = 0; y0 < rows; y0 += 65535u) {
+      const uint32_t gy = (uint32_t)(rows - y0 < 65535u ? rows - y0 : 65535u);
+      hipLaunchKernelGGL(fn, dim3((uint32_t)gx, gy, 1), dim3(kBlock, 1, 1), 0, stream,
+                         d_descs + (size_t)ib * rows + y0);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
   return hipSuccess;
 }
 
@@ -1164,17 +1258,18 @@ hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed, uint6
   return hipGetLastError();
 }
 
-hipError_t launch_gf8_invert(const uint8_t* in, uint8_t* out, uint32_t* singular, uint32_t n,
-                             uint32_t batch, hipStream_t stream) {
-  if (n == 0 || n > (uint32_t)kInvMax || batch == 0) return hipErrorInvalidValue;
-  const size_t lds = 784 + (size_t)n * 2 * n;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gf8_invert_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(gf8_invert_kernel, dim3(batch), dim3(1024), lds, stream, in, out, singular, n);
+hipError_t launch_invert(int field, const uint8_t* in, uint8_t* out, uint32_t* singular,
+                         uint32_t n, uint32_t batch, uint16_t* gws, hipStream_t stream) {
+  if (n == 0 || batch == 0 || (field != 8 && field != 16) || (field == 8 && n > 255))
+    return hipErrorInvalidValue;
+  const size_t w = (size_t)n * 2 * n * 2;
+  if (!gws && w > kInvLds) return hipErrorInvalidValue;
+  const size_t lds = kTabBytes + 16 + (gws ? 0 : w);
+  auto fn = field == 8 ? invert_kernel<PlanF8> : invert_kernel<PlanF16>;
+  hipLaunchKernelGGL(fn, dim3(batch), dim3(1024), lds, stream, in, out, singular, n, gws);
   return hipGetLastError();
 }
+
+size_t invert_lds_max_bytes() { return kInvLds; }
 
 }  // namespace rse

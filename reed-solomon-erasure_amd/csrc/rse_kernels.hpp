@@ -191,17 +191,22 @@ struct WideHdr {
 // field is 8 or 16.  Returns a hipError_t.
 hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
 
-// Device-resident batched reconstruct (GF(2^8), k <= kMaxIn, p <= kMaxOut):
-// per stripe, plan (partition, inverse, composed rows) into d_descs[stripe]
-// on the device, then code every stripe from its descriptor.  `base` holds
-// n_stripes flat stripes of `total` shards of shard_bytes each; d_present is
-// n_stripes x total flags; d_matrix the (total x k) encoding matrix.
-// Only bytes [off, off + len) of every shard are coded (the bit-sliced batch
-// path codes the whole chunks before).
-hipError_t launch_recon_batch(const uint8_t* d_matrix, const uint8_t* d_present, uint32_t k,
-                              uint32_t total, uint32_t data_only, uint8_t* base,
-                              uint64_t shard_bytes, uint64_t off, uint64_t len,
-                              uint32_t n_stripes, CodeArgs* d_descs, hipStream_t stream);
+// Device-resident batched reconstruct planner (rse_kernels.hip
+// recon_plan_kernel), either field, any codec: per stripe of a group of n_grp
+// flat stripes (`base`: the group's first stripe; d_present: its n_grp x T
+// flags), the partition, the e x e syndrome inverse and the composed rows are
+// computed on the device and written as CodeArgs descriptors -- ceil(k / 32)
+// input blocks x ceil(nout_cap / 16) output blocks per stripe -- then the
+// table kernels code bytes [off, off + len) of every shard from them.
+// d_parity: the p x k parity rows (uint16 elements).  e_cap / nout_cap: the
+// most missing data shards / outputs of any stripe in the group.  Needs
+// recon_plan_lds(...) <= kReconPlanLdsMax.
+constexpr size_t kReconPlanLdsMax = 65536;
+size_t recon_plan_lds(uint32_t k, uint32_t T, uint32_t e_cap, uint32_t nout_cap);
+hipError_t launch_recon_plan(int field, const uint16_t* d_parity, const uint8_t* d_present,
+                             uint32_t k, uint32_t T, uint32_t data_only, uint32_t e_cap,
+                             uint32_t nout_cap, uint8_t* base, uint64_t shard_bytes, uint64_t off,
+                             uint64_t len, uint32_t n_grp, CodeArgs* d_descs, hipStream_t stream);
 
 // Table kernels only (launch_code minus the bit-sliced dispatch).
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
@@ -327,11 +332,15 @@ const char* last_kernel();
 hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed,
                                 uint64_t shard_id, hipStream_t stream);
 
-// Device Gauss-Jordan inversion of n x n matrices over GF(2^8) (batched: one
-// workgroup per matrix).  in/out are device pointers to batch*n*n bytes;
-// singular[b] receives 1 for a singular matrix.
-hipError_t launch_gf8_invert(const uint8_t* in, uint8_t* out, uint32_t* singular,
-                             uint32_t n, uint32_t batch, hipStream_t stream);
+// Device Gauss-Jordan inversion of n x n matrices over GF(2^8) or GF(2^16)
+// (batched: one workgroup per matrix).  in/out: batch x n x n elements of the
+// field's bytes (GF(2^16): [u8;2] {coefficient of x, constant}); singular[b]
+// receives 1 for a singular matrix.  The augmented matrix lives in LDS when
+// its n x 2n uint16 entries fit invert_lds_max_bytes(), else in gws (batch x
+// n x 2n uint16, device memory; nullptr: LDS only).
+hipError_t launch_invert(int field, const uint8_t* in, uint8_t* out, uint32_t* singular,
+                         uint32_t n, uint32_t batch, uint16_t* gws, hipStream_t stream);
+size_t invert_lds_max_bytes();
 #endif  // RSE_JIT
 
 }  // namespace rse

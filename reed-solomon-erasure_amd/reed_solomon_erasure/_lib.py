@@ -24,7 +24,7 @@ EXPORTS = (
     "rse_encode_flat", "rse_verify_flat", "rse_reconstruct_data_flat", "rse_reconstruct_batch",
     "rse_code_shards",
     "rse_code_shards_host", "rse_gf8_mul_slice", "rse_gal_mul", "rse_gal_mul_xor",
-    "rse_gf16_mul_slice", "rse_gf8_invert_batch",
+    "rse_gf16_mul_slice", "rse_gf8_invert_batch", "rse_gf16_invert_batch",
     "rse_encode_host", "rse_encode_host_flat", "rse_encode_sep_host", "rse_encode_single_host",
     "rse_encode_single_sep_host", "rse_verify_host", "rse_verify_with_buffer_host",
     "rse_verify_host_flat", "rse_reconstruct_host", "rse_reconstruct_data_host",
@@ -67,6 +67,7 @@ _SIGS = {
     "rse_code_shards": (_c.c_int, [_c.c_int, _u8p, _sz, _sz, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_gf8_mul_slice": (_c.c_int, [_c.c_uint8, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_gf8_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "rse_gf16_invert_batch": (_c.c_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "rse_encode_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp]),
     "rse_verify_host": (_c.c_int, [_vp, _vp, _szp, _sz, _ip, _vp]),
     "rse_encode_sep_host": (_c.c_int, [_vp, _vp, _szp, _sz, _vp, _szp, _sz, _vp]),

@@ -358,18 +358,21 @@ def test_scratch_pool_short_lived_threads(R):
         r.encode_host(shards)
         assert r.verify_host(shards)
 
-    work()
-    torch.cuda.synchronize()
-    free0 = torch.cuda.mem_get_info()[0]
-    for wave in range(12):
+    def wave():
         ts = [threading.Thread(target=work) for _ in range(4)]
         for t in ts:
             t.start()
         for t in ts:
             t.join()
-    torch.cuda.synchronize()
-    assert lib.rse_get_option(24) <= 4 + 1  # the idle cap (+ nothing leased now)
-    assert free0 - torch.cuda.mem_get_info()[0] < (256 << 20)
+        torch.cuda.synchronize()
+
+    wave()  # up to 4 sets in use at once, then kept idle (the cap)
+    free1 = torch.cuda.mem_get_info()[0]
+    live1 = lib.rse_get_option(24)
+    for _ in range(11):  # 44 more threads, each gone after its call
+        wave()
+    assert lib.rse_get_option(24) <= 4 and lib.rse_get_option(24) <= max(live1, 4)
+    assert free1 - torch.cuda.mem_get_info()[0] < (64 << 20)  # nothing piles up per thread
 
 
 def test_field_mul_slice_both_fields(R):

@@ -435,24 +435,32 @@ def test_flat_small_shards_many_stripes(R, field, k, p, n, stripes):
     assert (back[:, :k] == got[:, :k]).all()
 
 
-@pytest.mark.parametrize("field,k,p,n,stripes,bs", [
-    (8, 10, 4, 4096 + 16, 33, 0),     # device planner, aligned
-    (8, 10, 4, 1037, 9, 0),           # device planner, byte path
-    (8, 32, 16, 256, 5, 0),           # device planner at its limits
-    (8, 1, 1, 64, 3, 0),
-    (8, 40, 20, 512, 3, 0),           # host-planner fallback (k > 32)
-    (16, 20, 8, 300, 4, 0),           # host-planner fallback (GF(2^16))
-    (8, 10, 4, 2 * 16384 + 48, 9, 1),   # bit-sliced syndrome batch + table-planner tail
-    (8, 10, 2, 16384, 5, 1),            # bit-sliced only
-    (16, 20, 8, 16384 + 8, 5, 1),       # GF(2^16) device planner + host-planner tail
-    (8, 12, 4, 2 * 16384, 7, 1),        # run-time specialised codec
-    (16, 6, 3, 8192 * 3, 4, 1),         # run-time specialised GF(2^16) codec
+@pytest.mark.parametrize("field,k,p,n,stripes,bs,hp", [
+    (8, 10, 4, 4096 + 16, 33, 0, 0),     # device planner, aligned
+    (8, 10, 4, 1037, 9, 0, 0),           # device planner, byte path
+    (8, 32, 16, 256, 5, 0, 0),           # one descriptor block per stripe
+    (8, 1, 1, 64, 3, 0, 0),
+    (8, 40, 20, 512, 3, 0, 0),           # k > 32: 2 input x 2 output blocks
+    (8, 100, 60, 96, 3, 0, 0),           # 4 x 4 blocks, up to 60 erasures
+    (16, 20, 8, 300, 4, 0, 0),           # GF(2^16) device planner
+    (16, 300, 60, 64, 3, 0, 0),          # GF(2^16) past 256 shards: 10 x 4 blocks
+    (16, 33, 17, 1001, 3, 0, 0),         # GF(2^16), byte path, odd blocks
+    (16, 1, 40000, 8, 2, 0, 1),          # past the planner's LDS budget: host planner
+    (8, 10, 4, 2 * 16384 + 48, 9, 1, 0),   # bit-sliced syndrome batch + device-planned tail
+    (8, 10, 2, 16384, 5, 1, 0),            # bit-sliced only
+    (16, 20, 8, 16384 + 8, 5, 1, 0),       # GF(2^16) bit-sliced + device-planned tail
+    (8, 12, 4, 2 * 16384, 7, 1, 0),        # run-time specialised codec
+    (16, 6, 3, 8192 * 3, 4, 1, 0),         # run-time specialised GF(2^16) codec
 ])
-def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs):
+def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, hp):
     """rse_reconstruct_batch: every stripe with its own erasure pattern, against
     the oracle's reconstruct of each stripe (core.rs:680/690 semantics).  bs:
     the whole 16 KiB chunks run on the bit-sliced syndrome kernels from
-    per-stripe descriptors planned on the device (one launch, counted)."""
+    per-stripe descriptors planned on the device (one launch, counted); the
+    rest on the table kernels from descriptors the device planner writes
+    (either field, any k and p).  hp: stripes planned on the host per call
+    (RSE_OPT_HOST_PLANNED_STRIPES) -- none unless the batch is past the
+    device planner's LDS budget."""
     rng = np.random.default_rng(field * 1000 + k * 31 + p)
     lib = R._lib.load()
     old_jit = lib.rse_get_option(9)
@@ -485,9 +493,11 @@ def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs):
             want[s] = np.stack(ob)
         d = dev(buf)
         n0 = lib.rse_get_option(6)
+        h0 = lib.rse_get_option(25)
         r.reconstruct_batch(d, n, stripes, present, data_only=data_only)
         got = host(d).reshape(stripes, T, n * es)
         assert lib.rse_get_option(6) - n0 == bs, data_only
+        assert lib.rse_get_option(25) - h0 == (stripes if hp else 0), data_only
         assert (got == want).all(), data_only
         # every data shard is back; parity back unless data_only
         for s in range(stripes):
@@ -999,6 +1009,55 @@ def test_device_inversion_matches_oracle(R):
     sing = torch.zeros(1, dtype=torch.int32, device="cuda")
     lib.rse_gf8_invert_batch(src.data_ptr(), dst.data_ptr(), sing.data_ptr(), 2, 1, stream)
     assert host(sing)[0] == 1
+
+
+def test_device_inversion_gf16_matches_oracle(R):
+    """rse_gf16_invert_batch (matrix.rs:195-261 over galois_16): decode
+    submatrices of GF(2^16) codecs (20+8, 300+60 past 256 shards) and random
+    matrices, in LDS (n <= 127) and in the device workspace (n = 128, 300),
+    against the oracle's matrix_invert(16, ...); singular matrices flagged."""
+    lib = R._lib.load()
+    rng = np.random.default_rng(37)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    cases = []
+    for k, p, count in ((20, 8, 24), (300, 60, 2)):
+        m = O.Codec(16, k, p).matrix()
+        for _ in range(count):
+            erased = rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False)
+            valid = [i for i in range(k + p) if i not in erased][:k]
+            cases.append(m[valid])
+    for n in (1, 2, 7, 64, 127, 128):
+        for _ in range(2):
+            cases.append(rng.integers(0, 256, (n, n, 2), dtype=np.uint8))
+    by_n = {}
+    for a in cases:
+        try:
+            w = O.matrix_invert(16, a)
+        except ValueError:
+            continue
+        by_n.setdefault(a.shape[0], []).append((a, w))
+    assert {20, 300, 127, 128} <= set(by_n)
+    for n, items in by_n.items():
+        src = dev(np.stack([a for a, _ in items]))
+        dst = torch.empty_like(src)
+        sing = torch.full((len(items),), 7, dtype=torch.int32, device="cuda")
+        assert lib.rse_gf16_invert_batch(src.data_ptr(), dst.data_ptr(), sing.data_ptr(), n,
+                                         len(items), stream) == 0
+        assert (host(sing) == 0).all(), n
+        assert (host(dst) == np.stack([w for _, w in items])).all(), n
+    # singular: a repeated row, and a zero column, next to an invertible one
+    good = by_n[20][0][0]
+    bad1 = good.copy()
+    bad1[5] = bad1[2]
+    bad2 = good.copy()
+    bad2[:, 7] = 0
+    src = dev(np.stack([bad1, good, bad2]))
+    dst = torch.zeros_like(src)
+    sing = torch.full((3,), 7, dtype=torch.int32, device="cuda")
+    assert lib.rse_gf16_invert_batch(src.data_ptr(), dst.data_ptr(), sing.data_ptr(), 20, 3,
+                                     stream) == 0
+    assert host(sing).tolist() == [1, 0, 1]
+    assert (host(dst)[1] == by_n[20][0][1]).all()
 
 
 # ------------------------------------------------ quickcheck-style round trips
