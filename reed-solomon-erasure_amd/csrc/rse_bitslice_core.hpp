@@ -513,6 +513,93 @@ __device__ __forceinline__ void wide_rounds(uint32_t (&acc)[C::p * 16], u32x4 (&
   }
 }
 
+// wide_rounds with D inputs in flight per wave instead of one.  A wave's own
+// inputs are R * W + WI over the rounds R; in round R it loads round R + D's
+// (ring of D + 1 slots, indexed at compile time so it stays in VGPRs).  Past
+// the chunk's last round it loads the first rounds of the workgroup's next
+// chunk (next_off, ~0 if none), so loads stay in flight through the output
+// phase too.  Why: one 4 KiB input per wave in flight is 16 KiB per 4-wave
+// workgroup, ~32 KiB per CU at 2 workgroups -- ~8 MiB over the chip, which at
+// ~2 us of loaded HBM latency caps the read rate near 4 TB/s whatever the
+// VALU does (Little's law); D inputs per wave raise that cap D-fold.
+template <class C, int W, int WI, int D, int R, class A>
+__device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
+                                                 u32x4 (&buf)[D + 1][4], const A& a, uint64_t off,
+                                                 uint64_t next_off, WidePlanes<W>& lds, uint32_t& g,
+                                                 uint32_t lane) {
+  constexpr int K = C::k, NR = (K + W - 1) / W;
+  if constexpr (R < NR) {
+    constexpr int mine = R * W + WI, ahead = R + D;
+    if constexpr (ahead < NR) {
+      if constexpr (ahead * W + WI < K) load4<false, 1024u>(buf[ahead % (D + 1)], a.in[ahead * W + WI] + off);
+    } else if constexpr ((ahead - NR) * W + WI < K) {
+      if (next_off != ~0ull) load4<false, 1024u>(buf[ahead % (D + 1)], a.in[(ahead - NR) * W + WI] + next_off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint4(&set)[W][4][64] = lds[g & 1u];
+    if constexpr (mine < K) {
+      uint32_t pl[16];
+      slice<typename C::Field>(buf[R % (D + 1)], pl);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        set[WI][q4][lane] = make_uint4(pl[q4 * 4], pl[q4 * 4 + 1], pl[q4 * 4 + 2], pl[q4 * 4 + 3]);
+    }
+    __syncthreads();
+    wide_code_round<C, W, R, 0>(acc, set, lane);
+    ++g;
+    wide_rounds_deep<C, W, WI, D, R + 1, A>(acc, buf, a, off, next_off, lds, g, lane);
+  }
+}
+
+// Wave WI of W; C its share of the outputs (O0 the first).  All W waves call
+// this with the same `lds` (one workgroup-wide array).  D: inputs in flight
+// per wave (wide_rounds_deep); 1 is wide_rounds.
+template <class C, int O0, int W, int WI, int D, class A>
+__device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& lds) {
+  const WideHdr& h = a.h;
+  constexpr int K = C::k, NR = (K + W - 1) / W;
+  const uint64_t total = h.chunks_per_stripe * h.n_stripes;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = lane * 16u;
+  const uint32_t mode = h.mode;
+  bool diff = false;
+  uint32_t g = 0;
+  auto chunk_off = [&](uint64_t c) {
+    const uint64_t stripe = c / h.chunks_per_stripe, chunk = c - stripe * h.chunks_per_stripe;
+    return stripe * h.stripe_stride + chunk * 4096u + lane_off;
+  };
+  u32x4 buf[D + 1][4];
+  if (blockIdx.x < total) {
+    const uint64_t off0 = chunk_off(blockIdx.x);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (j < NR && j * W + WI < K) load4<false, 1024u>(buf[j], a.in[j * W + WI] + off0);
+  }
+  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const uint64_t off = chunk_off(c);
+    const uint64_t next = c + gridDim.x;
+    const uint64_t next_off = next < total ? chunk_off(next) : ~0ull;
+    uint32_t acc[C::p * 16];
+    wide_rounds_deep<C, W, WI, D, 0, A>(acc, buf, a, off, next_off, lds, g, lane);
+    if constexpr (NR % (D + 1) != 0) {  // the next chunk's rounds j into slots j
+      u32x4 t[D][4];
+#pragma unroll
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[j][q] = buf[(NR + j) % (D + 1)][q];
+#pragma unroll
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) buf[j][q] = t[j][q];
+    }
+    store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
+    if (h.per_stripe && diff) {
+      flag_mismatch(h.mismatch + (c / h.chunks_per_stripe));
+      diff = false;
+    }
+  }
+  if (mode != kStore && diff) flag_mismatch(h.mismatch);
+}
+
 // Wave WI of W; C its share of the outputs (O0 the first).  All W waves call
 // this with the same `lds` (one workgroup-wide array).
 template <class C, int O0, int W, int WI, class A>

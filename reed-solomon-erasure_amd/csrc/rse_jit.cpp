@@ -243,8 +243,9 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       wide_share(p, w, &o0, &n);
       if (shared)
         std::snprintf(buf, sizeof buf,
-                      "    case %d: rse::wide_body_lds<rse::JitWide%d, %u, %d, %d>(a, lds); break;\n",
-                      w, w, o0, W, w);
+                      "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d>(a, lds); "
+                      "break;\n",
+                      w, w, o0, W, w, (int)get_option(26));
       else
         std::snprintf(buf, sizeof buf,
                       "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);

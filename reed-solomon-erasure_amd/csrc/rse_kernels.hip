@@ -785,6 +785,8 @@ struct Options {
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
   int64_t host_copy_2d = 1;       // host pipeline: 2D copies for runs of a flat buffer's shards
   int64_t jit_exact = 1;          // run-time networks: exact-decomposition temporaries
+  int64_t wide_depth = 2;         // wide modules: inputs in flight per wave (1..4)
+  int64_t recon_depth = 1;        // syndrome reconstruct: inputs in flight per lane (1..4)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1207,6 +1209,8 @@ int set_option(int key, int64_t value) {
     case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;
     case 21: g_opt.host_copy_2d = value ? 1 : 0; return 0;
     case 23: g_opt.jit_exact = value ? 1 : 0; return 0;
+    case 26: g_opt.wide_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
+    case 27: g_opt.recon_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     default: return -1;
   }
 }
@@ -1244,6 +1248,8 @@ int64_t get_option(int key) {
     case 20: return g_opt.wide_occupancy;
     case 21: return g_opt.host_copy_2d;
     case 23: return g_opt.jit_exact;
+    case 26: return g_opt.wide_depth;
+    case 27: return g_opt.recon_depth;
     default: return -1;
   }
 }
