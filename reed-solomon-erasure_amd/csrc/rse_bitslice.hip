@@ -168,6 +168,25 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
   bitslice_recon_desc_body<C, NT, NS>(descs, chunks_per_stripe, n_stripes);
 }
 
+template <class C, int NS>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_w4_kernel(
+    const BsReconArgs* descs, uint64_t cps4, uint64_t n_stripes, uint64_t base) {
+  bitslice_recon_desc_body_w4<C, true, NS>(descs, cps4, n_stripes, base);
+}
+
+// The same with D inputs in flight per lane (RSE_OPT_RECON_DEPTH; Horner mixing).
+template <class C, int NS, int D>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_deep_kernel(
+    const BsReconArgs a, uint64_t chunks_per_stripe) {
+  bitslice_recon_body_deep<C, true, NS, D>(a, chunks_per_stripe);
+}
+
+template <class C, int NS, int D>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_deep_kernel(
+    const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
+  bitslice_recon_desc_body_deep<C, true, NS, D>(descs, chunks_per_stripe, n_stripes);
+}
+
 // ------------------------------------------------- batched reconstruct planner
 // One lane per stripe of rse_reconstruct_batch: the syndrome plan of
 // rse_codec.cpp bitslice_reconstruct on the device.  The valid/invalid
@@ -311,6 +330,7 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
 
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
 using BsDescFn = void (*)(const BsReconArgs*, uint64_t, uint64_t);
+using BsDesc4Fn = void (*)(const BsReconArgs*, uint64_t, uint64_t, uint64_t);
 
 using BsFn = void (*)(const CodeArgs, uint64_t);
 struct BsShape {
@@ -328,6 +348,9 @@ struct BsShape {
   BsRecFn rec[3][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
                       // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
+  BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
+  BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
+  BsDescFn rec_desc_deep[2][4];
 };
 
 template <class C, int NS, int MIX>
@@ -338,6 +361,21 @@ constexpr BsRecFn rec_fn() {
 template <class C, int NS>
 constexpr BsDescFn rec_desc_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_desc_kernel<C, true, NS>;
+  else return nullptr;
+}
+template <class C, int NS>
+constexpr BsDesc4Fn rec_desc4_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_desc_w4_kernel<C, NS>;
+  else return nullptr;
+}
+template <class C, int NS, int D>
+constexpr BsRecFn rec_deep_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_deep_kernel<C, NS, D>;
+  else return nullptr;
+}
+template <class C, int NS, int D>
+constexpr BsDescFn rec_desc_deep_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_desc_deep_kernel<C, NS, D>;
   else return nullptr;
 }
 #define BS(C, CP, FIELD)                                                          \
@@ -358,7 +396,16 @@ constexpr BsDescFn rec_desc_fn() {
    {{rec_fn<C, 1, 0>(), rec_fn<C, 2, 0>(), rec_fn<C, 4, 0>(), rec_fn<C, 8, 0>()},  \
     {rec_fn<C, 1, 1>(), rec_fn<C, 2, 1>(), rec_fn<C, 4, 1>(), rec_fn<C, 8, 1>()},  \
     {rec_fn<C, 1, 2>(), rec_fn<C, 2, 2>(), rec_fn<C, 4, 2>(), rec_fn<C, 8, 2>()}}, \
-   {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()}}
+   {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()},   \
+   {rec_desc4_fn<C, 1>(), rec_desc4_fn<C, 2>(), rec_desc4_fn<C, 4>(), rec_desc4_fn<C, 8>()}, \
+   {{rec_deep_fn<C, 1, 2>(), rec_deep_fn<C, 2, 2>(), rec_deep_fn<C, 4, 2>(),           \
+     rec_deep_fn<C, 8, 2>()},                                                          \
+    {rec_deep_fn<C, 1, 3>(), rec_deep_fn<C, 2, 3>(), rec_deep_fn<C, 4, 3>(),           \
+     rec_deep_fn<C, 8, 3>()}},                                                         \
+   {{rec_desc_deep_fn<C, 1, 2>(), rec_desc_deep_fn<C, 2, 2>(), rec_desc_deep_fn<C, 4, 2>(), \
+     rec_desc_deep_fn<C, 8, 2>()},                                                     \
+    {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
+     rec_desc_deep_fn<C, 8, 3>()}}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -478,9 +525,12 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
       if (sh.rec[0][q] && (1u << q) >= need) slot = q;
     if (slot < 0) return hipSuccess;
     const int mix = (int)get_option(17);
+    const int depth = mix == kReconMixHorner ? (int)get_option(27) : 1;  // RSE_OPT_RECON_DEPTH
     static const char* const kMixName[3] = {"mix-tables", "mix-chain", "mix-horner"};
-    note_kernel("bitslice-recon gf%d %u+%u ns%d %s", field, k, p, 1 << slot, kMixName[mix]);
-    hipLaunchKernelGGL(sh.rec[mix][slot], dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
+    note_kernel("bitslice-recon gf%d %u+%u ns%d %s d%d", field, k, p, 1 << slot, kMixName[mix],
+                depth > 3 ? 3 : depth);
+    BsRecFn fn = depth > 1 ? sh.rec_deep[depth > 2 ? 1 : 0][slot] : sh.rec[mix][slot];
+    hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     count_bitslice_launch();
@@ -510,21 +560,26 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                                        const uint8_t* d_present, uint32_t data_only,
                                        uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
                                        uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
-                                       bool* handled) {
-  *handled = false;
-  if (!get_option(5) || shard_bytes < kBsChunk || k == 0 || k > (uint32_t)kMaxIn ||
+                                       uint64_t* done) {
+  *done = 0;
+  if (!get_option(5) || shard_bytes < 4096 || k == 0 || k > (uint32_t)kMaxIn ||
       p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0)
     return hipSuccess;
   BsDescFn sfn = nullptr;
-  hipFunction_t jfn = nullptr;
+  BsDesc4Fn sfn4 = nullptr;
+  hipFunction_t jfn = nullptr, jfn4 = nullptr;
   bool compiled = false;
   for (const BsShape& sh : kBsShapes) {
     if (sh.field != field || sh.k != k || sh.p != p) continue;
     compiled = true;
     for (uint32_t i = 0; i < k * p; ++i)
       if (parity_rows[i] != sh.m[i]) return hipSuccess;
+    const int depth = (int)get_option(27);  // RSE_OPT_RECON_DEPTH
     for (int q = 0; q < 4 && !sfn; ++q)
-      if (sh.rec_desc[q] && (1u << q) >= need) sfn = sh.rec_desc[q];
+      if (sh.rec_desc[q] && (1u << q) >= need) {
+        sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
+        sfn4 = sh.rec_desc4[q];
+      }
     if (!sfn) return hipSuccess;
   }
   if (!compiled) {
@@ -532,7 +587,10 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
     hipError_t e = hipSuccess;
     if (!jit_find(field, k, p, parity_rows, k, 1, &jf, &e)) return e;
     for (int q = 0; q < jf.n_rec && !jfn; ++q)
-      if ((uint32_t)jf.rec_ns[q] >= need) jfn = jf.rec_desc[q];
+      if ((uint32_t)jf.rec_ns[q] >= need) {
+        jfn = jf.rec_desc[q];
+        jfn4 = jf.rec_desc4[q];
+      }
     if (!jfn) return hipSuccess;
   }
   hipLaunchKernelGGL(bs_recon_plan_kernel, dim3((n_stripes + kPlanBlock - 1) / kPlanBlock),
@@ -540,24 +598,45 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                      shard_bytes, n_stripes, d_descs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
-  const uint64_t total = cps * ns;
   const int64_t grid = get_option(2);
-  uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;
-  if (gx > total) gx = total;
-  if (gx > 0x7fffffffu) gx = 0x7fffffffu;
-  if (sfn) {
-    hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
-                       (const BsReconArgs*)d_descs, cps, ns);
-    e = hipGetLastError();
-  } else {
-    const BsReconArgs* dp = d_descs;
-    void* args[] = {&dp, &cps, &ns};
-    e = hipModuleLaunchKernel(jfn, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args, nullptr);
+  auto grid_for = [&](uint64_t steps) {
+    uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;
+    if (gx > steps) gx = steps;
+    return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
+  };
+  // whole 16 KiB chunks, then whole 4 KiB chunks of the rest (one per wave)
+  uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
+  uint64_t cps4 = (shard_bytes - cps * kBsChunk) / 4096u, base4 = cps * kBsChunk;
+  if (cps) {
+    const uint64_t gx = grid_for(cps * ns);
+    if (sfn) {
+      hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
+                         (const BsReconArgs*)d_descs, cps, ns);
+      e = hipGetLastError();
+    } else {
+      const BsReconArgs* dp = d_descs;
+      void* args[] = {&dp, &cps, &ns};
+      e = hipModuleLaunchKernel(jfn, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args, nullptr);
+    }
+    if (e != hipSuccess) return e;
+    *done = base4;
+    count_bitslice_launch();
   }
-  if (e != hipSuccess) return e;
-  count_bitslice_launch();
-  *handled = true;
+  if (cps4 && (sfn4 || jfn4)) {
+    const uint64_t gx = grid_for((cps4 * ns + 3) / 4);
+    if (sfn4) {
+      hipLaunchKernelGGL(sfn4, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
+                         (const BsReconArgs*)d_descs, cps4, ns, base4);
+      e = hipGetLastError();
+    } else {
+      const BsReconArgs* dp = d_descs;
+      void* args[] = {&dp, &cps4, &ns, &base4};
+      e = hipModuleLaunchKernel(jfn4, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args, nullptr);
+    }
+    if (e != hipSuccess) return e;
+    *done = base4 + cps4 * 4096u;
+    if (!cps) count_bitslice_launch();
+  }
   return hipSuccess;
 }
 

@@ -642,14 +642,14 @@ __device__ __forceinline__ uint64_t recon_mask(const BsReconArgs& a, uint32_t k)
 
 // NS: sigma rows computed (rows 0..NS-1; the host picks NS above every row it
 // needs), so a reconstruct pays for the rows it uses, not all p.
-template <class C, bool NT, int NS, int I>
+template <class C, bool NT, int NS, int I, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&cur)[4],
                                              const BsReconArgs& a, uint64_t mask, uint64_t off) {
   if constexpr (I < C::k + NS) {
     if ((mask >> I) & 1u) {
       const uint64_t rest = mask >> (I + 1);
       u32x4 nxt[4];
-      if (rest) load4<NT>(nxt, recon_ptr(a, C::k, I + 1 + __builtin_ctzll(rest)) + off);
+      if (rest) load4<NT, S>(nxt, recon_ptr(a, C::k, I + 1 + __builtin_ctzll(rest)) + off);
       __builtin_amdgcn_sched_barrier(0);  // as in code_inputs (SB)
       uint32_t pl[16];
       slice<typename C::Field>(cur, pl);
@@ -668,7 +668,7 @@ __device__ __forceinline__ void recon_inputs(uint32_t (&acc)[NS * 16], u32x4 (&c
         for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
       }
     }
-    recon_inputs<C, NT, NS, I + 1>(acc, cur, a, mask, off);
+    recon_inputs<C, NT, NS, I + 1, S>(acc, cur, a, mask, off);
   }
 }
 
@@ -1015,7 +1015,7 @@ __device__ __forceinline__ void h_group(uint32_t (&v)[16], const uint32_t (&s)[N
 
 // The mixing of recon_chunk by Horner's rule on the sliced rows acc (converted
 // in place to the basis for GF(2^16)); each output un-sliced once and stored.
-template <class C, bool NT, int NS>
+template <class C, bool NT, int NS, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t (&acc)[NS * 16],
                                                  uint64_t off) {
   using F = typename C::Field;
@@ -1065,15 +1065,18 @@ __device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t 
     unslice<F>(v, x);
     uint8_t* dst = a.out[o];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) stv<NT>(dst + off + j * (kBsBlock * 16), x[j]);
+    for (int j = 0; j < 4; ++j) stv<NT>(dst + off + j * S, x[j]);
   }
 }
 
 // One 16 KiB chunk of one stripe: off is the lane's byte offset from the
 // argument block's shard pointers.  MIX: the e x e mixing (kReconMix*).
-template <class C, bool NT, int NS, int MIX>
+// S: bytes between a lane's 4 vectors (4 KiB: a 256-lane workgroup per 16 KiB
+// chunk; 1 KiB: each wave its own 4 KiB chunk -- Horner mixing only).
+template <class C, bool NT, int NS, int MIX, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* tq,
                                             const uint32_t* tt2, uint64_t off) {
+  static_assert(S == kBsBlock * 16 || MIX == kReconMixHorner, "4 KiB chunks: Horner mixing");
   using F = typename C::Field;
   const uint32_t n_out = a.n_out;
   const uint64_t mask = recon_mask(a, C::k);
@@ -1082,10 +1085,10 @@ __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* t
 #pragma unroll
   for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
   u32x4 cur[4];
-  load4<NT>(cur, recon_ptr(a, C::k, first) + off);
-  recon_inputs<C, NT, NS, 0>(acc, cur, a, mask, off);
+  load4<NT, S>(cur, recon_ptr(a, C::k, first) + off);
+  recon_inputs<C, NT, NS, 0, S>(acc, cur, a, mask, off);
   if constexpr (MIX == kReconMixHorner) {
-    recon_mix_horner<C, NT, NS>(a, acc, off);
+    recon_mix_horner<C, NT, NS, S>(a, acc, off);
     return;
   } else if constexpr (!recon_mix_tables(NS, MIX)) {  // the mixing on the sliced syndromes
     // outputs per pass: NS rows + G outputs + the y pair within the VGPR
@@ -1168,6 +1171,16 @@ __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
   }
 }
 
+// bitslice_recon_desc_body over whole 4 KiB chunks, one per wave (lane l
+// codes vectors l, l + 64, l + 128, l + 192 of its wave's chunk), for shards
+// -- or the rest of shards past their 16 KiB chunks, from byte `base` on --
+// shorter than 16 KiB: reconstruct_batch of small shards at bit-sliced speed.
+// chunks_per_stripe counts 4 KiB chunks.  Horner mixing.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_desc_body_w4(const BsReconArgs* __restrict__ descs,
+                                                            uint64_t chunks_per_stripe,
+                                                            uint64_t n_stripes, uint64_t base);
+
 // A stripe's descriptor through the constant address space: the planner wrote
 // it before this kernel, nothing writes it during, so its fields can be scalar
 // loads (through a generic pointer they were vector loads + readfirstlane).
@@ -1209,6 +1222,147 @@ __device__ __forceinline__ void bitslice_recon_desc_body(const BsReconArgs* __re
       built = stripe;
     }
     recon_chunk<C, NT, NS, MIX>(a, tq, tt2, chunk * kBsChunk + threadIdx.x * 16u);
+  }
+}
+
+// ---- deeper input pipeline (RSE_OPT_RECON_DEPTH) ----------------------------
+// recon_inputs with D inputs in flight per lane: at input index I the loads of
+// index I + D are issued (if that input is read), into a ring of D + 1 slots
+// indexed at compile time by the input INDEX, so the ring stays in VGPRs
+// whatever the erasure pattern (an absent index just leaves its slot unused,
+// so the depth in inputs actually read is at most D).  Past the chunk's last
+// index the loads continue into the first X indices of the workgroup's next
+// chunk (next_off, ~0 if none), so the e x e mixing overlaps them.  Why: one
+// 16 KiB input in flight per 256-lane workgroup, two workgroups per CU at
+// NS = 8, is ~8 MiB over the chip -- at ~2 us of loaded HBM latency a read
+// cap near 4 TB/s (Little's law), while the mixing phase has no loads in
+// flight at all.
+template <class C, bool NT, int NS, int D, int X, int I>
+__device__ __forceinline__ void recon_inputs_deep(uint32_t (&acc)[NS * 16], u32x4 (&buf)[D + 1][4],
+                                                  const BsReconArgs& a, uint64_t mask,
+                                                  uint64_t off, uint64_t next_off) {
+  constexpr int N = C::k + NS;
+  if constexpr (I < N) {
+    constexpr int J = I + D;
+    if constexpr (J < N) {
+      if ((mask >> J) & 1u) load4<NT>(buf[J % (D + 1)], recon_ptr(a, C::k, J) + off);
+    } else if constexpr (J - N < X) {
+      if (next_off != ~0ull && ((mask >> (J - N)) & 1u))
+        load4<NT>(buf[J % (D + 1)], recon_ptr(a, C::k, J - N) + next_off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if ((mask >> I) & 1u) {
+      uint32_t pl[16];
+      slice<typename C::Field>(buf[I % (D + 1)], pl);
+      if constexpr (I < C::k) {
+        mac_input<C, I, false>(acc, pl, make_int_seq<NS * 16>{});
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[(I - C::k) * 16 + q] ^= pl[q];
+      }
+#pragma unroll
+      for (int q = 0; q < NS * 16; ++q) asm volatile("" : "+v"(acc[q]));
+    }
+    recon_inputs_deep<C, NT, NS, D, X, I + 1>(acc, buf, a, mask, off, next_off);
+  }
+}
+
+// Loads of the first min(D, X') input indices of a chunk (X' = D for the
+// first chunk of a workgroup, when nothing was prefetched).
+template <class C, bool NT, int NS, int D>
+__device__ __forceinline__ void recon_prime(u32x4 (&buf)[D + 1][4], const BsReconArgs& a,
+                                            uint64_t mask, uint64_t off, int from) {
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j >= from && j < C::k + NS && ((mask >> j) & 1u))
+      load4<NT>(buf[j], recon_ptr(a, C::k, j) + off);
+}
+
+// recon_chunk with the deeper pipeline: buf holds the loads of this chunk's
+// first indices on entry and, when next_off != ~0, of the next chunk's first X
+// indices on return (moved to slots 0..X-1).
+template <class C, bool NT, int NS, int MIX, int D, int X>
+__device__ __forceinline__ void recon_chunk_deep(const BsReconArgs& a, const uint4* tq,
+                                                 const uint32_t* tt2, uint64_t off,
+                                                 uint64_t next_off, u32x4 (&buf)[D + 1][4]) {
+  static_assert(MIX == kReconMixHorner, "the deeper pipeline is for Horner mixing");
+  constexpr int N = C::k + NS;
+  const uint64_t mask = recon_mask(a, C::k);
+  uint32_t acc[NS * 16];
+#pragma unroll
+  for (int q = 0; q < NS * 16; ++q) acc[q] = 0u;
+  recon_inputs_deep<C, NT, NS, D, X, 0>(acc, buf, a, mask, off, next_off);
+  if constexpr (N % (D + 1) != 0) {
+    if (next_off != ~0ull) {
+      u32x4 t[X][4];
+#pragma unroll
+      for (int j = 0; j < X; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[j][q] = buf[(N + j) % (D + 1)][q];
+#pragma unroll
+      for (int j = 0; j < X; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) buf[j][q] = t[j][q];
+    }
+  }
+  recon_mix_horner<C, NT, NS>(a, acc, off);
+}
+
+// bitslice_recon_body with the deeper pipeline (one argument block for every
+// stripe: the next chunk has the same pattern, so the cross-chunk loads apply).
+template <class C, bool NT, int NS, int D>
+__device__ __forceinline__ void bitslice_recon_body_deep(const BsReconArgs& a,
+                                                         uint64_t chunks_per_stripe) {
+  constexpr int X = 1;  // the mixing's registers leave room for one input (NS = 8: 240 VGPRs)
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint64_t mask = recon_mask(a, C::k);
+  auto chunk_off = [&](uint64_t idx) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    return stripe * a.stripe_stride + chunk * kBsChunk + threadIdx.x * 16u;
+  };
+  u32x4 buf[D + 1][4];
+  if (blockIdx.x < total) recon_prime<C, NT, NS, D>(buf, a, mask, chunk_off(blockIdx.x), 0);
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t nidx = idx + gridDim.x;
+    const uint64_t next_off = nidx < total ? chunk_off(nidx) : ~0ull;
+    recon_chunk_deep<C, NT, NS, kReconMixHorner, D, X>(a, nullptr, nullptr, chunk_off(idx),
+                                                       next_off, buf);
+    if (next_off != ~0ull) recon_prime<C, NT, NS, D>(buf, a, mask, next_off, X);
+  }
+}
+
+// bitslice_recon_desc_body with the deeper pipeline inside each chunk (the
+// next chunk is usually another stripe's, with its own descriptor: no
+// cross-chunk loads).
+template <class C, bool NT, int NS, int D>
+__device__ __forceinline__ void bitslice_recon_desc_body_deep(const BsReconArgs* __restrict__ descs,
+                                                              uint64_t chunks_per_stripe,
+                                                              uint64_t n_stripes) {
+  const uint64_t total = chunks_per_stripe * n_stripes;
+  for (uint64_t idx = blockIdx.x; idx < total; idx += gridDim.x) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const BsReconArgs& a = desc_at(descs, stripe);
+    if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
+    const uint64_t off = chunk * kBsChunk + threadIdx.x * 16u;
+    u32x4 buf[D + 1][4];
+    recon_prime<C, NT, NS, D>(buf, a, recon_mask(a, C::k), off, 0);
+    recon_chunk_deep<C, NT, NS, kReconMixHorner, D, 1>(a, nullptr, nullptr, off, ~0ull, buf);
+  }
+}
+
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_desc_body_w4(const BsReconArgs* __restrict__ descs,
+                                                            uint64_t chunks_per_stripe,
+                                                            uint64_t n_stripes, uint64_t base) {
+  const uint64_t total = chunks_per_stripe * n_stripes;
+  const uint32_t sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const uint32_t lane_off = (threadIdx.x & 63u) * 16u;
+  for (uint64_t idx = (uint64_t)blockIdx.x * 4 + sub; idx < total; idx += (uint64_t)gridDim.x * 4) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    const BsReconArgs& a = desc_at(descs, stripe);
+    if (a.n_out == 0) continue;  // uniform: nothing to rebuild in this stripe
+    recon_chunk<C, NT, NS, kReconMixHorner, 1024u>(a, nullptr, nullptr,
+                                                   base + chunk * 4096u + lane_off);
   }
 }
 

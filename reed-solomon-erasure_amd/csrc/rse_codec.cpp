@@ -1607,7 +1607,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   size_t done = 0;  // bytes of every shard coded so far
   // 1. whole 16 KiB chunks on the bit-sliced syndrome kernels (compiled or
   //    run-time specialised codecs), planned per stripe on the device
-  if (fits && sb >= rse::bitslice_chunk_bytes() && sb % 16u == 0 && aligned16(base) &&
+  if (fits && sb >= 4096 && sb % 16u == 0 && aligned16(base) &&
       rse::get_option(RSE_OPT_BITSLICE)) {
     want_bitslice(c, sb, false, n_stripes);
     uint32_t need = 0;  // sigma rows any stripe uses: its R and missing parity rows
@@ -1630,17 +1630,17 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       hipError_t e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
       if (e == hipSuccess)
         e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
-      bool handled = false;
+      uint64_t bs_done = 0;
       if (e == hipSuccess)
         e = rse::launch_bitslice_recon_batch(
             c->field, (uint32_t)k, (uint32_t)p, rows.c.data(), reinterpret_cast<uint16_t*>(ws),
             ws + pres_off, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
-            reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &handled);
+            reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
       hipError_t f = hipFreeAsync(ws, st);
       if (e == hipSuccess) e = f;
       if (e == hipSuccess) e = hipStreamSynchronize(st);  // `rows` dies here
       if (e != hipSuccess) return dev_fail(e);
-      if (handled) done = (sb / rse::bitslice_chunk_bytes()) * rse::bitslice_chunk_bytes();
+      done = bs_done;
     } else {
       return RSE_OK;  // nothing missing that this call rebuilds, in any stripe
     }

@@ -277,17 +277,38 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   }
   int ns[5];
   const int n = recon_ns(p, ns);
+  const int depth = (int)std::min<int64_t>(3, get_option(27));  // RSE_OPT_RECON_DEPTH
   for (int q = 0; q < n; ++q) {
-    std::snprintf(buf, sizeof buf,
-                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
-                  "    const rse::BsReconArgs a, uint64_t cps) {\n"
-                  "  rse::bitslice_recon_body<rse::JitCode, true, %d, rse::kReconMixDefault>(a, cps);\n}\n",
-                  ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
+    if (depth > 1)
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
+                    "    const rse::BsReconArgs a, uint64_t cps) {\n"
+                    "  rse::bitslice_recon_body_deep<rse::JitCode, true, %d, %d>(a, cps);\n}\n",
+                    ns[q] > 4 ? 2 : 3, ns[q], ns[q], depth);
+    else
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
+                    "    const rse::BsReconArgs a, uint64_t cps) {\n"
+                    "  rse::bitslice_recon_body<rse::JitCode, true, %d, rse::kReconMixDefault>(a, cps);\n}\n",
+                    ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
+    s += buf;
+    if (depth > 1)
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
+                    "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+                    "  rse::bitslice_recon_desc_body_deep<rse::JitCode, true, %d, %d>(d, cps, n);\n}\n",
+                    ns[q] > 4 ? 2 : 3, ns[q], ns[q], depth);
+    else
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
+                    "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+                    "  rse::bitslice_recon_desc_body<rse::JitCode, true, %d>(d, cps, n);\n}\n",
+                    ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
     s += buf;
     std::snprintf(buf, sizeof buf,
-                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
-                  "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
-                  "  rse::bitslice_recon_desc_body<rse::JitCode, true, %d>(d, cps, n);\n}\n",
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc4_%d(\n"
+                  "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n, uint64_t base) {\n"
+                  "  rse::bitslice_recon_desc_body_w4<rse::JitCode, true, %d>(d, cps, n, base);\n}\n",
                   ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
     s += buf;
   }
@@ -860,6 +881,9 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
         if (he != hipSuccess) break;
         std::snprintf(name, sizeof name, "rse_jit_recon_desc%d", f.rec_ns[q]);
         he = hipModuleGetFunction(&f.rec_desc[q], m, name);
+        if (he != hipSuccess) break;
+        std::snprintf(name, sizeof name, "rse_jit_recon_desc4_%d", f.rec_ns[q]);
+        he = hipModuleGetFunction(&f.rec_desc4[q], m, name);
       }
     }
     if (he != hipSuccess) {

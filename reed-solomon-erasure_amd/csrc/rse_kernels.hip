@@ -831,18 +831,31 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* dst, uin
 constexpr int kExLen = 520;
 constexpr uint32_t kTabBytes = 784;  // lg[256] + ex[kExLen], rounded to 16
 
-__device__ __forceinline__ void build_log_exp(uint8_t* lg, uint8_t* ex) {
-  if (threadIdx.x == 0) {
-    uint32_t b = 1;
-    for (int l = 0; l < kExLen; ++l) {
-      if (l < 255) lg[b] = (uint8_t)l;
-      ex[l] = (uint8_t)b;
-      b <<= 1;
-      if (b & 0x100u) b ^= 0x11Du;
-      if (l % 255 == 254) b = 1;  // 2^255 = 1
-    }
-    lg[0] = 0;
+// Every thread computes its entries on its own (2^l by square-and-multiply,
+// 14 carry-less steps) instead of one thread walking 520 doublings: the
+// planner runs one workgroup per stripe, so this is per stripe.  The caller
+// synchronises before use.
+__device__ __forceinline__ uint32_t gf8_mul_slow(uint32_t a, uint32_t b) {  // modulo 0x11D
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r ^= ((b >> i) & 1u) ? a : 0u;
+    a = (a << 1) ^ ((a & 0x80u) ? 0x11Du : 0u);
   }
+  return r;
+}
+__device__ __forceinline__ void build_log_exp(uint8_t* lg, uint8_t* ex) {
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kExLen; l += blockDim.x) {
+    uint32_t e = l % 255u, r = 1u, b = 2u;
+    while (e) {  // r = 2^e
+      if (e & 1u) r = gf8_mul_slow(r, b);
+      b = gf8_mul_slow(b, b);
+      e >>= 1;
+    }
+    ex[l] = (uint8_t)r;
+    if (l < 255u) lg[r] = (uint8_t)l;
+  }
+  if (threadIdx.x == 0) lg[0] = 0;
 }
 
 struct PlanF8 {

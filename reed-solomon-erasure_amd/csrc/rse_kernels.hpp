@@ -231,16 +231,17 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
 
 // rse_reconstruct_batch on the bit-sliced kernels: a device planner writes one
 // BsReconArgs per stripe (its own erasure pattern: partition, e x e syndrome
-// inverse, mixing rows), then the syndrome kernel codes the whole 16 KiB
-// chunks of every stripe from them.  d_rows: the p x k parity rows on the
-// device (parity_rows: the same on the host, to select the kernels); need:
-// sigma rows any stripe uses (max row + 1).  *handled unset = nothing queued.
+// inverse, mixing rows), then the syndrome kernels code the whole 16 KiB
+// chunks of every stripe from them, and the whole 4 KiB chunks of the rest
+// (one per wave).  d_rows: the p x k parity rows on the device (parity_rows:
+// the same on the host, to select the kernels); need: sigma rows any stripe
+// uses (max row + 1).  *done = bytes of every shard coded (0: nothing queued).
 hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                                        const uint16_t* parity_rows, const uint16_t* d_rows,
                                        const uint8_t* d_present, uint32_t data_only,
                                        uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
                                        uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
-                                       bool* handled);
+                                       uint64_t* done);
 
 // ---- run-time specialisation (rse_jit.cpp) ----------------------------------
 // Bit-sliced kernels for codecs not compiled into the library: the XOR networks
@@ -305,6 +306,7 @@ struct JitFns {
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
   hipFunction_t rec_desc[5] = {};  // ... over per-stripe BsReconArgs (descs, cps, n_stripes)
+  hipFunction_t rec_desc4[5] = {}; // ... over 4 KiB chunks, one per wave (descs, cps4, n, base)
   hipFunction_t wide = nullptr;    // kJitWide: rse_jit_wide (WideArgs)
 };
 // Kernels of `stage` (0: encode/verify, 1: reconstruct) for a launch whose

@@ -58,6 +58,9 @@ def main():
                          "(rotations of --erase) instead of random ones (0)")
     ap.add_argument("--hog-gib", type=int, default=0,
                     help="allocate this much device memory first (the bench holds 112 GiB)")
+    ap.add_argument("--recon-depth", default="1",
+                    help="comma list of RSE_OPT_RECON_DEPTH values (syndrome reconstruct: inputs "
+                         "in flight per lane; compiled codecs)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="rse_set_option(KEY, VALUE) before the codec is created (repeatable)")
     args = ap.parse_args()
@@ -134,15 +137,17 @@ def main():
     mixes = [int(x) for x in args.recon_mix.split(",")]
     vlist = ([int(x) for x in args.variant_list.split(",")] if args.variant_list
              else list(range(args.variants)))
-    configs = [(nt, gx, gy, var, bs, pat, mx) for mx in mixes for pat in pats for bs in bss
-               for var in vlist for nt in nts for gx, gy in shapes]
+    depths = [int(x) for x in args.recon_depth.split(",")]
+    configs = [(nt, gx, gy, var, bs, pat, mx, dp) for dp in depths for mx in mixes for pat in pats
+               for bs in bss for var in vlist for nt in nts for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for c in configs:
-            nt, gx, gy, var, bs, pat, mx = c
+            nt, gx, gy, var, bs, pat, mx, dp = c
+            lib.rse_set_option(27, dp)
             lib.rse_set_option(17, mx)
             lib.rse_set_option(11, pat)
             lib.rse_set_option(5, bs)
@@ -161,9 +166,9 @@ def main():
     what = f" erased {erased}" if args.op == "reconstruct" else ""
     size = f"{args.shard_kib} KiB" if args.shard_kib else f"{args.shard_mib} MiB"
     print(f"{args.op} GF(2^{args.field}) {k}+{p} x {size}, {S} stripes{what}; GB/s (1e9)")
-    for med, lo, hi, (nt, gx, gy, var, bs, pat, mx) in rows:
-        print(f"  bitslice={bs} patterns={pat} mix={mx} variant={var} nt={nt} grid_x={gx:<5} "
-              f"stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
+    for med, lo, hi, (nt, gx, gy, var, bs, pat, mx, dp) in rows:
+        print(f"  bitslice={bs} patterns={pat} mix={mx} depth={dp} variant={var} nt={nt} "
+              f"grid_x={gx:<5} stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
     from reed_solomon_erasure.core import last_kernel
     print(f"last kernel: {last_kernel()}")
