@@ -306,6 +306,21 @@ def load_traffic(workload, kernel_id):
     return best
 
 
+def library_info():
+    """What ran: librse_hip.so's SHA-256 and the source commit its Makefile
+    stamped (BUILD_INFO.json next to it; the GPU box has no .git)."""
+    d = os.path.join(ROOT, "reed-solomon-erasure_amd", "reed_solomon_erasure")
+    out = {"sha256": hashlib.sha256(open(os.path.join(d, "librse_hip.so"), "rb").read()).hexdigest()}
+    try:
+        info = json.load(open(os.path.join(d, "BUILD_INFO.json")))
+        out.update(source_commit=info.get("source_commit"),
+                   uncommitted_source_files=info.get("uncommitted_source_files"),
+                   build_info_matches=info.get("library_sha256") == out["sha256"])
+    except (OSError, ValueError):
+        out["source_commit"] = None
+    return out
+
+
 # ----------------------------------------------------------------- main
 def golden_stripes():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
@@ -497,6 +512,7 @@ def main(argv=None):
             "collective": coll,
             "roofline": roof, "cpu_baseline": cpu.get("cpu_baseline"),
         }
+        line["library"] = library_info()
         for key in ("cpu_baseline_legs", "cpu_host"):
             if key in cpu:
                 line[key] = cpu[key]

@@ -8,8 +8,8 @@ MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide
 coalesced stream, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 Writes profiles/<tag>_pmc_traffic.json, which bench.py reports as
 roofline.traffic when the kernel that ran (rse_last_kernel, "kernel_id") is the
-one profiled here.  RSE_COMMIT (set by the caller: the GPU box has no .git)
-and the library's SHA-256 record what was measured.
+one profiled here.  The library's BUILD_INFO.json (its source commit, stamped
+by the Makefile when it was built) and its SHA-256 record what was measured.
 
     python tools/pmc_traffic.py --tag r01 [bench args...]
 """
@@ -40,6 +40,15 @@ def run(counter, outdir, bench_args):
     return json.loads(line), rows
 
 
+def build_info(lib_path):
+    """BUILD_INFO.json next to the library (written by its Makefile where the
+    tree has .git): the commit of the library's sources, stamped at build time."""
+    try:
+        return json.load(open(os.path.join(os.path.dirname(lib_path), "BUILD_INFO.json")))
+    except (OSError, ValueError):
+        return {}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
@@ -58,8 +67,11 @@ def main():
         "workload": bench["config"]["workload"],
         "kernel_family": bench["roofline"].get("kernel", "table"),
         "kernel_id": bench["roofline"].get("kernel_id"),
-        "commit": os.environ.get("RSE_COMMIT"),
+        "commit": build_info(lib_path).get("source_commit"),
+        "uncommitted_source_files": build_info(lib_path).get("uncommitted_source_files"),
         "library_sha256": hashlib.sha256(open(lib_path, "rb").read()).hexdigest(),
+        "build_info_matches_library": build_info(lib_path).get("library_sha256") ==
+        hashlib.sha256(open(lib_path, "rb").read()).hexdigest(),
         "kernel": [r["Kernel_Name"] for r in fetch][0],
         "dispatches": len(f),
         "fetch_size_kb_raw_mean": sum(f) / len(f),
