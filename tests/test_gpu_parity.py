@@ -437,7 +437,7 @@ def test_flat_small_shards_many_stripes(R, field, k, p, n, stripes):
 
 @pytest.mark.parametrize("field,k,p,n,stripes,bs,hp", [
     (8, 10, 4, 4096 + 16, 33, 1, 0),     # 4 KiB chunks bit-sliced (one per wave) + device planner
-    (16, 20, 8, 2048 + 4, 40, 1, 0),     # GF(2^16) 4 KiB shards + 8 bytes: the same
+    (16, 20, 8, 2048 + 8, 40, 1, 0),     # GF(2^16) 4 KiB shards + 16 bytes: the same
     (8, 12, 4, 3 * 4096, 7, 1, 0),       # run-time specialised codec, 4 KiB chunks only
     (8, 10, 4, 4096 + 1000, 9, 0, 0),    # unaligned stride: device planner only
     (8, 10, 4, 1037, 9, 0, 0),           # device planner, byte path
