@@ -334,7 +334,7 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        1/W of the inputs and shares the planes through LDS; 0 every
                                        wave slices every input */
 #define RSE_OPT_WIDE_DEPTH 26        /* wide-codec modules built after: 4 KiB inputs each wave keeps in
-                                       flight (1..4, default 2; past a chunk's last round, the next
+                                       flight (1..4, default 1; past a chunk's last round, the next
                                        chunk's first ones) */
 #define RSE_OPT_RECON_DEPTH 27       /* syndrome reconstruct: inputs in flight per lane (1..4) */
 #define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch

@@ -785,7 +785,7 @@ struct Options {
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
   int64_t host_copy_2d = 1;       // host pipeline: 2D copies for runs of a flat buffer's shards
   int64_t jit_exact = 1;          // run-time networks: exact-decomposition temporaries
-  int64_t wide_depth = 2;         // wide modules: inputs in flight per wave (1..4)
+  int64_t wide_depth = 1;         // wide modules: inputs in flight per wave (1..4)
   int64_t recon_depth = 1;        // syndrome reconstruct: inputs in flight per lane (1..4)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
