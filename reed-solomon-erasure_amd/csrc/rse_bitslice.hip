@@ -345,7 +345,7 @@ struct BsShape {
   BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
   BsFn chk;           // the default variant for the check modes (verify): the
                       // stored parity loaded before un-slicing (store_outputs CE)
-  BsRecFn rec[3][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
+  BsRecFn rec[4][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
                       // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
@@ -395,7 +395,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
    bitslice_kernel<C, true, C::NP == 8, false, false, false, false, true>,         \
    {{rec_fn<C, 1, 0>(), rec_fn<C, 2, 0>(), rec_fn<C, 4, 0>(), rec_fn<C, 8, 0>()},  \
     {rec_fn<C, 1, 1>(), rec_fn<C, 2, 1>(), rec_fn<C, 4, 1>(), rec_fn<C, 8, 1>()},  \
-    {rec_fn<C, 1, 2>(), rec_fn<C, 2, 2>(), rec_fn<C, 4, 2>(), rec_fn<C, 8, 2>()}}, \
+    {rec_fn<C, 1, 2>(), rec_fn<C, 2, 2>(), rec_fn<C, 4, 2>(), rec_fn<C, 8, 2>()},  \
+    {rec_fn<C, 1, 3>(), rec_fn<C, 2, 3>(), rec_fn<C, 4, 3>(), rec_fn<C, 8, 3>()}}, \
    {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()},   \
    {rec_desc4_fn<C, 1>(), rec_desc4_fn<C, 2>(), rec_desc4_fn<C, 4>(), rec_desc4_fn<C, 8>()}, \
    {{rec_deep_fn<C, 1, 2>(), rec_deep_fn<C, 2, 2>(), rec_deep_fn<C, 4, 2>(),           \
@@ -526,7 +527,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     if (slot < 0) return hipSuccess;
     const int mix = (int)get_option(17);
     const int depth = mix == kReconMixHorner ? (int)get_option(27) : 1;  // RSE_OPT_RECON_DEPTH
-    static const char* const kMixName[3] = {"mix-tables", "mix-chain", "mix-horner"};
+    static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
     note_kernel("bitslice-recon gf%d %u+%u ns%d %s d%d", field, k, p, 1 << slot, kMixName[mix],
                 depth > 3 ? 3 : depth);
     BsRecFn fn = depth > 1 ? sh.rec_deep[depth > 2 ? 1 : 0][slot] : sh.rec[mix][slot];

@@ -893,7 +893,10 @@ __device__ __forceinline__ void recon_mix_bitsliced(const BsReconArgs& a,
 //  kReconMixChain   bit-sliced doubling chains above 4 syndrome rows, tables
 //                   below (round 2: +11 % at 8 rows);
 //  kReconMixHorner  bit-sliced Horner's rule (below), any number of rows.
-constexpr int kReconMixTables = 0, kReconMixChain = 1, kReconMixHorner = 2;
+//  kReconMixHorner4 the same, four steps per mask word unrolled (the step
+//                   bytes by constant shifts, no 64-bit mask shifting or
+//                   per-step loop control; A/B).
+constexpr int kReconMixTables = 0, kReconMixChain = 1, kReconMixHorner = 2, kReconMixHorner4 = 3;
 constexpr int kReconMixDefault = kReconMixHorner;
 constexpr bool recon_mix_tables(int ns, int mix) {
   return mix == kReconMixTables || (mix == kReconMixChain && ns <= 4);
@@ -1015,7 +1018,7 @@ __device__ __forceinline__ void h_group(uint32_t (&v)[16], const uint32_t (&s)[N
 
 // The mixing of recon_chunk by Horner's rule on the sliced rows acc (converted
 // in place to the basis for GF(2^16)); each output un-sliced once and stored.
-template <class C, bool NT, int NS, uint32_t S = kBsBlock * 16>
+template <class C, bool NT, int NS, uint32_t S = kBsBlock * 16, bool U4 = false>
 __device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t (&acc)[NS * 16],
                                                  uint64_t off) {
   using F = typename C::Field;
@@ -1045,13 +1048,26 @@ __device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t 
     // (the fused shift writes a second register set; the case joins cost
     // 8 v_mov_b64 per step to move it back -- a tied in-place asm form and a
     // one-step lag of rows 4..7 were probed and the copies stayed)
+    if constexpr (U4) {
 #pragma unroll 1
-    for (int j = 0; j < NB; ++j) {
-      const uint32_t m = (uint32_t)lo & 0xFFu;
-      lo = (lo >> 8) | (hi << 56);
-      hi >>= 8;
-      h_group<F, true, 0, NS, ND>(v, acc, d, m & 15u);
-      if constexpr (NS > 4) h_group<F, false, 1, NS, ND>(v, acc, d, m >> 4);
+      for (int w = 0; w < NB / 4; ++w) {
+        const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane(a.hm[o][w]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t m = (word >> (8 * b)) & 0xFFu;
+          h_group<F, true, 0, NS, ND>(v, acc, d, m & 15u);
+          if constexpr (NS > 4) h_group<F, false, 1, NS, ND>(v, acc, d, m >> 4);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int j = 0; j < NB; ++j) {
+        const uint32_t m = (uint32_t)lo & 0xFFu;
+        lo = (lo >> 8) | (hi << 56);
+        hi >>= 8;
+        h_group<F, true, 0, NS, ND>(v, acc, d, m & 15u);
+        if constexpr (NS > 4) h_group<F, false, 1, NS, ND>(v, acc, d, m >> 4);
+      }
     }
     const int32_t os = __builtin_amdgcn_readfirstlane(a.out_sigma[o]);
 #pragma unroll
@@ -1076,7 +1092,7 @@ __device__ __forceinline__ void recon_mix_horner(const BsReconArgs& a, uint32_t 
 template <class C, bool NT, int NS, int MIX, uint32_t S = kBsBlock * 16>
 __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* tq,
                                             const uint32_t* tt2, uint64_t off) {
-  static_assert(S == kBsBlock * 16 || MIX == kReconMixHorner, "4 KiB chunks: Horner mixing");
+  static_assert(S == kBsBlock * 16 || MIX >= kReconMixHorner, "4 KiB chunks: Horner mixing");
   using F = typename C::Field;
   const uint32_t n_out = a.n_out;
   const uint64_t mask = recon_mask(a, C::k);
@@ -1087,8 +1103,8 @@ __device__ __forceinline__ void recon_chunk(const BsReconArgs& a, const uint4* t
   u32x4 cur[4];
   load4<NT, S>(cur, recon_ptr(a, C::k, first) + off);
   recon_inputs<C, NT, NS, 0, S>(acc, cur, a, mask, off);
-  if constexpr (MIX == kReconMixHorner) {
-    recon_mix_horner<C, NT, NS, S>(a, acc, off);
+  if constexpr (MIX == kReconMixHorner || MIX == kReconMixHorner4) {
+    recon_mix_horner<C, NT, NS, S, MIX == kReconMixHorner4>(a, acc, off);
     return;
   } else if constexpr (!recon_mix_tables(NS, MIX)) {  // the mixing on the sliced syndromes
     // outputs per pass: NS rows + G outputs + the y pair within the VGPR

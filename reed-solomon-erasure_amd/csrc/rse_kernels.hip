@@ -1216,7 +1216,7 @@ int set_option(int key, int64_t value) {
     case 13: g_opt.jit_cse = value < 0 ? 0 : value > 32 ? 32 : value; return 0;
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
-    case 17: g_opt.recon_mix = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
+    case 17: g_opt.recon_mix = value < 0 ? 0 : value > 3 ? 3 : value; return 0;
     case 18: g_opt.wide_split = value < 2 ? 2 : value > 8 ? 8 : value; return 0;
     case 19: g_opt.wide_balance = value ? 1 : 0; return 0;
     case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;
