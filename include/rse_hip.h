@@ -315,9 +315,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        another process loads them instead of compiling */
 #define RSE_OPT_JIT_CACHE_HITS 16   /* read-only: modules this process loaded from the disk cache */
 #define RSE_OPT_RECON_MIX 17        /* syndrome reconstruct of the compiled-in codecs, the e x e
-                                       mixing: 2 (default) bit-sliced Horner's rule, 1 bit-sliced
-                                       doubling chains above 4 rows, 0 v_perm tables, 3 Horner with
-                                       four steps per mask word unrolled (A/B) */
+                                       mixing: 3 (default) bit-sliced Horner's rule, four steps per
+                                       mask word unrolled; 2 the same one step at a time, 1 bit-sliced
+                                       doubling chains above 4 rows, 0 v_perm tables (A/B) */
 #define RSE_OPT_WIDE_SPLIT 18       /* outputs per wave of the one-module kernels (2..8, default 8):
                                        a codec with more parity rows than this (but <= 8 x this)
                                        is coded by W waves sharing each input chunk */

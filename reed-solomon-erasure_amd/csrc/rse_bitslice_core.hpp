@@ -897,7 +897,7 @@ __device__ __forceinline__ void recon_mix_bitsliced(const BsReconArgs& a,
 //                   bytes by constant shifts, no 64-bit mask shifting or
 //                   per-step loop control; A/B).
 constexpr int kReconMixTables = 0, kReconMixChain = 1, kReconMixHorner = 2, kReconMixHorner4 = 3;
-constexpr int kReconMixDefault = kReconMixHorner;
+constexpr int kReconMixDefault = kReconMixHorner4;
 constexpr bool recon_mix_tables(int ns, int mix) {
   return mix == kReconMixTables || (mix == kReconMixChain && ns <= 4);
 }

@@ -779,7 +779,7 @@ struct Options {
   int64_t jit_cse = 32;           // GF(2^16) specialised networks: temporaries per input
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
-  int64_t recon_mix = 2;          // syndrome reconstruct mixing: 2 Horner, 1 doubling chains, 0 tables
+  int64_t recon_mix = 3;          // syndrome reconstruct mixing: 3/2 Horner (4 steps per word / 1), 1 doubling chains, 0 tables
   int64_t wide_split = 8;         // outputs per wave of wide modules
   int64_t wide_balance = 1;       // wide modules: waves per workgroup rounded to 2, 4, 8
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)

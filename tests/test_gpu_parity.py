@@ -722,11 +722,11 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
                 list(range(p - 2)) + [k, k + p - 1], [1, k + 1]]
     patterns += [sorted(rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False).tolist())
                  for _ in range(6)]
-    names = {0: "mix-tables", 1: "mix-chain", 2: "mix-horner"}
+    names = {0: "mix-tables", 1: "mix-chain", 2: "mix-horner ", 3: "mix-horner4"}
     jp = lib.rse_get_option(11)
     lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
     try:
-        for mix in (2, 1, 0):
+        for mix in (3, 2, 1, 0):
             assert lib.rse_set_option(17, mix) == 0
             for erased in patterns:
                 present = [i not in erased for i in range(k + p)]
@@ -740,7 +740,7 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
                 for i in erased:
                     assert (host(tb[i]).reshape(-1) == full[i]).all(), (mix, erased, i)
     finally:
-        lib.rse_set_option(17, 2)
+        lib.rse_set_option(17, 3)
         lib.rse_set_option(11, jp)
 
 

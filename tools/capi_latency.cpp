@@ -49,6 +49,38 @@ int main() {
     std::printf("%s (C ABI, one stripe per call): %.1f us per call, %.1f GB/s\n",
                 leg ? "encode (asynchronous)" : "verify (synchronous)", dt * 1e6, bytes / dt / 1e9);
   }
+  {  // the floor of any synchronous call: one tiny launch + stream synchronisation
+    const int reps = 256;
+    for (int w = 0; w < 16; ++w) {
+      (void)rse_fill_splitmix(buf, 64, 1, 0, nullptr);
+      (void)hipStreamSynchronize(nullptr);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; ++r) {
+      (void)rse_fill_splitmix(buf, 64, 1, 0, nullptr);
+      (void)hipStreamSynchronize(nullptr);
+    }
+    const double dt =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / reps;
+    std::printf("tiny launch + synchronize (the floor): %.1f us per call\n", dt * 1e6);
+  }
+  {  // the verify kernel alone: events around back-to-back verifies of one stripe
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    int ok = 1;
+    const int reps = 32;
+    (void)hipEventRecord(a, nullptr);
+    for (int r = 0; r < reps; ++r)
+      (void)rse_verify(c, const_cast<const void* const*>(sh[r % S].data()), lens.data(), k + p,
+                       &ok, nullptr);
+    (void)hipEventRecord(b, nullptr);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("verify, device time between events (launch gaps included): %.1f us per call\n",
+                ms * 1e3 / reps);
+  }
   rse_codec_free(c);
   (void)hipFree(buf);
   return 0;

@@ -1,63 +1,77 @@
-// valu_probe.hip -- issue-rate probe: wave64 instructions per cycle per CU for
-// v_perm_b32 vs v_xor_b32 (and mixes), 8 independent chains per lane so
-// dependency latency is hidden; full occupancy.
+// VALU issue-rate probe for gfx950: how many VALU instructions per cycle a
+// SIMD retires for the instruction mixes of the bit-sliced kernels (v_bitop3
+// with three sources, v_xor with two, v_bfi), at 1..8 waves per SIMD.  The
+// chains are independent across 16 registers, so dependencies do not limit.
+// Cycles are read with s_memtime inside the kernel (shader clock), so the
+// rate is per clock, not per second.
 //   hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/valu_probe
 #include <hip/hip_runtime.h>
+
 #include <cstdio>
 
-#define CHAINS 8
-template <int KIND>
-__global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed, int iters) {
-  unsigned x[CHAINS], t0 = seed * 0x9E3779B9u + threadIdx.x, t1 = t0 ^ 0x5bd1e995u;
+constexpr int kIters = 4096;
+
+template <int OP>
+__global__ __launch_bounds__(256) void probe(uint32_t* out, uint64_t* cyc, uint32_t seed) {
+  uint32_t r[16];
 #pragma unroll
-  for (int c = 0; c < CHAINS; ++c) x[c] = t0 + c * 0x01010101u;
-  for (int i = 0; i < iters; ++i) {
+  for (int i = 0; i < 16; ++i) r[i] = seed * (threadIdx.x + i) + i;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < kIters; ++it) {
 #pragma unroll
-    for (int c = 0; c < CHAINS; ++c) {
-      if (KIND == 0) x[c] = __builtin_amdgcn_perm(t0, t1, x[c] & 0x07070707u);  // perm + and
-      if (KIND == 1) x[c] = (x[c] ^ t0) & t1;                                     // xor + and
-      if (KIND == 2) x[c] = __builtin_amdgcn_perm(t0, t1, x[c]);                  // perm only
-      if (KIND == 3) x[c] = (x[c] ^ t0) ^ (x[c] << 1);                            // xor, shl, xor
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (OP == 0)  // v_bitop3: three sources (XOR3)
+        asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r[i]) : "v"(r[(i + 5) & 15]), "v"(r[(i + 10) & 15]));
+      else if constexpr (OP == 1)  // v_xor: two sources
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[i]) : "v"(r[(i + 5) & 15]));
+      else  // v_bfi: three sources
+        asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(r[(i + 5) & 15]), "v"(r[(i + 10) & 15]));
     }
   }
-  unsigned r = 0;
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  uint32_t x = 0;
 #pragma unroll
-  for (int c = 0; c < CHAINS; ++c) r ^= x[c];
-  out[blockIdx.x * 256 + threadIdx.x] = r;
+  for (int i = 0; i < 16; ++i) x ^= r[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+  if (threadIdx.x % 64 == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) / 64] = t1 - t0;
 }
 
 int main() {
-  unsigned* out;
-  hipMalloc(&out, 2048 * 256 * 4);
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  int dev;
-  hipGetDevice(&dev);
-  int clk_khz;
-  hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, dev);
-  const int iters = 4096, blocks = 2048;
-  const char* names[] = {"perm+and", "xor+and", "perm", "xor+shl+xor"};
-  const int insts[] = {2, 2, 1, 3};
-  for (int kind = 0; kind < 4; ++kind) {
-    auto launch = [&] {
-      if (kind == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
-      if (kind == 1) hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
-      if (kind == 2) hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
-      if (kind == 3) hipLaunchKernelGGL(k<3>, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
-    };
-    launch();
-    hipDeviceSynchronize();
-    hipEventRecord(a);
-    launch();
-    hipEventRecord(b);
-    hipEventSynchronize(b);
-    float ms;
-    hipEventElapsedTime(&ms, a, b);
-    double wave_insts = (double)blocks * 4 * iters * CHAINS * insts[kind];
-    double per_s = wave_insts / (ms * 1e-3);
-    printf("%-12s %8.3f ms  %.3e wave-inst/s  = %.2f wave-inst/clk/CU at %d MHz nominal\n",
-           names[kind], ms, per_s, per_s / 256 / (clk_khz * 1e3), clk_khz / 1000);
-  }
+  int cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  const char* names[3] = {"v_bitop3 (3 src)", "v_xor (2 src)", "v_bfi (3 src)"};
+  for (int op = 0; op < 3; ++op)
+    for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: 4 SIMDs, 256-lane groups of 4 waves
+      const int blocks = cus * wps;
+      uint32_t* out;
+      uint64_t* cyc;
+      hipMalloc(&out, (size_t)blocks * 256 * 4);
+      hipMalloc(&cyc, (size_t)blocks * 4 * 8);
+      auto k = op == 0 ? probe<0> : op == 1 ? probe<1> : probe<2>;
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, cyc, 3u);
+      hipEvent_t a, b;
+      hipEventCreate(&a);
+      hipEventCreate(&b);
+      hipEventRecord(a);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, cyc, 5u);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms = 0;
+      hipEventElapsedTime(&ms, a, b);
+      uint64_t* h = new uint64_t[blocks * 4];
+      hipMemcpy(h, cyc, (size_t)blocks * 4 * 8, hipMemcpyDeviceToHost);
+      double mean = 0;
+      for (int i = 0; i < blocks * 4; ++i) mean += (double)h[i];
+      mean /= blocks * 4;
+      const double insts = (double)kIters * 16;  // per wave
+      // per SIMD: wps waves side by side; s_memtime counts shader clocks
+      const double per_ns = insts * blocks * 4 / (cus * 4.0) / (ms * 1e6);
+      std::printf("%-18s %d waves/SIMD: %.3f ms, %.3f VALU instr/ns per SIMD, %.0f clocks per "
+                  "wave -> %.3f instr/clock per SIMD, clock %.2f GHz\n",
+                  names[op], wps, ms, per_ns, mean, insts * wps / mean, mean / (ms * 1e6));
+      delete[] h;
+      hipFree(out);
+      hipFree(cyc);
+    }
   return 0;
 }
