@@ -1569,60 +1569,41 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
   const size_t k = c->k, p = c->p, T = c->total, sb = shard_len * c->esize();
-  for (size_t s = 0; s < n_stripes; ++s) {  // core.rs:747-772, stripe by stripe
-    size_t np = 0;
-    for (size_t i = 0; i < T; ++i) np += present[s * T + i] ? 1 : 0;
+  // One pass over the flags: validation (core.rs:747-772, stripe by stripe),
+  // and what the planners size their work by -- the sigma rows any stripe
+  // uses (its syndrome rows R and missing parity rows), the most missing
+  // data shards and the most outputs of a stripe.
+  uint32_t need = 0, e_cap = 0, nout_cap = 0;
+  for (size_t s = 0; s < n_stripes; ++s) {
+    const uint8_t* pr = present + s * T;
+    uint32_t ne = 0, nr = 0, nmp = 0;
+    for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0u : 1u;
+    size_t np = k - ne;
+    for (size_t r = 0; r < p; ++r) {
+      const bool here = pr[k + r] != 0;
+      np += here ? 1 : 0;
+      const bool syn = here && nr < ne;
+      nr += syn ? 1u : 0u;
+      if (!here && !data_only) ++nmp;
+      if (syn || (!here && !data_only)) need = std::max<uint32_t>(need, (uint32_t)r + 1);
+    }
     if (np && shard_len == 0) return RSE_EMPTY_SHARD;
     if (np < k) return RSE_TOO_FEW_SHARDS_PRESENT;
+    e_cap = std::max(e_cap, ne);
+    nout_cap = std::max(nout_cap, ne + nmp);
   }
-  uint8_t* base = static_cast<uint8_t*>(stripes);
-  hipStream_t st = (hipStream_t)stream;
-  // Runs of consecutive stripes with one erasure pattern (a lost disk: every
-  // stripe misses the same shards) go through the shared-pattern path: one
-  // plan per run, and the pattern's own kernel once it has one (core.rs:
-  // 697-731 caches the pattern; used twice, it is specialised), instead of a
-  // plan and a mixing per stripe.  Used when the runs are long (at most one
-  // run per 16 stripes on average).
-  {
-    std::vector<std::pair<size_t, size_t>> runs;  // [first, count)
-    for (size_t s0 = 0; s0 < n_stripes;) {
-      size_t s1 = s0 + 1;
-      while (s1 < n_stripes && std::memcmp(present + s1 * T, present + s0 * T, T) == 0) ++s1;
-      runs.emplace_back(s0, s1 - s0);
-      if (runs.size() * 16 > n_stripes) break;
-      s0 = s1;
-    }
-    size_t covered = 0;
-    for (auto& r : runs) covered += r.second;
-    if (covered == n_stripes && runs.size() * 16 <= n_stripes) {
-      for (auto& r : runs) {
-        const int rc = flat_reconstruct(c, base + r.first * T * sb, shard_len, r.second,
-                                        present + r.first * T, data_only != 0, st);
-        if (rc) return rc;
-      }
-      return RSE_OK;
-    }
-  }
-  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
+  if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
+  uint8_t* base = static_cast<uint8_t*>(stripes);  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
+  // host inputs of the copies below: alive until the stream is synchronised
+  const Rows prow = parity_rows(c);
   // 1. whole 16 KiB chunks on the bit-sliced syndrome kernels (compiled or
   //    run-time specialised codecs), planned per stripe on the device
   if (fits && sb >= 4096 && sb % 16u == 0 && aligned16(base) &&
       rse::get_option(RSE_OPT_BITSLICE)) {
     want_bitslice(c, sb, false, n_stripes);
-    uint32_t need = 0;  // sigma rows any stripe uses: its R and missing parity rows
-    for (size_t s = 0; s < n_stripes; ++s) {
-      const uint8_t* pr = present + s * T;
-      size_t ne = 0, nr = 0;
-      for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0 : 1;
-      for (size_t r = 0; r < p; ++r) {
-        const bool syn = pr[k + r] && nr < ne;
-        nr += syn ? 1 : 0;
-        if (syn || (!pr[k + r] && !data_only)) need = std::max<uint32_t>(need, (uint32_t)r + 1);
-      }
-    }
     if (need > 0) {
-      const Rows rows = parity_rows(c);
+      const Rows& rows = prow;
       const size_t rows_bytes = rows.c.size() * 2, pres_off = (rows_bytes + 255) & ~size_t(255);
       const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
       uint8_t* ws = nullptr;
@@ -1638,8 +1619,11 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
             reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
       hipError_t f = hipFreeAsync(ws, st);
       if (e == hipSuccess) e = f;
-      if (e == hipSuccess) e = hipStreamSynchronize(st);  // `rows` dies here
-      if (e != hipSuccess) return dev_fail(e);
+      if (e == hipSuccess && bs_done == sb) e = hipStreamSynchronize(st);  // `prow` dies next
+      if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        return dev_fail(e);
+      }
       done = bs_done;
     } else {
       return RSE_OK;  // nothing missing that this call rebuilds, in any stripe
@@ -1649,17 +1633,6 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   // 2. the rest of every shard (all of it if step 1 did not apply): planned
   //    per stripe on the device (recon_plan_kernel: e x e syndrome inverse,
   //    composed rows as descriptors), coded by the table kernels
-  uint32_t e_cap = 0, nout_cap = 0;
-  for (size_t s = 0; s < n_stripes; ++s) {
-    const uint8_t* pr = present + s * T;
-    uint32_t ne = 0, nmp = 0;
-    for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0 : 1;
-    if (!data_only)
-      for (size_t r = 0; r < p; ++r) nmp += pr[k + r] ? 0 : 1;
-    e_cap = std::max(e_cap, ne);
-    nout_cap = std::max(nout_cap, ne + nmp);
-  }
-  if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
   if (T > 0xffffu ||
       rse::recon_plan_lds((uint32_t)k, (uint32_t)T, e_cap, nout_cap) > rse::kReconPlanLdsMax) {
     // past the device planner's LDS budget: the host planner, stripe by stripe
@@ -1668,12 +1641,15 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     for (size_t s = 0; s < n_stripes; ++s) {
       for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb + done;
       int rc = reconstruct_impl(c, ptrs.data(), lens.data(), present + s * T, T, data_only != 0, st);
-      if (rc) return rc;
+      if (rc) {
+        (void)hipStreamSynchronize(st);  // step 1's copies read `prow`
+        return rc;
+      }
       ++g_host_planned;
     }
+    RSE_HIP(hipStreamSynchronize(st));
     return RSE_OK;
   }
-  const Rows prow = parity_rows(c);
   const size_t n_ib = (k + 31) / 32, n_ob = (nout_cap + 15) / 16;
   const size_t per_stripe = n_ib * n_ob * sizeof(CodeArgs);
   // stripes per planning group: descriptors of at most 256 MiB at a time
@@ -1694,11 +1670,11 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
                                st);
   }
   const hipError_t f = hipFreeAsync(ws, st);
+  // `prow` and the caller's flags must outlive the copies that read them
+  const hipError_t y = hipStreamSynchronize(st);
   if (e != hipSuccess) return dev_fail(e);
   if (f != hipSuccess) return dev_fail(f);
-  // The pageable copies above were staged before returning, but `prow` dies
-  // here: make sure the runtime is done reading it.
-  RSE_HIP(hipStreamSynchronize(st));
+  RSE_HIP(y);
   return RSE_OK;
 }
 
