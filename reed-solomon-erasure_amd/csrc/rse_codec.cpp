@@ -1593,7 +1593,8 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     nout_cap = std::max(nout_cap, ne + nmp);
   }
   if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
-  uint8_t* base = static_cast<uint8_t*>(stripes);  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
+  uint8_t* base = static_cast<uint8_t*>(stripes);
+  hipStream_t st = (hipStream_t)stream;  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
   // host inputs of the copies below: alive until the stream is synchronised
   const Rows prow = parity_rows(c);
