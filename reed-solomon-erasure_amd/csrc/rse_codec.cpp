@@ -1594,7 +1594,34 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   }
   if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
   uint8_t* base = static_cast<uint8_t*>(stripes);
-  hipStream_t st = (hipStream_t)stream;  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
+  hipStream_t st = (hipStream_t)stream;
+  // Runs of consecutive stripes with one erasure pattern (a lost disk: every
+  // stripe misses the same shards) go through the shared-pattern path: one
+  // plan per run, and the pattern's own kernel once it has one (core.rs:
+  // 697-731 caches the pattern; used twice, it is specialised), instead of a
+  // plan and a mixing per stripe.  Used when the runs are long (at most one
+  // run per 16 stripes on average).
+  {
+    std::vector<std::pair<size_t, size_t>> runs;  // [first, count)
+    for (size_t s0 = 0; s0 < n_stripes;) {
+      size_t s1 = s0 + 1;
+      while (s1 < n_stripes && std::memcmp(present + s1 * T, present + s0 * T, T) == 0) ++s1;
+      runs.emplace_back(s0, s1 - s0);
+      if (runs.size() * 16 > n_stripes) break;
+      s0 = s1;
+    }
+    size_t covered = 0;
+    for (auto& r : runs) covered += r.second;
+    if (covered == n_stripes && runs.size() * 16 <= n_stripes) {
+      for (auto& r : runs) {
+        const int rc = flat_reconstruct(c, base + r.first * T * sb, shard_len, r.second,
+                                        present + r.first * T, data_only != 0, st);
+        if (rc) return rc;
+      }
+      return RSE_OK;
+    }
+  }
+  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
   // host inputs of the copies below: alive until the stream is synchronised
   const Rows prow = parity_rows(c);
