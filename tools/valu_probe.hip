@@ -4,7 +4,7 @@
 // chains are independent across 16 registers, so dependencies do not limit.
 // Cycles are read with s_memtime inside the kernel (shader clock), so the
 // rate is per clock, not per second.
-//   hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/valu_probe
+//   hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/bin/valu_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
