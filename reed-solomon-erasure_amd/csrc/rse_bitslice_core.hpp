@@ -94,13 +94,16 @@ __device__ __forceinline__ uint32_t temp_source(const uint32_t* src, int t) {
   return c == 255 ? src[a] ^ src[b] : xor3(src[a], src[b], src[c == 255 ? 0 : c]);
 }
 
-// (x & m) | (y & ~m) as one v_bfi_b32.  Written out because the C form of the
-// transpose below is rewritten by the compiler into masked shifts that share
-// subexpressions across the pair: ~1.4 extra v_and per bfi (1026 in the
-// GF(2^16) 20+8 kernel; tools/isa_probe.sh).
+// (x & m) | (y & ~m) in one instruction.  Written out because the C form of
+// the transpose below is rewritten by the compiler into masked shifts that
+// share subexpressions across the pair: ~1.4 extra v_and per select (1026 in
+// the GF(2^16) 20+8 kernel; tools/isa_probe.sh).  As v_bitop3_b32 with the
+// select's truth table (0xCA: S0 ? S1 : S2 per bit), not v_bfi_b32: on gfx950
+// v_bfi issues at about half the rate of v_bitop3 (tools/valu_probe.hip,
+// profiles/r03/valu_probe.log).
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
   uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(m), "v"(x), "v"(y));
   return r;
 }
 

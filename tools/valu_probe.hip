@@ -24,8 +24,14 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint64_t* cyc, uint3
         asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r[i]) : "v"(r[(i + 5) & 15]), "v"(r[(i + 10) & 15]));
       else if constexpr (OP == 1)  // v_xor: two sources
         asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[i]) : "v"(r[(i + 5) & 15]));
-      else  // v_bfi: three sources
+      else if constexpr (OP == 2)  // v_bfi: three sources
         asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(r[(i + 5) & 15]), "v"(r[(i + 10) & 15]));
+      else if constexpr (OP == 3)  // v_bfi with the mask in an SGPR (the transposes' form)
+        asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(r[i]) : "s"(seed), "v"(r[(i + 5) & 15]));
+      else if constexpr (OP == 4)  // the same select as v_bitop3 (truth table 0xCA)
+        asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0xca" : "+v"(r[i]) : "s"(seed), "v"(r[(i + 5) & 15]));
+      else  // shift (the transposes' other half)
+        asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(r[i]) : "v"(r[(i + 5) & 15]));
     }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -39,15 +45,17 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint64_t* cyc, uint3
 int main() {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const char* names[3] = {"v_bitop3 (3 src)", "v_xor (2 src)", "v_bfi (3 src)"};
-  for (int op = 0; op < 3; ++op)
+  const char* names[6] = {"v_bitop3 (3 src)", "v_xor (2 src)", "v_bfi (3 src)",
+                          "v_bfi (s mask)", "v_bitop3 0xca (s)", "v_lshlrev"};
+  for (int op = 0; op < 6; ++op)
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: 4 SIMDs, 256-lane groups of 4 waves
       const int blocks = cus * wps;
       uint32_t* out;
       uint64_t* cyc;
       hipMalloc(&out, (size_t)blocks * 256 * 4);
       hipMalloc(&cyc, (size_t)blocks * 4 * 8);
-      auto k = op == 0 ? probe<0> : op == 1 ? probe<1> : probe<2>;
+      auto k = op == 0 ? probe<0> : op == 1 ? probe<1> : op == 2 ? probe<2>
+             : op == 3 ? probe<3> : op == 4 ? probe<4> : probe<5>;
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, cyc, 3u);
       hipEvent_t a, b;
       hipEventCreate(&a);
