@@ -98,9 +98,9 @@ __device__ __forceinline__ uint32_t temp_source(const uint32_t* src, int t) {
 // the transpose below is rewritten by the compiler into masked shifts that
 // share subexpressions across the pair: ~1.4 extra v_and per select (1026 in
 // the GF(2^16) 20+8 kernel; tools/isa_probe.sh).  As v_bitop3_b32 with the
-// select's truth table (0xCA: S0 ? S1 : S2 per bit), not v_bfi_b32: on gfx950
-// v_bfi issues at about half the rate of v_bitop3 (tools/valu_probe.hip,
-// profiles/r03/valu_probe.log).
+// select's truth table (0xCA: S0 ? S1 : S2 per bit) rather than v_bfi_b32:
+// the same issue rate with an SGPR mask (tools/valu_probe.hip), +0.5-1 % on
+// the headline and wide encodes in a same-box A/B (profiles/r03/ab_bitop3/).
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
   uint32_t r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(m), "v"(x), "v"(y));
