@@ -588,34 +588,37 @@ def other_configs(stream):
         out[f"gf{field}_{k}_{p}"] = d
         del buf, v
         torch.cuda.empty_cache()
-    out["gf8_50_20"] = wide_config(stream, g)
+    out["gf8_50_20"] = wide_config(stream, g, 8, 50, 20)
+    out["gf16_40_12"] = wide_config(stream, g, 16, 40, 12)
     return out
 
 
-def wide_config(stream, g):
-    """GF(2^8) 50+20 x 1 MiB -- the widest codec of the reference's own bench
-    (benches/bandwidth.rs:128) -- on its one-module kernel (rse_jit.cpp
+def wide_config(stream, g, field, k, p):
+    """A wide codec x 1 MiB shards on its one-module kernel (rse_jit.cpp
     kJitWide, built by hiprtc in helper processes before timing), stripe 0's
-    parity against the reference digests of tests/golden."""
+    parity against the digests of tests/golden: GF(2^8) 50+20, the widest
+    codec of the reference's own bench (benches/bandwidth.rs:128; digest from
+    the reference's compiled kernel), and GF(2^16) 40+12 (digest from the
+    restatement of lib.rs:99-118)."""
     import torch
     import reed_solomon_erasure as R
     from reed_solomon_erasure.core import fill_splitmix, last_kernel
-    lib = R_lib()
-    k, p, nbytes, stripes = 50, 20, MiB, 128
+    nbytes, stripes = MiB, 128
     T = k + p
     buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
     v = buf.view(stripes, T, nbytes)
     for s_ in range(stripes):
         for i in range(k):
             fill_splitmix(v[s_, i], SEED, shard_id(s_, i))
-    r = R.core.ReedSolomon(k, p, 8)
+    r = R.core.ReedSolomon(k, p, field)
     t0 = time.perf_counter()
     kind = r.kernel_kind(wait=True)
     build_s = time.perf_counter() - t0
-    enc = timed_gbps(lambda: r.encode_flat(buf, nbytes, stripes), stripes * T * nbytes, stream)
-    want = g["full_size"][f"gf8_{k}_{p}_{nbytes}"]["parity_sha256"]
+    elems = nbytes // (field // 8)
+    enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream)
+    want = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]["parity_sha256"]
     got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
-    d = {"workload": f"gf8 {k}+{p} x 1 MiB, {stripes} stripes/launch", "kernels": kind,
+    d = {"workload": f"gf{field} {k}+{p} x 1 MiB, {stripes} stripes/launch", "kernels": kind,
          "kernel": last_kernel(), "build_seconds": round(build_s, 1),
          "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
          "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),

@@ -164,6 +164,16 @@ def generated():
     O.code_some_slices(16, rr, data, par)
     full[f"gf16_{k}_{p}_{nbytes}"] = {"data_sha256": [sha(d) for d in data],
                                       "parity_sha256": [sha(x) for x in par]}
+    # GF(2^16) 40+12 x 1 MiB: a wide GF(2^16) codec (k > 32, p > 8) on its
+    # one-module kernel in bench.py's other_configs
+    k, p, nbytes = 40, 12, 1 << 20
+    cc = O.Codec(16, k, p)
+    rr = np.ascontiguousarray(cc.matrix()[k:])
+    data = [O.splitmix_bytes(SEED, s, nbytes) for s in range(k)]
+    par = [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    O.code_some_slices(16, rr, data, par)
+    full[f"gf16_{k}_{p}_{nbytes}"] = {"data_sha256": [sha(d) for d in data],
+                                      "parity_sha256": [sha(x) for x in par]}
     out["full_size"] = full
     out["gf8_10_4_stripe_parity"] = stripe_parity(ref)
     return out

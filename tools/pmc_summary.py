@@ -37,8 +37,12 @@ def load(root, regex):
 def main():
     root = sys.argv[1]
     regex = sys.argv[2] if len(sys.argv) > 2 else ""
-    tot, disp = load(root, regex)
-    out = {"counters": {k: tot[k] for k in sorted(tot)}, "dispatches": dict(disp)}
+    raw, disp = load(root, regex)
+    # every pass repeats SQ_WAVE_CYCLES / SQ_WAVES: ratios are taken between
+    # per-dispatch means, so a counter of one pass and one of all passes agree
+    tot = {k: raw[k] / disp[k] for k in raw}
+    out = {"counters": {k: raw[k] for k in sorted(raw)}, "dispatches": dict(disp),
+           "per_dispatch_mean": {k: round(tot[k], 1) for k in sorted(tot)}}
     wc = tot.get("SQ_WAVE_CYCLES")
     if wc:
         for name, key in (("valu_per_wave_cycle", "SQ_ACTIVE_INST_VALU"),
