@@ -187,6 +187,19 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
   bitslice_recon_desc_body_deep<C, true, NS, D>(descs, chunks_per_stripe, n_stripes);
 }
 
+// 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD).
+template <class C>
+__global__ __launch_bounds__(kBsBlock, 3) void bitslice_recon_pair_kernel(
+    const BsReconArgs a, uint64_t chunks_per_stripe) {
+  bitslice_recon_pair_body<C, true>(a, chunks_per_stripe);
+}
+
+template <class C>
+__global__ __launch_bounds__(kBsBlock, 3) void bitslice_recon_desc_pair_kernel(
+    const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
+  bitslice_recon_desc_pair_body<C, true>(descs, chunks_per_stripe, n_stripes);
+}
+
 // ------------------------------------------------- batched reconstruct planner
 // One lane per stripe of rse_reconstruct_batch: the syndrome plan of
 // rse_codec.cpp bitslice_reconstruct on the device.  The valid/invalid
@@ -351,6 +364,8 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
+  BsRecFn rec_pair;            // NS = 8 on wave pairs (nullptr below 8 parity rows)
+  BsDescFn rec_desc_pair;
 };
 
 template <class C, int NS, int MIX>
@@ -371,6 +386,16 @@ constexpr BsDesc4Fn rec_desc4_fn() {
 template <class C, int NS, int D>
 constexpr BsRecFn rec_deep_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_deep_kernel<C, NS, D>;
+  else return nullptr;
+}
+template <class C>
+constexpr BsRecFn rec_pair_fn() {
+  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C>;
+  else return nullptr;
+}
+template <class C>
+constexpr BsDescFn rec_desc_pair_fn() {
+  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C>;
   else return nullptr;
 }
 template <class C, int NS, int D>
@@ -406,7 +431,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
    {{rec_desc_deep_fn<C, 1, 2>(), rec_desc_deep_fn<C, 2, 2>(), rec_desc_deep_fn<C, 4, 2>(), \
      rec_desc_deep_fn<C, 8, 2>()},                                                     \
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
-     rec_desc_deep_fn<C, 8, 3>()}}}
+     rec_desc_deep_fn<C, 8, 3>()}},                                                    \
+   rec_pair_fn<C>(), rec_desc_pair_fn<C>()}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -528,6 +554,19 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const int mix = (int)get_option(17);
     const int depth = mix == kReconMixHorner ? (int)get_option(27) : 1;  // RSE_OPT_RECON_DEPTH
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
+    // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
+    if (slot == 3 && sh.rec_pair && get_option(28) && mix >= kReconMixHorner && depth == 1) {
+      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs", field, k, p);
+      uint64_t gp = grid > 0 ? (uint64_t)grid : 8192u;
+      if (gp > 2 * total) gp = 2 * total;
+      if (gp > 0x7fffffffu) gp = 0x7fffffffu;
+      hipLaunchKernelGGL(sh.rec_pair, dim3((uint32_t)gp), dim3(kBsBlock), 0, stream, a, cps);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      count_bitslice_launch();
+      *handled = true;
+      return hipSuccess;
+    }
     note_kernel("bitslice-recon gf%d %u+%u ns%d %s d%d", field, k, p, 1 << slot, kMixName[mix],
                 depth > 3 ? 3 : depth);
     BsRecFn fn = depth > 1 ? sh.rec_deep[depth > 2 ? 1 : 0][slot] : sh.rec[mix][slot];
@@ -569,7 +608,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   BsDescFn sfn = nullptr;
   BsDesc4Fn sfn4 = nullptr;
   hipFunction_t jfn = nullptr, jfn4 = nullptr;
-  bool compiled = false;
+  bool compiled = false, pairs = false;
   for (const BsShape& sh : kBsShapes) {
     if (sh.field != field || sh.k != k || sh.p != p) continue;
     compiled = true;
@@ -580,6 +619,10 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       if (sh.rec_desc[q] && (1u << q) >= need) {
         sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
         sfn4 = sh.rec_desc4[q];
+        if (q == 3 && sh.rec_desc_pair && get_option(28) && depth == 1) {
+          sfn = sh.rec_desc_pair;  // 8 sigma rows on wave pairs (8 KiB units)
+          pairs = true;
+        }
       }
     if (!sfn) return hipSuccess;
   }
@@ -609,7 +652,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
   uint64_t cps4 = (shard_bytes - cps * kBsChunk) / 4096u, base4 = cps * kBsChunk;
   if (cps) {
-    const uint64_t gx = grid_for(cps * ns);
+    const uint64_t gx = grid_for(cps * ns * (pairs ? 2 : 1));
     if (sfn) {
       hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
                          (const BsReconArgs*)d_descs, cps, ns);

@@ -1385,5 +1385,297 @@ __device__ __forceinline__ void bitslice_recon_desc_body_w4(const BsReconArgs* _
   }
 }
 
+// ---- 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS) ----------------------
+// At NS = 8 one wave holds 128 VGPRs of syndromes and, in the mixing, 64 of
+// pair XORs: 2 waves per SIMD, and the mixing phase (half the VALU work of an
+// 8-erasure chunk) has no loads in flight.  Here two waves share one 4 KiB
+// column of every shard: wave H of the pair accumulates sigma rows 4H..4H+3
+// only (64 VGPRs), so 3 waves fit per SIMD.
+//  * Data inputs: wave H loads and slices the present data shards of index
+//    parity H and passes their planes to its partner through LDS (one barrier
+//    per index pair); both code every data input into their own rows.
+//  * Syndrome inputs: each wave loads the parity shards of its own rows.
+//  * Mixing: output o = sum_r w[o][r] s_r splits into the two waves' partial
+//    sums over their rows, each by Horner's rule over 4 rows (one nibble of the
+//    step mask per step, 19 ops).  A wave computes its partner's outputs'
+//    partials into LDS, then its own, adds the partner's, converts, un-slices
+//    and stores (outputs split in halves).
+// A workgroup's 4 waves are 2 pairs on the two 4 KiB halves of an 8 KiB unit.
+constexpr int kPairRows = 4;
+struct PairLds {
+  u32x4 v[2][2][2][4][64];  // [buffer][pair][role][vector][lane]: 32 KiB
+};
+
+template <class C, int I, int R0, int... OP>
+__device__ __forceinline__ void mac_rows(uint32_t (&acc)[kPairRows * 16], const uint32_t (&pl)[16],
+                                         int_seq<int, OP...>) {
+  if constexpr (C::kGTemps > 0) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint32_t src[8 + C::kGTemps];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) src[q] = pl[g * 8 + q];
+#pragma unroll
+      for (int t = 0; t < C::kGTemps; ++t)
+        if (t < C::planes.ntmp[I]) src[8 + t] = temp_source<C, I>(src, t);
+      // OP < 32: row OP / 8, plane OP % 8 of group g
+      if (g == 0)
+        ((acc[(OP / 8) * 16 + OP % 8] =
+              xacc<C::planes.sel[R0 + OP / 8][I][OP % 8]>(acc[(OP / 8) * 16 + OP % 8], src)),
+         ...);
+      else
+        ((acc[(OP / 8) * 16 + 8 + OP % 8] =
+              xacc<C::planes.sel[R0 + OP / 8][I][OP % 8]>(acc[(OP / 8) * 16 + 8 + OP % 8], src)),
+         ...);
+    }
+  } else {
+    uint32_t in[16 + C::kTemps];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) in[q] = pl[q];
+    if constexpr (C::kTemps > 0) {
+#pragma unroll
+      for (int t = 0; t < C::kTemps; ++t)
+        if (t < C::planes.ntmp[I]) in[16 + t] = temp_source<C, I>(in, t);
+    }
+    ((acc[OP] = xacc<C::planes.sel[R0 + OP / 16][I][OP % C::NP]>(acc[OP],
+                                                                  in + (OP % 16) / C::NP * C::NP)),
+     ...);
+  }
+}
+
+template <class C, int I, int R0>
+__device__ __forceinline__ void mac_rows(uint32_t (&acc)[kPairRows * 16], const uint32_t (&pl)[16]) {
+  if constexpr (I < C::k) {
+    if constexpr (C::kGTemps > 0) mac_rows<C, I, R0>(acc, pl, make_int_seq<kPairRows * 8>{});
+    else mac_rows<C, I, R0>(acc, pl, make_int_seq<kPairRows * 16>{});
+  }
+}
+
+// The wave's next own input after index J (own: bit set in `own`; bits < k
+// data shards, k + r parity row r), loaded into nxt; returns whether there is one.
+template <class C, bool NT>
+__device__ __forceinline__ bool pair_prefetch(u32x4 (&nxt)[4], const BsReconArgs& a, uint64_t own,
+                                              int J, uint64_t off) {
+  const uint64_t rest = own & ~((2ull << J) - 1ull);
+  if (!rest) return false;
+  load4<NT, 1024u>(nxt, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(rest)) + off);
+  return true;
+}
+
+// Data rounds T.. : indices 2T (role 0) and 2T + 1 (role 1).
+template <class C, bool NT, int H, int T>
+__device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4 (&cur)[4],
+                                          const BsReconArgs& a, uint64_t own, uint32_t present,
+                                          uint64_t off, u32x4 (*mine)[64], u32x4 (*theirs)[64],
+                                          uint32_t lane, uint32_t& buf) {
+  if constexpr (2 * T < C::k) {
+    constexpr int J = 2 * T + H, JP = 2 * T + 1 - H;
+    const bool has_own = J < C::k && ((present >> J) & 1u);
+    const bool has_oth = JP < C::k && ((present >> JP) & 1u);
+    if (has_own || has_oth) {  // workgroup-uniform (one pattern per unit)
+      uint32_t pl[16];
+      u32x4* const wr = mine[buf * 16];    // [buf][pair][role] flattened by the caller
+      const u32x4* const rd = theirs[buf * 16];
+      if (has_own) {
+        u32x4 nxt[4];
+        const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
+        __builtin_amdgcn_sched_barrier(0);
+        slice<typename C::Field>(cur, pl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          wr[j * 64 + lane] = (u32x4){pl[4 * j], pl[4 * j + 1], pl[4 * j + 2], pl[4 * j + 3]};
+        if (more) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+        }
+      }
+      __syncthreads();
+      if (has_own) mac_rows<C, J, H * kPairRows>(acc, pl);
+      if (has_oth) {
+        uint32_t pp[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32x4 x = rd[j * 64 + lane];
+          pp[4 * j] = x[0];
+          pp[4 * j + 1] = x[1];
+          pp[4 * j + 2] = x[2];
+          pp[4 * j + 3] = x[3];
+        }
+        mac_rows<C, JP, H * kPairRows>(acc, pp);
+      }
+#pragma unroll
+      for (int q = 0; q < kPairRows * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      buf ^= 1u;
+    }
+    pair_data<C, NT, H, T + 1>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  }
+}
+
+// The partial sum over the wave's rows of output o (Horner's rule, 4 rows),
+// plus its sigma row if that is one of them.
+template <class C, int H>
+__device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
+                                             const uint32_t (&acc)[kPairRows * 16],
+                                             const uint32_t (&d)[2][16], uint32_t (&v)[16]) {
+  using F = typename C::Field;
+  constexpr int NB = HornerF<F>::N;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = 0u;
+#pragma unroll 1
+  for (int w = 0; w < NB / 4; ++w) {
+    const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane(a.hm[o][w]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t m = (word >> (8 * b)) & 0xFFu;
+      h_group<F, true, 0, kPairRows, 2>(v, acc, d, H ? (m >> 4) : (m & 15u));
+    }
+  }
+  const int32_t os = __builtin_amdgcn_readfirstlane(a.out_sigma[o]) - H * kPairRows;
+#pragma unroll
+  for (int r = 0; r < kPairRows; ++r)
+    if (os == r) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] ^= acc[r * 16 + q];
+    }
+}
+
+// One 8 KiB unit of one stripe for wave H of pair `pair`: off = the lane's
+// byte offset (pair's 4 KiB half + lane * 16) from the argument block's shard
+// pointers.
+template <class C, bool NT, int H>
+__device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t off,
+                                                PairLds& lds, uint32_t pair, uint32_t lane) {
+  using F = typename C::Field;
+  constexpr int R0 = H * kPairRows;
+  const uint32_t present = a.present;
+  const uint32_t synd = a.synd, sigma = a.sigma;
+  const uint32_t n_out = __builtin_amdgcn_readfirstlane(a.n_out);
+  // own inputs: data shards of index parity H, then the parity shards of own
+  // syndrome rows
+  const uint64_t par_mask = H ? 0xAAAAAAAAull : 0x55555555ull;
+  const uint64_t own = ((uint64_t)present & par_mask) |
+                       ((uint64_t)((synd >> R0) & 0xFu) << (C::k + R0));
+  uint32_t acc[kPairRows * 16];
+#pragma unroll
+  for (int q = 0; q < kPairRows * 16; ++q) acc[q] = 0u;
+  u32x4 cur[4];
+  if (own) load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + off);
+  uint32_t buf = 0;
+  u32x4(*mine)[64] = lds.v[0][pair][H];
+  u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
+  pair_data<C, NT, H, 0>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  // own syndrome rows: s_r = sigma_r ^ parity_r
+#pragma unroll
+  for (int i = 0; i < kPairRows; ++i) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int J = C::k + R0 + i;
+    if ((own >> J) & 1u) {
+      u32x4 nxt[4];
+      const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t pl[16];
+      slice<F>(cur, pl);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i * 16 + q] ^= pl[q];
+      if (more) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+  }
+  if constexpr (HornerF<F>::N == 16) {
+#pragma unroll
+    for (int r = 0; r < kPairRows; ++r)
+      if ((sigma >> (R0 + r)) & 1u) to_basis16(&acc[r * 16], make_int_seq<16>{});
+  }
+  uint32_t d[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[t][q] = acc[2 * t * 16 + q] ^ acc[(2 * t + 1) * 16 + q];
+  // outputs [0, half) are role 0's, [half, n_out) role 1's; exchange rounds of
+  // two outputs a wave through the same LDS (the partner may still be reading
+  // the last data round's planes: one barrier first)
+  const uint32_t half = (n_out + 1) / 2;
+  const uint32_t mine0 = H * half, theirs0 = (1 - H) * half;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t m = 0; m < half; m += 2) {
+#pragma unroll 1
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t po = theirs0 + m + j;
+      if (m + j < half && po < n_out) {
+        uint32_t v[16];
+        pair_partial<C, H>(a, po, acc, d, v);
+        u32x4(*x)[64] = lds.v[j][pair][H];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q][lane] = (u32x4){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t o = mine0 + m + j;
+      if (m + j < half && o < n_out) {
+        uint32_t v[16];
+        pair_partial<C, H>(a, o, acc, d, v);
+        const u32x4(*x)[64] = lds.v[j][pair][1 - H];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4 t = x[q][lane];
+          v[4 * q] ^= t[0];
+          v[4 * q + 1] ^= t[1];
+          v[4 * q + 2] ^= t[2];
+          v[4 * q + 3] ^= t[3];
+        }
+        if constexpr (HornerF<F>::N == 16) from_basis16(v, make_int_seq<16>{});
+        u32x4 xs[4];
+        unslice<F>(v, xs);
+        uint8_t* dst = a.out[o];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stv<NT>(dst + off + q * 1024u, xs[q]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Units of 8 KiB: unit u of a stripe with cps 16 KiB chunks covers bytes
+// [u * 8192, u * 8192 + 8192); pair p its half p.
+template <class C, bool NT>
+__device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
+                                                         uint64_t chunks_per_stripe) {
+  __shared__ PairLds lds;
+  const uint64_t upc = chunks_per_stripe * 2, total = upc * a.n_stripes;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
+  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    const uint64_t stripe = u / upc, sub = u - stripe * upc;
+    const uint64_t off = stripe * a.stripe_stride + sub * 8192u + pair * 4096u + lane * 16u;
+    if (wave & 1u) recon_pair_unit<C, NT, 1>(a, off, lds, pair, lane);
+    else recon_pair_unit<C, NT, 0>(a, off, lds, pair, lane);
+  }
+}
+
+// The same over per-stripe argument blocks (rse_reconstruct_batch).
+template <class C, bool NT>
+__device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs* __restrict__ descs,
+                                                              uint64_t chunks_per_stripe,
+                                                              uint64_t n_stripes) {
+  __shared__ PairLds lds;
+  const uint64_t upc = chunks_per_stripe * 2, total = upc * n_stripes;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
+  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    const uint64_t stripe = u / upc, sub = u - stripe * upc;
+    const BsReconArgs& a = desc_at(descs, stripe);
+    if (a.n_out == 0) continue;  // workgroup-uniform
+    const uint64_t off = sub * 8192u + pair * 4096u + lane * 16u;
+    if (wave & 1u) recon_pair_unit<C, NT, 1>(a, off, lds, pair, lane);
+    else recon_pair_unit<C, NT, 0>(a, off, lds, pair, lane);
+  }
+}
+
 }  // namespace
 }  // namespace rse

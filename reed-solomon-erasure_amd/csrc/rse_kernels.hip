@@ -787,6 +787,7 @@ struct Options {
   int64_t jit_exact = 1;          // run-time networks: exact-decomposition temporaries
   int64_t wide_depth = 1;         // wide modules: inputs in flight per wave (1..4)
   int64_t recon_depth = 1;        // syndrome reconstruct: inputs in flight per lane (1..4)
+  int64_t recon_pairs = 1;        // syndrome reconstruct at 8 sigma rows on wave pairs
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1224,6 +1225,7 @@ int set_option(int key, int64_t value) {
     case 23: g_opt.jit_exact = value ? 1 : 0; return 0;
     case 26: g_opt.wide_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 27: g_opt.recon_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
+    case 28: g_opt.recon_pairs = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1263,6 +1265,7 @@ int64_t get_option(int key) {
     case 23: return g_opt.jit_exact;
     case 26: return g_opt.wide_depth;
     case 27: return g_opt.recon_depth;
+    case 28: return g_opt.recon_pairs;
     default: return -1;
   }
 }

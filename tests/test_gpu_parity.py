@@ -725,6 +725,7 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
     names = {0: "mix-tables", 1: "mix-chain", 2: "mix-horner ", 3: "mix-horner4"}
     jp = lib.rse_get_option(11)
     lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
+    lib.rse_set_option(28, 0)  # 8 sigma rows in one wave too (pairs: test_reconstruct_wave_pairs)
     try:
         for mix in (3, 2, 1, 0):
             assert lib.rse_set_option(17, mix) == 0
@@ -741,6 +742,73 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
                     assert (host(tb[i]).reshape(-1) == full[i]).all(), (mix, erased, i)
     finally:
         lib.rse_set_option(17, 3)
+        lib.rse_set_option(11, jp)
+        lib.rse_set_option(28, 1)
+
+
+def test_reconstruct_wave_pairs(R):
+    """GF(2^16) 20+8 syndrome reconstruct at 8 sigma rows on wave pairs
+    (RSE_OPT_RECON_PAIRS, the default): each wave of a pair holds 4 syndrome
+    rows, data planes are exchanged through LDS and the outputs' partial sums
+    combined there.  Against the oracle: 8 data shards lost (the bench's
+    pattern), odd output counts (one wave owns one more output), missing
+    parity rows on either wave's rows, data shards of only one index parity
+    present in a round, patterns whose syndrome rows are all on one wave, and
+    random patterns; the shared-pattern kernel (flat stripes, one 16 KiB chunk
+    plus a table-kernel tail) and reconstruct_batch (per-stripe patterns, the
+    descriptor kernel) alike, each checked to run on the pair kernels."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    k, p, field = 20, 8, 16
+    nbytes = 16384 * 3  # 3 chunks = 6 units of 8 KiB (last_kernel names the pair kernel)
+    n_elems = nbytes // 2
+    rng = np.random.default_rng(2028)
+    r = R.core.ReedSolomon(k, p, field)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    patterns = [list(range(8)), list(range(12, 20)), [1, 3, 5, 7, 9, 11, 13], [0, 2, 4, 6, 8],
+                list(range(5)) + [k + 5, k + 6, k + 7], [0, k + 4, k + 5, k + 6, k + 7],
+                [19, k + 7], list(range(7)) + [k], [3, 4, 5, 6, 7, 8, 9, 10],
+                [0, 1, 2, 3, 4, 5, 6, k + 7]]
+    patterns += [sorted(rng.choice(k + p, int(rng.integers(5, p + 1)), replace=False).tolist())
+                 for _ in range(8)]
+    jp = lib.rse_get_option(11)
+    lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
+    try:
+        for erased in patterns:
+            present = [i not in erased for i in range(k + p)]
+            tb = [dev(x).reshape(n_elems, 2) for x in full]
+            for e in erased:
+                tb[e].fill_(0x5A)
+            r.reconstruct(list(zip(tb, present)))
+            torch.cuda.synchronize()
+            for i in erased:
+                assert (host(tb[i]).reshape(-1) == full[i]).all(), (erased, i)
+            # more than 4 data shards lost: syndrome rows past the 4th, NS = 8
+            if sum(1 for e in erased if e < k) > 4:
+                assert "ns8 pairs" in last_kernel(), (erased, last_kernel())
+        # reconstruct_batch: every stripe its own pattern, all with 8 sigma
+        # rows; shards with a 4 KiB remainder (one-wave kernel) and a tail
+        nbytes = 16384 * 3 + 4096 + 32
+        n_elems = nbytes // 2
+        full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+        oc.encode(full)
+        stripes = 6
+        flat = np.concatenate([np.stack(full)] * stripes)
+        d = dev(flat.reshape(-1)).reshape(stripes * (k + p), n_elems, 2)
+        pres = np.ones((stripes, k + p), bool)
+        for s_ in range(stripes):
+            pres[s_, patterns[s_]] = False
+            for e in patterns[s_]:
+                d[s_ * (k + p) + e].fill_(0x33)
+        r.reconstruct_batch(d.reshape(-1), n_elems, stripes, pres, data_only=False)
+        torch.cuda.synchronize()
+        got = host(d).reshape(stripes, k + p, nbytes)
+        for s_ in range(stripes):
+            for i in range(k + p):
+                assert (got[s_, i] == full[i]).all(), (s_, i)
+    finally:
         lib.rse_set_option(11, jp)
 
 

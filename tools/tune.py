@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--recon-depth", default="1",
                     help="comma list of RSE_OPT_RECON_DEPTH values (syndrome reconstruct: inputs "
                          "in flight per lane; compiled codecs)")
+    ap.add_argument("--ab", default="", metavar="KEY=V1,V2",
+                    help="one more interleaved dimension: RSE_OPT KEY set to each value")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="rse_set_option(KEY, VALUE) before the codec is created (repeatable)")
     args = ap.parse_args()
@@ -138,15 +140,22 @@ def main():
     vlist = ([int(x) for x in args.variant_list.split(",")] if args.variant_list
              else list(range(args.variants)))
     depths = [int(x) for x in args.recon_depth.split(",")]
-    configs = [(nt, gx, gy, var, bs, pat, mx, dp) for dp in depths for mx in mixes for pat in pats
-               for bs in bss for var in vlist for nt in nts for gx, gy in shapes]
+    ab_key, ab_vals = -1, [0]
+    if args.ab:
+        ab_key, vals = args.ab.split("=")
+        ab_key, ab_vals = int(ab_key), [int(x) for x in vals.split(",")]
+    configs = [(nt, gx, gy, var, bs, pat, mx, dp, ab) for ab in ab_vals for dp in depths
+               for mx in mixes for pat in pats for bs in bss for var in vlist for nt in nts
+               for gx, gy in shapes]
     res = {c: [] for c in configs}
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     op()
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for c in configs:
-            nt, gx, gy, var, bs, pat, mx, dp = c
+            nt, gx, gy, var, bs, pat, mx, dp, ab = c
+            if ab_key >= 0:
+                lib.rse_set_option(ab_key, ab)
             lib.rse_set_option(27, dp)
             lib.rse_set_option(17, mx)
             lib.rse_set_option(11, pat)
@@ -166,8 +175,9 @@ def main():
     what = f" erased {erased}" if args.op == "reconstruct" else ""
     size = f"{args.shard_kib} KiB" if args.shard_kib else f"{args.shard_mib} MiB"
     print(f"{args.op} GF(2^{args.field}) {k}+{p} x {size}, {S} stripes{what}; GB/s (1e9)")
-    for med, lo, hi, (nt, gx, gy, var, bs, pat, mx, dp) in rows:
-        print(f"  bitslice={bs} patterns={pat} mix={mx} depth={dp} variant={var} nt={nt} "
+    for med, lo, hi, (nt, gx, gy, var, bs, pat, mx, dp, ab) in rows:
+        abs_ = f"opt{ab_key}={ab} " if ab_key >= 0 else ""
+        print(f"  {abs_}bitslice={bs} patterns={pat} mix={mx} depth={dp} variant={var} nt={nt} "
               f"grid_x={gx:<5} stripes_in_flight={gy:<3}  median {med:7.1f}  [{lo:7.1f}, {hi:7.1f}]")
     b = rows[0][3]
     from reed_solomon_erasure.core import last_kernel
