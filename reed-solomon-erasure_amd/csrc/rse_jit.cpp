@@ -278,38 +278,51 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   int ns[5];
   const int n = recon_ns(p, ns);
   const int depth = (int)std::min<int64_t>(3, get_option(27));  // RSE_OPT_RECON_DEPTH
+  // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS): 8 KiB units, 3 waves
+  // per SIMD; the launchers' grid-stride loops cover either unit size
+  const bool pairs = get_option(28) != 0 && depth <= 1 && p >= 8;
   for (int q = 0; q < n; ++q) {
-    if (depth > 1)
-      std::snprintf(buf, sizeof buf,
-                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
-                    "    const rse::BsReconArgs a, uint64_t cps) {\n"
-                    "  rse::bitslice_recon_body_deep<rse::JitCode, true, %d, %d>(a, cps);\n}\n",
-                    ns[q] > 4 ? 2 : 3, ns[q], ns[q], depth);
-    else
-      std::snprintf(buf, sizeof buf,
-                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
-                    "    const rse::BsReconArgs a, uint64_t cps) {\n"
-                    "  rse::bitslice_recon_body<rse::JitCode, true, %d, rse::kReconMixDefault>(a, cps);\n}\n",
-                    ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
-    s += buf;
-    if (depth > 1)
-      std::snprintf(buf, sizeof buf,
-                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
-                    "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
-                    "  rse::bitslice_recon_desc_body_deep<rse::JitCode, true, %d, %d>(d, cps, n);\n}\n",
-                    ns[q] > 4 ? 2 : 3, ns[q], ns[q], depth);
-    else
-      std::snprintf(buf, sizeof buf,
-                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
-                    "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
-                    "  rse::bitslice_recon_desc_body<rse::JitCode, true, %d>(d, cps, n);\n}\n",
-                    ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
-    s += buf;
+    const int wpe = ns[q] > 4 ? 2 : 3;
+    if (pairs && ns[q] == 8) {
+      s += "extern \"C\" __global__ __launch_bounds__(256, 3) void rse_jit_recon8(\n"
+           "    const rse::BsReconArgs a, uint64_t cps) {\n"
+           "  rse::bitslice_recon_pair_body<rse::JitCode, true>(a, cps);\n}\n"
+           "extern \"C\" __global__ __launch_bounds__(256, 3) void rse_jit_recon_desc8(\n"
+           "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+           "  rse::bitslice_recon_desc_pair_body<rse::JitCode, true>(d, cps, n);\n}\n";
+    } else {
+      if (depth > 1)
+        std::snprintf(buf, sizeof buf,
+                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
+                      "    const rse::BsReconArgs a, uint64_t cps) {\n"
+                      "  rse::bitslice_recon_body_deep<rse::JitCode, true, %d, %d>(a, cps);\n}\n",
+                      wpe, ns[q], ns[q], depth);
+      else
+        std::snprintf(buf, sizeof buf,
+                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon%d(\n"
+                      "    const rse::BsReconArgs a, uint64_t cps) {\n"
+                      "  rse::bitslice_recon_body<rse::JitCode, true, %d, rse::kReconMixDefault>(a, cps);\n}\n",
+                      wpe, ns[q], ns[q]);
+      s += buf;
+      if (depth > 1)
+        std::snprintf(buf, sizeof buf,
+                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
+                      "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+                      "  rse::bitslice_recon_desc_body_deep<rse::JitCode, true, %d, %d>(d, cps, n);\n}\n",
+                      wpe, ns[q], ns[q], depth);
+      else
+        std::snprintf(buf, sizeof buf,
+                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc%d(\n"
+                      "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
+                      "  rse::bitslice_recon_desc_body<rse::JitCode, true, %d>(d, cps, n);\n}\n",
+                      wpe, ns[q], ns[q]);
+      s += buf;
+    }
     std::snprintf(buf, sizeof buf,
                   "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc4_%d(\n"
                   "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n, uint64_t base) {\n"
                   "  rse::bitslice_recon_desc_body_w4<rse::JitCode, true, %d>(d, cps, n, base);\n}\n",
-                  ns[q] > 4 ? 2 : 3, ns[q], ns[q]);
+                  wpe, ns[q], ns[q]);
     s += buf;
   }
   return s;
