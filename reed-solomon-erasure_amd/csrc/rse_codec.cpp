@@ -1561,38 +1561,43 @@ int rse_reconstruct_data_flat(const rse_codec* c, void* stripes, size_t shard_le
 // stripe on the device, then every stripe is coded from its descriptor.  No
 // host round trip and no decode-matrix cache: a batch of distinct patterns
 // costs one inversion per stripe on the GPU instead of one per stripe on the
-// host.  Validation happens up front on the host, so an error leaves every
-// stripe untouched.
+// host.  Validation happens up front (on the host, or for large batches in a
+// device pass before anything is coded), so an error leaves every stripe
+// untouched.
+// One stripe's validation (core.rs:747-772) and the counts the planners size
+// their work by: the highest sigma row + 1 it uses (its syndrome rows R and
+// missing parity rows), its missing data shards and its outputs.
+int batch_stripe(const uint8_t* pr, size_t k, size_t p, bool data_only, size_t shard_len,
+                 uint32_t* need, uint32_t* ne_out, uint32_t* nout) {
+  uint32_t ne = 0, nr = 0, nmp = 0, nd = 0;
+  for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0u : 1u;
+  size_t np = k - ne;
+  for (size_t r = 0; r < p; ++r) {
+    const bool here = pr[k + r] != 0;
+    np += here ? 1 : 0;
+    const bool syn = here && nr < ne;
+    nr += syn ? 1u : 0u;
+    if (!here && !data_only) ++nmp;
+    if (syn || (!here && !data_only)) nd = (uint32_t)r + 1;
+  }
+  if (np && shard_len == 0) return RSE_EMPTY_SHARD;
+  if (np < k) return RSE_TOO_FEW_SHARDS_PRESENT;
+  *need = nd;
+  *ne_out = ne;
+  *nout = ne + nmp;
+  return RSE_OK;
+}
+
+// Batches from this many stripes on are validated on the device (one
+// synchronisation instead of a host pass over every flag).
+constexpr size_t kDeviceScanStripes = 2048;
+
 int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
                           const uint8_t* present, int data_only, rse_stream_t stream) {
   RSE_ON_STREAM(stream);
   if (!c || !stripes || !present) return RSE_ERR_INVALID_ARGUMENT;
   if (n_stripes == 0) return RSE_OK;
   const size_t k = c->k, p = c->p, T = c->total, sb = shard_len * c->esize();
-  // One pass over the flags: validation (core.rs:747-772, stripe by stripe),
-  // and what the planners size their work by -- the sigma rows any stripe
-  // uses (its syndrome rows R and missing parity rows), the most missing
-  // data shards and the most outputs of a stripe.
-  uint32_t need = 0, e_cap = 0, nout_cap = 0;
-  for (size_t s = 0; s < n_stripes; ++s) {
-    const uint8_t* pr = present + s * T;
-    uint32_t ne = 0, nr = 0, nmp = 0;
-    for (size_t j = 0; j < k; ++j) ne += pr[j] ? 0u : 1u;
-    size_t np = k - ne;
-    for (size_t r = 0; r < p; ++r) {
-      const bool here = pr[k + r] != 0;
-      np += here ? 1 : 0;
-      const bool syn = here && nr < ne;
-      nr += syn ? 1u : 0u;
-      if (!here && !data_only) ++nmp;
-      if (syn || (!here && !data_only)) need = std::max<uint32_t>(need, (uint32_t)r + 1);
-    }
-    if (np && shard_len == 0) return RSE_EMPTY_SHARD;
-    if (np < k) return RSE_TOO_FEW_SHARDS_PRESENT;
-    e_cap = std::max(e_cap, ne);
-    nout_cap = std::max(nout_cap, ne + nmp);
-  }
-  if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
   uint8_t* base = static_cast<uint8_t*>(stripes);
   hipStream_t st = (hipStream_t)stream;
   // Runs of consecutive stripes with one erasure pattern (a lost disk: every
@@ -1600,7 +1605,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   // plan per run, and the pattern's own kernel once it has one (core.rs:
   // 697-731 caches the pattern; used twice, it is specialised), instead of a
   // plan and a mixing per stripe.  Used when the runs are long (at most one
-  // run per 16 stripes on average).
+  // run per 16 stripes on average).  Every run is validated before any runs.
   {
     std::vector<std::pair<size_t, size_t>> runs;  // [first, count)
     for (size_t s0 = 0; s0 < n_stripes;) {
@@ -1613,6 +1618,15 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     size_t covered = 0;
     for (auto& r : runs) covered += r.second;
     if (covered == n_stripes && runs.size() * 16 <= n_stripes) {
+      uint32_t nout_any = 0;
+      for (auto& r : runs) {
+        uint32_t nd, ne, no;
+        const int rc = batch_stripe(present + r.first * T, k, p, data_only != 0, shard_len, &nd,
+                                    &ne, &no);
+        if (rc) return rc;
+        nout_any |= no;
+      }
+      if (nout_any == 0) return RSE_OK;
       for (auto& r : runs) {
         const int rc = flat_reconstruct(c, base + r.first * T * sb, shard_len, r.second,
                                         present + r.first * T, data_only != 0, st);
@@ -1620,6 +1634,69 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       }
       return RSE_OK;
     }
+  }
+  // Validation of every stripe, and the largest counts any stripe needs.
+  // The flags go to the device once (the planners read them there); a large
+  // batch is validated there too, one lane per stripe.
+  uint32_t need = 0, e_cap = 0, nout_cap = 0;
+  uint8_t* dflags = nullptr;  // n_stripes * T flags, then the scan's 6 result words
+  const size_t fl_bytes = (n_stripes * T + 255) & ~size_t(255);
+  auto release = [&](hipError_t e) {  // drop dflags after the stream's work on it
+    if (dflags) (void)hipFreeAsync(dflags, st);
+    dflags = nullptr;
+    return e;
+  };
+  if (shard_len == 0) {  // stripe 0 fails: EmptyShard, or TooFewShardsPresent (none present)
+    uint32_t nd, ne, no;
+    return batch_stripe(present, k, p, data_only != 0, shard_len, &nd, &ne, &no);
+  }
+  const bool dev_scan = n_stripes >= kDeviceScanStripes;
+  if (!dev_scan) {
+    for (size_t s = 0; s < n_stripes; ++s) {
+      uint32_t nd, ne, no;
+      const int rc = batch_stripe(present + s * T, k, p, data_only != 0, shard_len, &nd, &ne, &no);
+      if (rc) return rc;
+      need = std::max(need, nd);
+      e_cap = std::max(e_cap, ne);
+      nout_cap = std::max(nout_cap, no);
+    }
+    if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
+  }
+  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&dflags), fl_bytes + 64, st));
+  {
+    hipError_t e = hipMemcpyAsync(dflags, present, n_stripes * T, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return dev_fail(release(e));
+  }
+  if (dev_scan) {
+    Lease lease;
+    hipError_t e = lease.acquire();
+    if (e == hipSuccess) e = lease_words(lease.get(), 6);
+    uint32_t* res = reinterpret_cast<uint32_t*>(dflags + fl_bytes);
+    const uint32_t init[6] = {0u, 0u, 0u, 0u, ~0u, ~0u};
+    if (e == hipSuccess) e = hipMemcpyAsync(res, init, sizeof init, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+      e = rse::launch_batch_scan(dflags, n_stripes, (uint32_t)k, (uint32_t)p, data_only ? 1u : 0u,
+                                 res, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(lease->wh, res, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(st);
+      return dev_fail(release(e));
+    }
+    const volatile uint32_t* w = lease->wh;
+    need = w[0];
+    e_cap = w[1];
+    nout_cap = w[2];
+    if (((uint64_t)w[5] << 32 | w[4]) != ~0ull) {  // too few shards in some stripe
+      (void)release(hipSuccess);
+      return RSE_TOO_FEW_SHARDS_PRESENT;
+    }
+  }
+  if (nout_cap == 0) {  // nothing this call rebuilds, in any stripe
+    (void)release(hipSuccess);
+    RSE_HIP(hipStreamSynchronize(st));
+    return RSE_OK;
   }
   const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
@@ -1632,28 +1709,32 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     want_bitslice(c, sb, false, n_stripes);
     if (need > 0) {
       const Rows& rows = prow;
-      const size_t rows_bytes = rows.c.size() * 2, pres_off = (rows_bytes + 255) & ~size_t(255);
-      const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
+      const size_t rows_bytes = rows.c.size() * 2, desc_off = (rows_bytes + 255) & ~size_t(255);
       uint8_t* ws = nullptr;
-      RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + n_stripes * sizeof(rse::BsReconArgs), st));
-      hipError_t e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
+      hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws),
+                                    desc_off + n_stripes * sizeof(rse::BsReconArgs), st);
+      if (e != hipSuccess) return dev_fail(release(e));
+      e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
       uint64_t bs_done = 0;
       if (e == hipSuccess)
         e = rse::launch_bitslice_recon_batch(
             c->field, (uint32_t)k, (uint32_t)p, rows.c.data(), reinterpret_cast<uint16_t*>(ws),
-            ws + pres_off, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
+            dflags, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
             reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
       hipError_t f = hipFreeAsync(ws, st);
       if (e == hipSuccess) e = f;
-      if (e == hipSuccess && bs_done == sb) e = hipStreamSynchronize(st);  // `prow` dies next
+      if (e == hipSuccess && bs_done == sb) {
+        e = release(hipSuccess);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);  // `prow` dies next
+      }
       if (e != hipSuccess) {
         (void)hipStreamSynchronize(st);
-        return dev_fail(e);
+        return dev_fail(release(e));
       }
       done = bs_done;
     } else {
+      (void)release(hipSuccess);
+      RSE_HIP(hipStreamSynchronize(st));
       return RSE_OK;  // nothing missing that this call rebuilds, in any stripe
     }
   }
@@ -1664,6 +1745,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   if (T > 0xffffu ||
       rse::recon_plan_lds((uint32_t)k, (uint32_t)T, e_cap, nout_cap) > rse::kReconPlanLdsMax) {
     // past the device planner's LDS budget: the host planner, stripe by stripe
+    (void)release(hipSuccess);
     std::vector<void*> ptrs(T);
     std::vector<size_t> lens(T, (sb - done) / c->esize());
     for (size_t s = 0; s < n_stripes; ++s) {
@@ -1682,26 +1764,27 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   const size_t per_stripe = n_ib * n_ob * sizeof(CodeArgs);
   // stripes per planning group: descriptors of at most 256 MiB at a time
   const size_t grp = std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per_stripe));
-  const size_t p_bytes = prow.c.size() * sizeof(uint16_t), pres_off = (p_bytes + 255) & ~size_t(255);
-  const size_t desc_off = (pres_off + n_stripes * T + 255) & ~size_t(255);
+  const size_t p_bytes = prow.c.size() * sizeof(uint16_t), desc_off = (p_bytes + 255) & ~size_t(255);
   uint8_t* ws = nullptr;
-  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + grp * per_stripe, st));
+  {
+    const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + grp * per_stripe, st);
+    if (e != hipSuccess) return dev_fail(release(e));
+  }
   hipError_t e = hipMemcpyAsync(ws, prow.c.data(), p_bytes, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(ws + pres_off, present, n_stripes * T, hipMemcpyHostToDevice, st);
   for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {
     const size_t ng = std::min(grp, n_stripes - g0);
-    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(ws),
-                               ws + pres_off + g0 * T, (uint32_t)k, (uint32_t)T,
-                               data_only ? 1u : 0u, e_cap, nout_cap, base + g0 * T * sb, sb, done,
-                               sb - done, (uint32_t)ng, reinterpret_cast<CodeArgs*>(ws + desc_off),
-                               st);
+    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(ws), dflags + g0 * T,
+                               (uint32_t)k, (uint32_t)T, data_only ? 1u : 0u, e_cap, nout_cap,
+                               base + g0 * T * sb, sb, done, sb - done, (uint32_t)ng,
+                               reinterpret_cast<CodeArgs*>(ws + desc_off), st);
   }
   const hipError_t f = hipFreeAsync(ws, st);
+  const hipError_t g = release(hipSuccess);
   // `prow` and the caller's flags must outlive the copies that read them
   const hipError_t y = hipStreamSynchronize(st);
   if (e != hipSuccess) return dev_fail(e);
   if (f != hipSuccess) return dev_fail(f);
+  if (g != hipSuccess) return dev_fail(g);
   RSE_HIP(y);
   return RSE_OK;
 }

@@ -1166,6 +1166,52 @@ size_t recon_plan_lds(uint32_t k, uint32_t T, uint32_t e_cap, uint32_t nout_cap)
          2 * ((size_t)k + T + 2 * (size_t)e_cap + 2 * (size_t)e_cap * e_cap + (size_t)nout_cap * e_cap);
 }
 
+// One lane per stripe: the per-stripe counts of the host loop in
+// rse_reconstruct_batch, reduced over the wave before one atomic each.
+__global__ __launch_bounds__(256) void batch_scan_kernel(const uint8_t* __restrict__ present,
+                                                         uint64_t n, uint32_t k, uint32_t p,
+                                                         uint32_t data_only, uint32_t* res) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t need = 0, ne = 0, nout = 0;
+  unsigned long long err = ~0ull;
+  if (s < n) {
+    const uint8_t* pr = present + s * (k + p);
+    for (uint32_t j = 0; j < k; ++j) ne += pr[j] ? 0u : 1u;
+    uint32_t np = k - ne, nr = 0, nmp = 0;
+    for (uint32_t r = 0; r < p; ++r) {
+      const bool here = pr[k + r] != 0;
+      np += here ? 1u : 0u;
+      const bool syn = here && nr < ne;
+      nr += syn ? 1u : 0u;
+      if (!here && !data_only) ++nmp;
+      if (syn || (!here && !data_only)) need = r + 1;
+    }
+    nout = ne + nmp;
+    if (np < k) err = (unsigned long long)s * 2 + 1;
+  }
+  for (int m = 32; m > 0; m >>= 1) {
+    need = max(need, (uint32_t)__shfl_xor((int)need, m));
+    ne = max(ne, (uint32_t)__shfl_xor((int)ne, m));
+    nout = max(nout, (uint32_t)__shfl_xor((int)nout, m));
+    const unsigned long long o = __shfl_xor(err, m);
+    err = o < err ? o : err;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (need) atomicMax(&res[0], need);
+    if (ne) atomicMax(&res[1], ne);
+    if (nout) atomicMax(&res[2], nout);
+    if (err != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(res + 4), err);
+  }
+}
+
+hipError_t launch_batch_scan(const uint8_t* d_present, uint64_t n_stripes, uint32_t k, uint32_t p,
+                             uint32_t data_only, uint32_t* d_res, hipStream_t stream) {
+  if (n_stripes == 0) return hipSuccess;
+  hipLaunchKernelGGL(batch_scan_kernel, dim3((uint32_t)((n_stripes + 255) / 256)), dim3(256), 0,
+                     stream, d_present, n_stripes, k, p, data_only, d_res);
+  return hipGetLastError();
+}
+
 hipError_t launch_recon_plan(int field, const uint16_t* d_parity, const uint8_t* d_present,
                              uint32_t k, uint32_t T, uint32_t data_only, uint32_t e_cap,
                              uint32_t nout_cap, uint8_t* base, uint64_t shard_bytes, uint64_t off,

@@ -203,6 +203,13 @@ hipError_t launch_code(int field, const CodeArgs& args, hipStream_t stream);
 // recon_plan_lds(...) <= kReconPlanLdsMax.
 constexpr size_t kReconPlanLdsMax = 65536;
 size_t recon_plan_lds(uint32_t k, uint32_t T, uint32_t e_cap, uint32_t nout_cap);
+// rse_reconstruct_batch's validation of many stripes on the device
+// (core.rs:747-772 per stripe): d_res[0..2] = max over stripes of `need` (the
+// highest sigma row + 1), e (missing data) and outputs; d_res[4..5] = the
+// 64-bit (first stripe with too few shards present) * 2 + 1, ~0 if none.
+// d_res (8-byte aligned) must hold zeros in words 0..2 and all ones in 4..5.
+hipError_t launch_batch_scan(const uint8_t* d_present, uint64_t n_stripes, uint32_t k, uint32_t p,
+                             uint32_t data_only, uint32_t* d_res, hipStream_t stream);
 hipError_t launch_recon_plan(int field, const uint16_t* d_parity, const uint8_t* d_present,
                              uint32_t k, uint32_t T, uint32_t data_only, uint32_t e_cap,
                              uint32_t nout_cap, uint8_t* base, uint64_t shard_bytes, uint64_t off,

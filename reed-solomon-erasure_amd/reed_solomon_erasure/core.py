@@ -294,7 +294,7 @@ class ReedSolomon:
         if flags.shape != (n_stripes, T):
             raise RSError(Error.InvalidShardFlags)
         _check_flat(stripes, shard_len, n_stripes, T, self.field)
-        pres = flags.astype(np.uint8)
+        pres = flags.view(np.uint8)  # bool is one byte, 0 or 1: no copy
         _raise(_lib.rse_reconstruct_batch(
             self._h, _dev(stripes), shard_len, n_stripes,
             pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1 if data_only else 0,
@@ -421,7 +421,7 @@ class ReedSolomon:
         if flags.shape != (n_stripes, T):
             raise RSError(Error.InvalidShardFlags)
         _check_host_flat(stripes, shard_len, n_stripes, T, self.field)
-        pres = flags.astype(np.uint8)
+        pres = flags.view(np.uint8)  # bool is one byte, 0 or 1: no copy
         _raise(_lib.rse_reconstruct_host_batch(
             self._h, _host_ptr(stripes), shard_len, n_stripes,
             pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 1 if data_only else 0, _stream()))
