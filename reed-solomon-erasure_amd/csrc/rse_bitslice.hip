@@ -557,7 +557,8 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
     if (slot == 3 && sh.rec_pair && get_option(28) && mix >= kReconMixHorner && depth == 1) {
       note_kernel("bitslice-recon gf%d %u+%u ns8 pairs", field, k, p);
-      uint64_t gp = grid > 0 ? (uint64_t)grid : 8192u;
+      // (tools/tune.py: 32768 workgroups 4.24 TB/s, 8192 4.16, 4096 4.10 at 8 lost)
+      uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u;
       if (gp > 2 * total) gp = 2 * total;
       if (gp > 0x7fffffffu) gp = 0x7fffffffu;
       hipLaunchKernelGGL(sh.rec_pair, dim3((uint32_t)gp), dim3(kBsBlock), 0, stream, a, cps);
@@ -644,7 +645,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   if (e != hipSuccess) return e;
   const int64_t grid = get_option(2);
   auto grid_for = [&](uint64_t steps) {
-    uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : pairs ? 32768u : 8192u;
     if (gx > steps) gx = steps;
     return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
   };

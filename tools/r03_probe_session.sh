@@ -14,5 +14,5 @@ bash tools/gpu_session.sh \
  "r8_grid:300:$T16 --op reconstruct --erase 0,1,2,3,4,5,6,7 --shapes 4096:0,8192:0,16384:0,32768:0 --recon-mix 3 --ab 28=1" \
  "r4:300:$T16 --op reconstruct --erase 0,1,2,3 --shapes 0:0 --recon-mix 3" \
  "batch_trace:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/batch_trace -o b -- python3 tools/tune.py --rounds 2 --nt-only --shapes 0:0 --field 16 --k 20 --p 8 --shard-kib 4 --stripes 65536 --op batch --erase 0,1,2,3" \
- "capi:120:./tools/bin/capi_latency" \
+ "capi:180:hipcc --offload-arch=gfx950 -O2 -I include tools/capi_latency.cpp -L reed-solomon-erasure_amd/reed_solomon_erasure -lrse_hip -Wl,-rpath,$PWD/reed-solomon-erasure_amd/reed_solomon_erasure -o /tmp/capi_latency && /tmp/capi_latency" \
  "clock:900:bash tools/clock_session.sh"
