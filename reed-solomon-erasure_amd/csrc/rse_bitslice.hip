@@ -187,17 +187,18 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
   bitslice_recon_desc_body_deep<C, true, NS, D>(descs, chunks_per_stripe, n_stripes);
 }
 
-// 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD).
-template <class C>
-__global__ __launch_bounds__(kBsBlock, 3) void bitslice_recon_pair_kernel(
+// 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD),
+// P pairs per workgroup.
+template <class C, int P>
+__global__ __launch_bounds__(128 * P, 3) void bitslice_recon_pair_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_pair_body<C, true>(a, chunks_per_stripe);
+  bitslice_recon_pair_body<C, true, P>(a, chunks_per_stripe);
 }
 
-template <class C>
-__global__ __launch_bounds__(kBsBlock, 3) void bitslice_recon_desc_pair_kernel(
+template <class C, int P>
+__global__ __launch_bounds__(128 * P, 3) void bitslice_recon_desc_pair_kernel(
     const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
-  bitslice_recon_desc_pair_body<C, true>(descs, chunks_per_stripe, n_stripes);
+  bitslice_recon_desc_pair_body<C, true, P>(descs, chunks_per_stripe, n_stripes);
 }
 
 // ------------------------------------------------- batched reconstruct planner
@@ -364,8 +365,8 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
-  BsRecFn rec_pair;            // NS = 8 on wave pairs (nullptr below 8 parity rows)
-  BsDescFn rec_desc_pair;
+  BsRecFn rec_pair[2];         // NS = 8 on wave pairs, [pairs per workgroup - 1]
+  BsDescFn rec_desc_pair[2];   // (nullptr below 8 parity rows)
 };
 
 template <class C, int NS, int MIX>
@@ -388,14 +389,14 @@ constexpr BsRecFn rec_deep_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_deep_kernel<C, NS, D>;
   else return nullptr;
 }
-template <class C>
+template <class C, int P>
 constexpr BsRecFn rec_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C>;
+  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C, P>;
   else return nullptr;
 }
-template <class C>
+template <class C, int P>
 constexpr BsDescFn rec_desc_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C>;
+  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C, P>;
   else return nullptr;
 }
 template <class C, int NS, int D>
@@ -432,7 +433,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
      rec_desc_deep_fn<C, 8, 2>()},                                                     \
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
-   rec_pair_fn<C>(), rec_desc_pair_fn<C>()}
+   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>()},                                        \
+   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -528,6 +530,13 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   return hipSuccess;
 }
 
+// RSE_OPT_RECON_PAIRS: 0 off, 1 two pairs per workgroup, 2 one pair per
+// workgroup; returns pairs per workgroup (0: off).
+int pair_groups() {
+  const int64_t o = get_option(28);
+  return o == 0 ? 0 : o == 2 ? 1 : 2;
+}
+
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
                                  bool* handled) {
@@ -555,13 +564,15 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const int depth = mix == kReconMixHorner ? (int)get_option(27) : 1;  // RSE_OPT_RECON_DEPTH
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
-    if (slot == 3 && sh.rec_pair && get_option(28) && mix >= kReconMixHorner && depth == 1) {
-      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs", field, k, p);
-      // (tools/tune.py: 32768 workgroups 4.24 TB/s, 8192 4.16, 4096 4.10 at 8 lost)
-      uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u;
-      if (gp > 2 * total) gp = 2 * total;
+    const int np = pair_groups();
+    if (slot == 3 && np && sh.rec_pair[np - 1] && mix >= kReconMixHorner && depth == 1) {
+      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d", field, k, p, np);
+      // (tools/tune.py: 32768 workgroups 4.24 TB/s, 8192 4.16, 4096 4.10 at 8 lost, 2 pairs)
+      uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);
+      const uint64_t units = total * (4 / np);
+      if (gp > units) gp = units;
       if (gp > 0x7fffffffu) gp = 0x7fffffffu;
-      hipLaunchKernelGGL(sh.rec_pair, dim3((uint32_t)gp), dim3(kBsBlock), 0, stream, a, cps);
+      hipLaunchKernelGGL(sh.rec_pair[np - 1], dim3((uint32_t)gp), dim3(128 * np), 0, stream, a, cps);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       count_bitslice_launch();
@@ -620,8 +631,8 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       if (sh.rec_desc[q] && (1u << q) >= need) {
         sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
         sfn4 = sh.rec_desc4[q];
-        if (q == 3 && sh.rec_desc_pair && get_option(28) && depth == 1) {
-          sfn = sh.rec_desc_pair;  // 8 sigma rows on wave pairs (8 KiB units)
+        if (q == 3 && pair_groups() && sh.rec_desc_pair[pair_groups() - 1] && depth == 1) {
+          sfn = sh.rec_desc_pair[pair_groups() - 1];  // 8 sigma rows on wave pairs
           pairs = true;
         }
       }
@@ -645,7 +656,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   if (e != hipSuccess) return e;
   const int64_t grid = get_option(2);
   auto grid_for = [&](uint64_t steps) {
-    uint64_t gx = grid > 0 ? (uint64_t)grid : pairs ? 32768u : 8192u;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : pairs ? 32768u * (2 / pair_groups()) : 8192u;
     if (gx > steps) gx = steps;
     return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
   };
@@ -653,9 +664,10 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
   uint64_t cps4 = (shard_bytes - cps * kBsChunk) / 4096u, base4 = cps * kBsChunk;
   if (cps) {
-    const uint64_t gx = grid_for(cps * ns * (pairs ? 2 : 1));
+    const int np = pairs ? pair_groups() : 2;
+    const uint64_t gx = grid_for(cps * ns * (pairs ? 4 / np : 1));
     if (sfn) {
-      hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,
+      hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(pairs ? 128 * np : kBsBlock), 0, stream,
                          (const BsReconArgs*)d_descs, cps, ns);
       e = hipGetLastError();
     } else {

@@ -1400,10 +1400,12 @@ __device__ __forceinline__ void bitslice_recon_desc_body_w4(const BsReconArgs* _
 //    step mask per step, 19 ops).  A wave computes its partner's outputs'
 //    partials into LDS, then its own, adds the partner's, converts, un-slices
 //    and stores (outputs split in halves).
-// A workgroup's 4 waves are 2 pairs on the two 4 KiB halves of an 8 KiB unit.
+// A workgroup of P pairs (2P waves) takes a unit of P 4 KiB columns; the
+// barriers then sync P pairs (P = 1: only the pair itself).
 constexpr int kPairRows = 4;
+template <int P>
 struct PairLds {
-  u32x4 v[2][2][2][4][64];  // [buffer][pair][role][vector][lane]: 32 KiB
+  u32x4 v[2][P][2][4][64];  // [buffer][pair][role][vector][lane]: 16 KiB per pair
 };
 
 template <class C, int I, int R0, int... OP>
@@ -1463,7 +1465,7 @@ __device__ __forceinline__ bool pair_prefetch(u32x4 (&nxt)[4], const BsReconArgs
 }
 
 // Data rounds T.. : indices 2T (role 0) and 2T + 1 (role 1).
-template <class C, bool NT, int H, int T>
+template <class C, bool NT, int H, int T, int P>
 __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4 (&cur)[4],
                                           const BsReconArgs& a, uint64_t own, uint32_t present,
                                           uint64_t off, u32x4 (*mine)[64], u32x4 (*theirs)[64],
@@ -1474,8 +1476,9 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
     const bool has_oth = JP < C::k && ((present >> JP) & 1u);
     if (has_own || has_oth) {  // workgroup-uniform (one pattern per unit)
       uint32_t pl[16];
-      u32x4* const wr = mine[buf * 16];    // [buf][pair][role] flattened by the caller
-      const u32x4* const rd = theirs[buf * 16];
+      // buffer `buf` of this wave's / the partner's slot: [buf][pair][role][4][64]
+      u32x4* const wr = mine[buf * (P * 2 * 4)];
+      const u32x4* const rd = theirs[buf * (P * 2 * 4)];
       if (has_own) {
         u32x4 nxt[4];
         const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
@@ -1507,7 +1510,7 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
       for (int q = 0; q < kPairRows * 16; ++q) asm volatile("" : "+v"(acc[q]));
       buf ^= 1u;
     }
-    pair_data<C, NT, H, T + 1>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+    pair_data<C, NT, H, T + 1, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
   }
 }
 
@@ -1542,9 +1545,9 @@ __device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
 // One 8 KiB unit of one stripe for wave H of pair `pair`: off = the lane's
 // byte offset (pair's 4 KiB half + lane * 16) from the argument block's shard
 // pointers.
-template <class C, bool NT, int H>
+template <class C, bool NT, int H, int P>
 __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t off,
-                                                PairLds& lds, uint32_t pair, uint32_t lane) {
+                                                PairLds<P>& lds, uint32_t pair, uint32_t lane) {
   using F = typename C::Field;
   constexpr int R0 = H * kPairRows;
   const uint32_t present = a.present;
@@ -1563,7 +1566,7 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
-  pair_data<C, NT, H, 0>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  pair_data<C, NT, H, 0, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
   // own syndrome rows: s_r = sigma_r ^ parity_r
 #pragma unroll
   for (int i = 0; i < kPairRows; ++i) {
@@ -1641,39 +1644,40 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
   }
 }
 
-// Units of 8 KiB: unit u of a stripe with cps 16 KiB chunks covers bytes
-// [u * 8192, u * 8192 + 8192); pair p its half p.
-template <class C, bool NT>
+// Units of P 4 KiB columns: unit u of a stripe (cps 16 KiB chunks) covers
+// bytes [u * 4096P, (u + 1) * 4096P); pair q its column q.  Workgroups of
+// 128P lanes.
+template <class C, bool NT, int P>
 __device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
                                                          uint64_t chunks_per_stripe) {
-  __shared__ PairLds lds;
-  const uint64_t upc = chunks_per_stripe * 2, total = upc * a.n_stripes;
+  __shared__ PairLds<P> lds;
+  const uint64_t upc = chunks_per_stripe * (4 / P), total = upc * a.n_stripes;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
   for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
     const uint64_t stripe = u / upc, sub = u - stripe * upc;
-    const uint64_t off = stripe * a.stripe_stride + sub * 8192u + pair * 4096u + lane * 16u;
-    if (wave & 1u) recon_pair_unit<C, NT, 1>(a, off, lds, pair, lane);
-    else recon_pair_unit<C, NT, 0>(a, off, lds, pair, lane);
+    const uint64_t off = stripe * a.stripe_stride + sub * (4096u * P) + pair * 4096u + lane * 16u;
+    if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane);
+    else recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane);
   }
 }
 
 // The same over per-stripe argument blocks (rse_reconstruct_batch).
-template <class C, bool NT>
+template <class C, bool NT, int P>
 __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs* __restrict__ descs,
                                                               uint64_t chunks_per_stripe,
                                                               uint64_t n_stripes) {
-  __shared__ PairLds lds;
-  const uint64_t upc = chunks_per_stripe * 2, total = upc * n_stripes;
+  __shared__ PairLds<P> lds;
+  const uint64_t upc = chunks_per_stripe * (4 / P), total = upc * n_stripes;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
   for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
     const uint64_t stripe = u / upc, sub = u - stripe * upc;
     const BsReconArgs& a = desc_at(descs, stripe);
     if (a.n_out == 0) continue;  // workgroup-uniform
-    const uint64_t off = sub * 8192u + pair * 4096u + lane * 16u;
-    if (wave & 1u) recon_pair_unit<C, NT, 1>(a, off, lds, pair, lane);
-    else recon_pair_unit<C, NT, 0>(a, off, lds, pair, lane);
+    const uint64_t off = sub * (4096u * P) + pair * 4096u + lane * 16u;
+    if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane);
+    else recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane);
   }
 }
 

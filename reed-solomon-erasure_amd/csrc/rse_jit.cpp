@@ -280,16 +280,17 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   const int depth = (int)std::min<int64_t>(3, get_option(27));  // RSE_OPT_RECON_DEPTH
   // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS): 8 KiB units, 3 waves
   // per SIMD; the launchers' grid-stride loops cover either unit size
+  // (two pairs per 256-lane workgroup: the launchers' block size)
   const bool pairs = get_option(28) != 0 && depth <= 1 && p >= 8;
   for (int q = 0; q < n; ++q) {
     const int wpe = ns[q] > 4 ? 2 : 3;
     if (pairs && ns[q] == 8) {
       s += "extern \"C\" __global__ __launch_bounds__(256, 3) void rse_jit_recon8(\n"
            "    const rse::BsReconArgs a, uint64_t cps) {\n"
-           "  rse::bitslice_recon_pair_body<rse::JitCode, true>(a, cps);\n}\n"
+           "  rse::bitslice_recon_pair_body<rse::JitCode, true, 2>(a, cps);\n}\n"
            "extern \"C\" __global__ __launch_bounds__(256, 3) void rse_jit_recon_desc8(\n"
            "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n) {\n"
-           "  rse::bitslice_recon_desc_pair_body<rse::JitCode, true>(d, cps, n);\n}\n";
+           "  rse::bitslice_recon_desc_pair_body<rse::JitCode, true, 2>(d, cps, n);\n}\n";
     } else {
       if (depth > 1)
         std::snprintf(buf, sizeof buf,

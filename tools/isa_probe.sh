@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void rprobe(const BsRecon
 }
 template <class C>
 __global__ __launch_bounds__(kBsBlock, 3) void pprobe(const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_pair_body<C, true>(a, chunks_per_stripe);
+  bitslice_recon_pair_body<C, true, 2>(a, chunks_per_stripe);
 }
 }  // namespace
 void* probe_fns[] = {(void*)probe_kernel<Bs16_20_8, false>, (void*)probe_kernel<Bs8_10_4, true>, (void*)rprobe<Bs16_20_8, 8>, (void*)rprobe<Bs16_20_8, 4>, (void*)rprobe<Bs8_10_4, 4>, (void*)pprobe<Bs16_20_8>};

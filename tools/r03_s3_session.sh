@@ -14,9 +14,10 @@ bash tools/gpu_session.sh \
  "b4k_e4:300:$T16 --shard-kib 4 --stripes 65536 --op batch --erase 0,1,2,3" \
  "b4k_e8:300:$T16 --shard-kib 4 --stripes 65536 --op batch --erase 0,1,2,3,4,5,6,7" \
  "b4m_e4:300:$T16 --shard-mib 4 --stripes 128 --op batch --erase 0,1,2,3" \
- "b4m_e8:300:$T16 --shard-mib 4 --stripes 128 --op batch --erase 0,1,2,3,4,5,6,7 --ab 28=0,1" \
- "r8:300:$T16 --shard-mib 4 --stripes 128 --op reconstruct --patterns 0 --erase 0,1,2,3,4,5,6,7 --recon-mix 3 --ab 28=0,1" \
+ "b4m_e8:300:$T16 --shard-mib 4 --stripes 128 --op batch --erase 0,1,2,3,4,5,6,7 --ab 28=0,1,2" \
+ "r8:300:$T16 --shard-mib 4 --stripes 128 --op reconstruct --patterns 0 --erase 0,1,2,3,4,5,6,7 --recon-mix 3 --ab 28=0,1,2" \
  "trace_r8:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_r8 -o r -- $R8" \
  "trace_b4k:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_b4k -o b -- python3 tools/tune.py --rounds 2 --nt-only --shapes 0:0 --field 16 --k 20 --p 8 --shard-kib 4 --stripes 65536 --op batch --erase 0,1,2,3" \
  "pmc_pairs:500:bash tools/pmc_kernel_session.sh pairs8 bitslice_recon_pair_kernel $R8" \
+ "pmc_pairs1:500:bash tools/pmc_kernel_session.sh pairs8p1 bitslice_recon_pair_kernel $R8 --set 28=2" \
  "pmc_onewave:500:bash tools/pmc_kernel_session.sh onewave8 bitslice_recon_kernel $R8 --set 28=0"
