@@ -701,9 +701,12 @@ int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKin
   Worker& w = worker();
   std::lock_guard<std::mutex> g(g_mu);
   if (find_locked(field, k, p, rows, k, kind)) return 1;
+  // decode patterns are an optimisation: never queue without bound -- except
+  // under RSE_OPT_JIT 2, where the caller waits for this very build
   if (kind == kJitPattern &&
-      (g_patterns >= kMaxPatterns || g_jobs[kEnc].size() >= kMaxPendingPatternJobs))
-    return 0;  // decode patterns are an optimisation: never queue without bound
+      (g_patterns >= kMaxPatterns ||
+       (get_option(9) < 2 && g_jobs[kEnc].size() >= kMaxPendingPatternJobs)))
+    return 0;
   if ((kind == kJitBlock || kind == kJitBlockAcc) && g_blocks >= kMaxBlocks) return 0;
   add_locked(field, k, p, rows, k, kind);
   w.start();
