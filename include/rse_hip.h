@@ -340,8 +340,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_RECON_DEPTH 27       /* syndrome reconstruct: inputs in flight per lane (1..4) */
 #define RSE_OPT_RECON_PAIRS 28       /* syndrome reconstruct at 8 sigma rows on wave pairs (4 rows
                                         each, planes shared through LDS, 3 waves per SIMD): 1
-                                        (default) two pairs per workgroup, 2 one pair per workgroup
-                                        (compiled codecs); 0: one wave holds all 8 rows */
+                                        (default) one pair per workgroup, 2 two pairs per workgroup
+                                        (compiled codecs; run-time ones use two); 0: one wave holds
+                                        all 8 rows */
 #define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch
                                        planned on the host (a batch past the device planner's LDS
                                        budget: more than 8192 shards or very many erasures) */

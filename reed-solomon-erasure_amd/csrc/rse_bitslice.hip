@@ -530,11 +530,13 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   return hipSuccess;
 }
 
-// RSE_OPT_RECON_PAIRS: 0 off, 1 two pairs per workgroup, 2 one pair per
-// workgroup; returns pairs per workgroup (0: off).
+// RSE_OPT_RECON_PAIRS: 0 off, 1 one pair per workgroup (its barriers sync
+// the pair only: 4.26 TB/s at 8 lost against 4.18 for two pairs per
+// workgroup, profiles/r03/s3/r8.log), 2 two pairs; returns pairs per
+// workgroup (0: off).
 int pair_groups() {
   const int64_t o = get_option(28);
-  return o == 0 ? 0 : o == 2 ? 1 : 2;
+  return o == 0 ? 0 : o == 2 ? 2 : 1;
 }
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
@@ -567,7 +569,8 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const int np = pair_groups();
     if (slot == 3 && np && sh.rec_pair[np - 1] && mix >= kReconMixHorner && depth == 1) {
       note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d", field, k, p, np);
-      // (tools/tune.py: 32768 workgroups 4.24 TB/s, 8192 4.16, 4096 4.10 at 8 lost, 2 pairs)
+      // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
+      // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
       uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);
       const uint64_t units = total * (4 / np);
       if (gp > units) gp = units;

@@ -725,6 +725,7 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
     names = {0: "mix-tables", 1: "mix-chain", 2: "mix-horner ", 3: "mix-horner4"}
     jp = lib.rse_get_option(11)
     lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
+    pairs = lib.rse_get_option(28)
     lib.rse_set_option(28, 0)  # 8 sigma rows in one wave too (pairs: test_reconstruct_wave_pairs)
     try:
         for mix in (3, 2, 1, 0):
@@ -743,10 +744,11 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
     finally:
         lib.rse_set_option(17, 3)
         lib.rse_set_option(11, jp)
-        lib.rse_set_option(28, 1)
+        lib.rse_set_option(28, pairs)
 
 
-def test_reconstruct_wave_pairs(R):
+@pytest.mark.parametrize("pairs", [1, 2])  # RSE_OPT_RECON_PAIRS: pairs per workgroup
+def test_reconstruct_wave_pairs(R, pairs):
     """GF(2^16) 20+8 syndrome reconstruct at 8 sigma rows on wave pairs
     (RSE_OPT_RECON_PAIRS, the default): each wave of a pair holds 4 syndrome
     rows, data planes are exchanged through LDS and the outputs' partial sums
@@ -773,8 +775,9 @@ def test_reconstruct_wave_pairs(R):
                 [0, 1, 2, 3, 4, 5, 6, k + 7]]
     patterns += [sorted(rng.choice(k + p, int(rng.integers(5, p + 1)), replace=False).tolist())
                  for _ in range(8)]
-    jp = lib.rse_get_option(11)
+    jp, pp = lib.rse_get_option(11), lib.rse_get_option(28)
     lib.rse_set_option(11, 0)  # no decode-pattern kernels: every use is a first use
+    lib.rse_set_option(28, pairs)
     try:
         for erased in patterns:
             present = [i not in erased for i in range(k + p)]
@@ -787,7 +790,7 @@ def test_reconstruct_wave_pairs(R):
                 assert (host(tb[i]).reshape(-1) == full[i]).all(), (erased, i)
             # more than 4 data shards lost: syndrome rows past the 4th, NS = 8
             if sum(1 for e in erased if e < k) > 4:
-                assert "ns8 pairs" in last_kernel(), (erased, last_kernel())
+                assert f"ns8 pairs{pairs}" in last_kernel(), (erased, last_kernel())
         # reconstruct_batch: every stripe its own pattern, all with 8 sigma
         # rows; shards with a 4 KiB remainder (one-wave kernel) and a tail
         nbytes = 16384 * 3 + 4096 + 32
@@ -810,6 +813,7 @@ def test_reconstruct_wave_pairs(R):
                 assert (got[s_, i] == full[i]).all(), (s_, i)
     finally:
         lib.rse_set_option(11, jp)
+        lib.rse_set_option(28, pp)
 
 
 JIT_CODECS = [(8, 12, 4), (8, 6, 3), (8, 4, 2), (8, 32, 8), (8, 1, 1), (8, 17, 5),

@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 T16="python3 -u tools/tune.py --rounds 3 --nt-only --field 16 --k 20 --p 8 --shapes 0:0"
 R8="python3 tools/tune.py --rounds 1 --nt-only --shapes 0:0 --field 16 --k 20 --p 8 --shard-mib 4 --stripes 128 --op reconstruct --erase 0,1,2,3,4,5,6,7 --patterns 0 --recon-mix 3"
+bash tools/gpu_session.sh "dbg:120:python3 -u tools/dbg_runs.py"
 bash tools/gpu_session.sh \
  "pytest_batch:600:python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_host_paths.py -m gpu -k 'batch or wave_pairs or every_mixing'" || exit $?
 grep -q " passed" gpurun_out/pytest_batch.log && ! grep -q -E "[0-9]+ failed" gpurun_out/pytest_batch.log || exit 1
