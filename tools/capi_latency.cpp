@@ -7,12 +7,18 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "rse_hip.h"
 
-int main() {
+int main(int argc, char** argv) {
   const size_t k = 10, p = 4, L = 16u << 20, S = 8;
+  if (argc > 1) {  // workgroups of the bit-sliced launches (RSE_OPT_GRID_X; 0 = default)
+    const long g = std::atol(argv[1]);
+    if (rse_set_option(RSE_OPT_GRID_X, g)) return 7;
+    std::printf("grid %ld\n", g);
+  }
   rse_codec* c = nullptr;
   if (rse_codec_new(RSE_FIELD_GF8, k, p, &c)) return 1;
   uint8_t* buf = nullptr;
