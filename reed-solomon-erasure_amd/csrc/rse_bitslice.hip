@@ -189,16 +189,17 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
 
 // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD),
 // P pairs per workgroup.
-template <class C, int P>
+// PF: the next unit's first input loaded during the mixing (A/B, option 28 = 3).
+template <class C, int P, bool PF = false>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_pair_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_pair_body<C, true, P>(a, chunks_per_stripe);
+  bitslice_recon_pair_body<C, true, P, PF>(a, chunks_per_stripe);
 }
 
-template <class C, int P>
+template <class C, int P, bool PF = false>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_desc_pair_kernel(
     const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
-  bitslice_recon_desc_pair_body<C, true, P>(descs, chunks_per_stripe, n_stripes);
+  bitslice_recon_desc_pair_body<C, true, P, PF>(descs, chunks_per_stripe, n_stripes);
 }
 
 // ------------------------------------------------- batched reconstruct planner
@@ -365,8 +366,8 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
-  BsRecFn rec_pair[2];         // NS = 8 on wave pairs, [pairs per workgroup - 1]
-  BsDescFn rec_desc_pair[2];   // (nullptr below 8 parity rows)
+  BsRecFn rec_pair[3];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
+  BsDescFn rec_desc_pair[3];   // pair with the next unit prefetched (nullptr below 8 rows)
 };
 
 template <class C, int NS, int MIX>
@@ -389,14 +390,14 @@ constexpr BsRecFn rec_deep_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_deep_kernel<C, NS, D>;
   else return nullptr;
 }
-template <class C, int P>
+template <class C, int P, bool PF = false>
 constexpr BsRecFn rec_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C, P>;
+  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C, P, PF>;
   else return nullptr;
 }
-template <class C, int P>
+template <class C, int P, bool PF = false>
 constexpr BsDescFn rec_desc_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C, P>;
+  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C, P, PF>;
   else return nullptr;
 }
 template <class C, int NS, int D>
@@ -433,8 +434,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
      rec_desc_deep_fn<C, 8, 2>()},                                                     \
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
-   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>()},                                        \
-   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>()}}
+   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>()},            \
+   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>(), rec_desc_pair_fn<C, 1, true>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -538,6 +539,11 @@ int pair_groups() {
   const int64_t o = get_option(28);
   return o == 0 ? 0 : o == 2 ? 2 : 1;
 }
+// index into BsShape::rec_pair / rec_desc_pair (option 28 = 3: prefetching variant)
+int pair_slot() {
+  const int64_t o = get_option(28);
+  return o == 3 ? 2 : pair_groups() - 1;
+}
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
@@ -567,7 +573,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
     const int np = pair_groups();
-    if (slot == 3 && np && sh.rec_pair[np - 1] && mix >= kReconMixHorner && depth == 1) {
+    if (slot == 3 && np && sh.rec_pair[pair_slot()] && mix >= kReconMixHorner && depth == 1) {
       note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d", field, k, p, np);
       // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
       // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
@@ -575,7 +581,8 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
       const uint64_t units = total * (4 / np);
       if (gp > units) gp = units;
       if (gp > 0x7fffffffu) gp = 0x7fffffffu;
-      hipLaunchKernelGGL(sh.rec_pair[np - 1], dim3((uint32_t)gp), dim3(128 * np), 0, stream, a, cps);
+      hipLaunchKernelGGL(sh.rec_pair[pair_slot()], dim3((uint32_t)gp), dim3(128 * np), 0, stream,
+                         a, cps);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       count_bitslice_launch();
@@ -634,8 +641,8 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       if (sh.rec_desc[q] && (1u << q) >= need) {
         sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
         sfn4 = sh.rec_desc4[q];
-        if (q == 3 && pair_groups() && sh.rec_desc_pair[pair_groups() - 1] && depth == 1) {
-          sfn = sh.rec_desc_pair[pair_groups() - 1];  // 8 sigma rows on wave pairs
+        if (q == 3 && pair_groups() && sh.rec_desc_pair[pair_slot()] && depth == 1) {
+          sfn = sh.rec_desc_pair[pair_slot()];  // 8 sigma rows on wave pairs
           pairs = true;
         }
       }

@@ -1542,12 +1542,16 @@ __device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
     }
 }
 
-// One 8 KiB unit of one stripe for wave H of pair `pair`: off = the lane's
-// byte offset (pair's 4 KiB half + lane * 16) from the argument block's shard
-// pointers.
+// One unit of one stripe for wave H of pair `pair`: off = the lane's byte
+// offset (the pair's 4 KiB column + lane * 16) from the argument block's shard
+// pointers.  cur holds the unit's first own input if `primed`; with next_off
+// != ~0 (the workgroup's next unit, same argument block) that unit's first own
+// input is loaded into cur before the mixing, so the mixing overlaps it, and
+// the call returns true.
 template <class C, bool NT, int H, int P>
-__device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t off,
-                                                PairLds<P>& lds, uint32_t pair, uint32_t lane) {
+__device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t off,
+                                                PairLds<P>& lds, uint32_t pair, uint32_t lane,
+                                                u32x4 (&cur)[4], bool primed, uint64_t next_off) {
   using F = typename C::Field;
   constexpr int R0 = H * kPairRows;
   const uint32_t present = a.present;
@@ -1561,8 +1565,8 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
   uint32_t acc[kPairRows * 16];
 #pragma unroll
   for (int q = 0; q < kPairRows * 16; ++q) acc[q] = 0u;
-  u32x4 cur[4];
-  if (own) load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + off);
+  const uint8_t* const first = own ? recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) : nullptr;
+  if (own && !primed) load4<NT, 1024u>(cur, first + off);
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
@@ -1570,8 +1574,6 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
   // own syndrome rows: s_r = sigma_r ^ parity_r
 #pragma unroll
   for (int i = 0; i < kPairRows; ++i) {
-    constexpr int dummy = 0;
-    (void)dummy;
     const int J = C::k + R0 + i;
     if ((own >> J) & 1u) {
       u32x4 nxt[4];
@@ -1587,6 +1589,8 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
       }
     }
   }
+  const bool prime = own && next_off != ~0ull;
+  if (prime) load4<NT, 1024u>(cur, first + next_off);
   if constexpr (HornerF<F>::N == 16) {
 #pragma unroll
     for (int r = 0; r < kPairRows; ++r)
@@ -1642,28 +1646,35 @@ __device__ __forceinline__ void recon_pair_unit(const BsReconArgs& a, uint64_t o
     }
     __syncthreads();
   }
+  return prime;
 }
 
 // Units of P 4 KiB columns: unit u of a stripe (cps 16 KiB chunks) covers
 // bytes [u * 4096P, (u + 1) * 4096P); pair q its column q.  Workgroups of
 // 128P lanes.
-template <class C, bool NT, int P>
+template <class C, bool NT, int P, bool PF = false>
 __device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
                                                          uint64_t chunks_per_stripe) {
   __shared__ PairLds<P> lds;
   const uint64_t upc = chunks_per_stripe * (4 / P), total = upc * a.n_stripes;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
-  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+  auto unit_off = [&](uint64_t u) {
     const uint64_t stripe = u / upc, sub = u - stripe * upc;
-    const uint64_t off = stripe * a.stripe_stride + sub * (4096u * P) + pair * 4096u + lane * 16u;
-    if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane);
-    else recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane);
+    return stripe * a.stripe_stride + sub * (4096u * P) + pair * 4096u + lane * 16u;
+  };
+  u32x4 cur[4];
+  bool primed = false;
+  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    const uint64_t nu = u + gridDim.x;
+    const uint64_t next_off = PF && nu < total ? unit_off(nu) : ~0ull;
+    if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
+    else primed = recon_pair_unit<C, NT, 0, P>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
   }
 }
 
 // The same over per-stripe argument blocks (rse_reconstruct_batch).
-template <class C, bool NT, int P>
+template <class C, bool NT, int P, bool PF = false>
 __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs* __restrict__ descs,
                                                               uint64_t chunks_per_stripe,
                                                               uint64_t n_stripes) {
@@ -1671,13 +1682,20 @@ __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs*
   const uint64_t upc = chunks_per_stripe * (4 / P), total = upc * n_stripes;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
+  u32x4 cur[4];
+  bool primed = false;
   for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
     const uint64_t stripe = u / upc, sub = u - stripe * upc;
     const BsReconArgs& a = desc_at(descs, stripe);
     if (a.n_out == 0) continue;  // workgroup-uniform
     const uint64_t off = sub * (4096u * P) + pair * 4096u + lane * 16u;
-    if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane);
-    else recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane);
+    // the next unit's first input only when it is this stripe's (same block)
+    const uint64_t nu = u + gridDim.x, nsub = sub + gridDim.x;
+    const uint64_t next_off = PF && nu < total && nsub < upc
+                                  ? nsub * (4096u * P) + pair * 4096u + lane * 16u
+                                  : ~0ull;
+    if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane, cur, primed, next_off);
+    else primed = recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane, cur, primed, next_off);
   }
 }
 
