@@ -15,6 +15,7 @@
 // launch's coefficients equal the compiled ones before dispatching here
 // (anything else takes the table kernels), so a matrix mismatch can only cost
 // speed, never correctness.
+#include <atomic>
 #include "rse_bitslice_core.hpp"
 
 namespace rse {
@@ -445,6 +446,22 @@ static const BsShape kBsShapes[] = {
 
 }  // namespace
 
+// Compute units of the current device (cached per device).
+uint32_t device_cus() {
+  static std::atomic<uint32_t> cus[64];  // zero-initialised (static storage)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  uint32_t c = cus[dev].load(std::memory_order_relaxed);
+  if (!c) {
+    int n = 0;
+    c = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0
+            ? (uint32_t)n
+            : 256u;
+    cus[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
+}
+
 hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                            hipStream_t stream, bool* handled, uint64_t* done) {
   *handled = false;
@@ -487,8 +504,17 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   }
   // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
   const uint64_t g0 = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);
+  // A launch of at most two rounds of the resident workgroups (one 10+4 x 16
+  // MiB stripe: 1024 chunks against 768) runs its chunks in equal shares
+  // instead of a full round plus a third of one: check mode two chunks per
+  // workgroup, store mode one round of resident workgroups (per call through
+  // the C ABI, tools/capi_latency.cpp: verify 52.3 -> 48.6 us, encode 43.8 ->
+  // 41.2 us, profiles/r03/s5/).
+  const uint64_t resident = (uint64_t)device_cus() * (a.n_out > 4 ? 2u : 3u);
   auto clamp = [&](uint64_t steps) {
     uint64_t gx = g0 < steps ? g0 : steps;
+    if (grid <= 0 && steps > resident && steps <= 2 * resident)
+      gx = a.mode != kStore ? (steps + 1) / 2 : resident;
     return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
   };
   auto launch = [&](BsFn f, hipFunction_t j, const CodeArgs& args, uint64_t cps, uint64_t steps) {
