@@ -504,17 +504,17 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   }
   // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
   const uint64_t g0 = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);
-  // A launch of at most two rounds of the resident workgroups (one 10+4 x 16
-  // MiB stripe: 1024 chunks against 768) runs its chunks in equal shares
-  // instead of a full round plus a third of one: check mode two chunks per
-  // workgroup, store mode one round of resident workgroups (per call through
-  // the C ABI, tools/capi_latency.cpp: verify 52.3 -> 48.6 us, encode 43.8 ->
-  // 41.2 us, profiles/r03/s5/).
+  // A launch of one to two rounds of the resident workgroups (one 10+4 x 16
+  // MiB stripe: 1024 chunks against 768) runs as one round of resident
+  // workgroups, grid-striding over the rest, instead of a full round plus a
+  // late third of one.  Per call through the C ABI (tools/capi_latency.cpp,
+  // two boxes, profiles/r03/s5/, s6/): verify 52.3-52.9 -> 48.5-49.5 us,
+  // encode 43.6-43.8 -> 40.9-41.2 us (half the chunks per workgroup, 512,
+  // was 48.6-51.8 for verify).
   const uint64_t resident = (uint64_t)device_cus() * (a.n_out > 4 ? 2u : 3u);
   auto clamp = [&](uint64_t steps) {
     uint64_t gx = g0 < steps ? g0 : steps;
-    if (grid <= 0 && steps > resident && steps <= 2 * resident)
-      gx = a.mode != kStore ? (steps + 1) / 2 : resident;
+    if (grid <= 0 && steps > resident && steps <= 2 * resident) gx = resident;
     return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
   };
   auto launch = [&](BsFn f, hipFunction_t j, const CodeArgs& args, uint64_t cps, uint64_t steps) {
