@@ -467,10 +467,71 @@ __device__ __forceinline__ void wide_body(const A& a) {
 template <int W>
 using WidePlanes = uint4[2][W][4][64];  // [set][slot][quad of planes][lane]
 
+// Paired inputs (C::kPairIn, GF(2^8), rse_netgen.hpp build_pairs): network
+// input J is data inputs 2J and 2J + 1, sources 0..7 the first's planes of a
+// group, 8..15 the second's, then J's temporaries (per group, both groups
+// sharing the bit matrices).  pb may be all zero (odd k: no second input).
+template <class C, int J, int... OP>
+__device__ __forceinline__ void mac_pair(uint32_t (&acc)[C::p * 16], const uint32_t (&pa)[16],
+                                         const uint32_t (&pb)[16], int_seq<int, OP...>) {
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    uint32_t src[16 + C::kGTemps];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      src[q] = pa[g * 8 + q];
+      src[8 + q] = pb[g * 8 + q];
+    }
+#pragma unroll
+    for (int t = 0; t < C::kGTemps; ++t)
+      if (t < C::planes.ntmp[J]) src[16 + t] = temp_source<C, J>(src, t);
+    // OP < p * 8: output OP / 8, plane OP % 8 of group g
+    if (g == 0)
+      ((acc[(OP / 8) * 16 + OP % 8] =
+            xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + OP % 8], src)),
+       ...);
+    else
+      ((acc[(OP / 8) * 16 + 8 + OP % 8] =
+            xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + 8 + OP % 8], src)),
+       ...);
+  }
+}
+
 template <class C, int W, int R, int S>
 __device__ __forceinline__ void wide_code_round(uint32_t (&acc)[C::p * 16],
                                                 const uint4 (&set)[W][4][64], uint32_t lane) {
-  if constexpr (S < W && R * W + S < C::k) {
+  if constexpr (C::kPairIn) {
+    // two inputs at a time (W even, so a round's inputs pair up)
+    static_assert(W % 2 == 0, "paired inputs need an even number of waves");
+    if constexpr (S < W && R * W + S < C::k) {
+      uint32_t pa[16], pb[16];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const uint4 v = set[S][q4][lane];
+        pa[q4 * 4 + 0] = v.x;
+        pa[q4 * 4 + 1] = v.y;
+        pa[q4 * 4 + 2] = v.z;
+        pa[q4 * 4 + 3] = v.w;
+      }
+      if constexpr (R * W + S + 1 < C::k) {
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const uint4 v = set[S + 1][q4][lane];
+          pb[q4 * 4 + 0] = v.x;
+          pb[q4 * 4 + 1] = v.y;
+          pb[q4 * 4 + 2] = v.z;
+          pb[q4 * 4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pb[q] = 0u;
+      }
+      mac_pair<C, (R * W + S) / 2>(acc, pa, pb, make_int_seq<C::p * 8>{});
+#pragma unroll
+      for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
+      wide_code_round<C, W, R, S + 2>(acc, set, lane);
+    }
+  } else if constexpr (S < W && R * W + S < C::k) {
     uint32_t pl[16];
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {

@@ -157,8 +157,9 @@ int recon_ns(uint32_t p, int* ns) {
 // The code struct `name` of p x k rows (rse_netgen.hpp), inside the
 // kernels' namespace.
 void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t p,
-               const std::vector<uint16_t>& rows, int temps) {
-  const netgen::Net net = netgen::build(field, k, p, rows.data(), temps, get_option(23) != 0);
+               const std::vector<uint16_t>& rows, int temps, bool pairs = false) {
+  const netgen::Net net = pairs ? netgen::build_pairs(k, p, rows.data(), temps)
+                                : netgen::build(field, k, p, rows.data(), temps, get_option(23) != 0);
   s += "\nnamespace rse {\nnamespace {\n";
   s += netgen::emit(net, name, rows.data());
   s += "}  // namespace\n}  // namespace rse\n";
@@ -214,6 +215,10 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   if (kind == kJitWide) {
     // one code struct per wave's share of the outputs, and the kernel
     const int W = wide_waves(p);
+    const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
+    // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS
+    // kernels code a round's inputs two at a time, so W must be even
+    const bool pairs = field == 8 && shared && W % 2 == 0 && get_option(29) != 0;
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, w, &o0, &n);
@@ -221,9 +226,11 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       char name[32];
       std::snprintf(name, sizeof name, "JitWide%d", w);
       // an input feeds many outputs here: shared temporaries in both fields
-      // (GF(2^8): per input, computed per plane group)
+      // (GF(2^8): per input or input pair, computed per plane group)
       emit_code(s, name, field, k, n, sub,
-                field == 16 ? (int)get_option(13) : std::min(16, (int)get_option(13)));
+                field == 16 ? (int)get_option(13)
+                            : std::min(pairs ? 32 : 16, (int)get_option(13)),
+                pairs);
     }
     char buf[512];
     std::snprintf(buf, sizeof buf,
@@ -237,7 +244,6 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
                   k, p, p, 64 * W, 64 * W, wide_waves_per_eu(p), W);
     s += buf;
-    const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, w, &o0, &n);

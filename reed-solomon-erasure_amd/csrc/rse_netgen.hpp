@@ -45,16 +45,22 @@ struct Net {
   int field = 8;
   int np = 8;  // planes per group: 8 (GF(2^8), two groups per 16 dwords) or 16
   uint32_t k = 0, p = 0;
-  int temps = 0;                                  // budget per input
-  std::vector<uint64_t> sel;                      // [o][i][q]
-  std::vector<uint8_t> ntmp;                      // [i]
-  std::vector<std::array<uint8_t, 3>> tmp;        // [i][t]: sources {a, b, c}; c = 255: a pair
-  uint64_t& at(uint32_t o, uint32_t i, int q) { return sel[((size_t)o * k + i) * np + q]; }
-  uint64_t at(uint32_t o, uint32_t i, int q) const { return sel[((size_t)o * k + i) * np + q]; }
+  // paired inputs (GF(2^8) wide modules, build_pairs): network input j is data
+  // inputs 2j and 2j + 1, sources 0..7 the planes of the first, 8..15 of the
+  // second, so temporaries may combine planes of both; ki = (k + 1) / 2
+  bool pairs = false;
+  uint32_t ki = 0;                                // network inputs: k, or (k + 1) / 2
+  int temps = 0;                                  // budget per network input
+  std::vector<uint64_t> sel;                      // [o][ki][q]
+  std::vector<uint8_t> ntmp;                      // [ki]
+  std::vector<std::array<uint8_t, 3>> tmp;        // [ki][t]: sources {a, b, c}; c = 255: a pair
+  int nsrc() const { return pairs ? 16 : np; }    // plane sources per network input
+  uint64_t& at(uint32_t o, uint32_t i, int q) { return sel[((size_t)o * ki + i) * np + q]; }
+  uint64_t at(uint32_t o, uint32_t i, int q) const { return sel[((size_t)o * ki + i) * np + q]; }
   // v_bitop3 count of one chunk's network (the cost model above)
   size_t ops() const {
     size_t n = 0;
-    for (uint32_t i = 0; i < k; ++i) n += ntmp[i];
+    for (uint32_t i = 0; i < ki; ++i) n += ntmp[i];
     for (uint64_t m : sel) n += ((size_t)__builtin_popcountll(m) + 1) / 2;
     return n;
   }
@@ -265,6 +271,7 @@ inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int bu
   net.field = field;
   net.np = field == 16 ? 16 : 8;
   net.k = k;
+  net.ki = k;
   net.p = p;
   net.temps = budget < 0 ? 0 : budget > kMaxTemps ? kMaxTemps : budget;
   net.sel.assign((size_t)p * k * net.np, 0);
@@ -316,6 +323,59 @@ inline Net build(int field, uint32_t k, uint32_t p, const uint16_t* rows, int bu
   return net;
 }
 
+// The GF(2^8) network of p x k rows over PAIRS of inputs (Net::pairs): the
+// rows of network input j are the two inputs' bit-matrix rows side by side (16
+// sources), factored like a GF(2^16) input (factor16, or the greedy if that is
+// cheaper), so a temporary can serve both inputs' terms of a row.  The wide
+// kernels code a round's inputs two at a time (rse_bitslice_core.hpp
+// wide_code_round).  50+20 in 4 output shares: 10293 -> ~8800 ops per plane
+// group at 32 temporaries (tools: offline count).
+inline Net build_pairs(uint32_t k, uint32_t p, const uint16_t* rows, int budget) {
+  const Net plain = build(8, k, p, rows, 0, false);
+  Net net;
+  net.field = 8;
+  net.np = 8;
+  net.k = k;
+  net.p = p;
+  net.pairs = true;
+  net.ki = (k + 1) / 2;
+  net.temps = budget < 0 ? 0 : budget > kMaxTemps ? kMaxTemps : budget;
+  const int nt = net.temps > 0 ? net.temps : 1;
+  net.sel.assign((size_t)p * net.ki * 8, 0);
+  net.ntmp.assign(net.ki, 0);
+  net.tmp.assign((size_t)net.ki * nt, {0, 0, 255});
+  for (uint32_t j = 0; j < net.ki; ++j) {
+    std::vector<uint64_t> r;
+    for (uint32_t o = 0; o < p; ++o)
+      for (int q = 0; q < 8; ++q) {
+        uint64_t m = plain.at(o, 2 * j, q);
+        if (2 * j + 1 < k) m |= plain.at(o, 2 * j + 1, q) << 8;
+        r.push_back(m);
+      }
+    std::array<uint8_t, 3>* t = &net.tmp[(size_t)j * nt];
+    if (net.temps > 0) {
+      std::vector<uint64_t> r2 = r;
+      net.ntmp[j] = (uint8_t)factor(r, net.temps, 16, t);
+      std::vector<std::array<uint8_t, 3>> t2((size_t)net.temps);
+      const int n2 = factor16(r2, net.temps, t2.data());
+      auto cost = [](const std::vector<uint64_t>& v, int n) {
+        size_t c = (size_t)n;
+        for (uint64_t m : v) c += ((size_t)__builtin_popcountll(m) + 1) / 2;
+        return c;
+      };
+      if (cost(r2, n2) <= cost(r, net.ntmp[j])) {
+        r.swap(r2);
+        for (int x = 0; x < n2; ++x) t[x] = t2[(size_t)x];
+        net.ntmp[j] = (uint8_t)n2;
+      }
+    }
+    size_t n = 0;
+    for (uint32_t o = 0; o < p; ++o)
+      for (int q = 0; q < 8; ++q) net.at(o, j, q) = r[n++];
+  }
+  return net;
+}
+
 // C++ source of code struct `name` for rse_bitslice_core.hpp:
 //   using Field; k, p, NP, NG, kTemps (GF(2^16) per-input temporaries),
 //   kGTemps (GF(2^8) per-group temporaries); planes.sel / ntmp / tmp; rows.
@@ -328,11 +388,12 @@ inline std::string emit(const Net& net, const char* name, const uint16_t* rows) 
                 "  uint8_t tmp[%u][%d][3];\n};\n"
                 "struct %s {\n  using Field = %s;\n"
                 "  static constexpr int k = %u, p = %u, NP = %d, NG = %d, kTemps = %d, "
-                "kGTemps = %d;\n"
+                "kGTemps = %d, kPairIn = %d;\n"
                 "  static constexpr uint16_t rows[%u][%u] = {",
-                name, net.p, net.k, net.np, net.k, net.k, nt, name,
+                name, net.p, net.ki, net.np, net.ki, net.ki, nt, name,
                 net.field == 16 ? "BitsF16" : "BitsF8", net.k, net.p, net.np, 16 / net.np,
-                net.field == 16 ? net.temps : 0, net.field == 16 ? 0 : net.temps, net.p, net.k);
+                net.field == 16 ? net.temps : 0, net.field == 16 ? 0 : net.temps,
+                net.pairs ? 1 : 0, net.p, net.k);
   s += buf;
   for (uint32_t o = 0; o < net.p; ++o) {
     s += "{";
@@ -346,7 +407,7 @@ inline std::string emit(const Net& net, const char* name, const uint16_t* rows) 
   s += buf;
   for (uint32_t o = 0; o < net.p; ++o) {
     s += "{";
-    for (uint32_t i = 0; i < net.k; ++i) {
+    for (uint32_t i = 0; i < net.ki; ++i) {
       s += "{";
       for (int q = 0; q < net.np; ++q) {
         std::snprintf(buf, sizeof buf, "%lluull,", (unsigned long long)net.at(o, i, q));
@@ -357,12 +418,12 @@ inline std::string emit(const Net& net, const char* name, const uint16_t* rows) 
     s += "},";
   }
   s += "}, {";
-  for (uint32_t i = 0; i < net.k; ++i) {
+  for (uint32_t i = 0; i < net.ki; ++i) {
     std::snprintf(buf, sizeof buf, "%d,", net.ntmp[i]);
     s += buf;
   }
   s += "}, {";
-  for (uint32_t i = 0; i < net.k; ++i) {
+  for (uint32_t i = 0; i < net.ki; ++i) {
     s += "{";
     for (int t = 0; t < nt; ++t) {
       const auto& x = net.tmp[(size_t)i * nt + t];

@@ -26,10 +26,10 @@ std::vector<uint16_t> parity(size_t k, size_t p) {  // core.rs:430-436
   return rows;
 }
 
-// Value (over the input's np planes) of source j of input i.
+// Value (over network input i's plane sources) of source j of input i.
 uint64_t source_value(const netgen::Net& net, uint32_t i, int j) {
-  if (j < net.np) return 1ull << j;
-  const auto& t = net.tmp[(size_t)i * (net.temps > 0 ? net.temps : 1) + (j - net.np)];
+  if (j < net.nsrc()) return 1ull << j;
+  const auto& t = net.tmp[(size_t)i * (net.temps > 0 ? net.temps : 1) + (j - net.nsrc())];
   uint64_t v = source_value(net, i, t[0]) ^ source_value(net, i, t[1]);
   if (t[2] != 255) v ^= source_value(net, i, t[2]);
   return v;
@@ -70,6 +70,42 @@ int check(int field, uint32_t k, uint32_t p, int budget) {
   return ops[1] <= ops[0] ? 0 : 6;
 }
 
+// Paired GF(2^8) networks (build_pairs): network input j's rows are inputs 2j
+// and 2j + 1's bit-matrix rows side by side (sources 0..7 and 8..15).
+int check_pairs(uint32_t k, uint32_t p, int budget) {
+  const auto rows = parity<Gf8Field>(k, p);
+  const netgen::Net plain = netgen::build(8, k, p, rows.data(), 0);
+  const netgen::Net net = netgen::build_pairs(k, p, rows.data(), budget);
+  if (!net.pairs || net.ki != (k + 1) / 2) return 11;
+  const int ns = net.nsrc();
+  for (uint32_t j = 0; j < net.ki; ++j) {
+    if (net.ntmp[j] > net.temps) return 12;
+    for (int t = 0; t < net.ntmp[j]; ++t) {
+      const auto& x = net.tmp[(size_t)j * (net.temps > 0 ? net.temps : 1) + t];
+      if (x[0] >= ns + t || x[1] >= ns + t || (x[2] != 255 && x[2] >= ns + t)) return 13;
+    }
+    for (uint32_t o = 0; o < p; ++o)
+      for (int q = 0; q < 8; ++q) {
+        uint64_t v = 0;
+        for (uint64_t m = net.at(o, j, q); m; m &= m - 1) {
+          const int s = __builtin_ctzll(m);
+          if (s >= ns + net.ntmp[j]) return 14;
+          v ^= source_value(net, j, s);
+        }
+        uint64_t want = plain.at(o, 2 * j, q);
+        if (2 * j + 1 < k) want |= plain.at(o, 2 * j + 1, q) << 8;
+        if (v != want) {
+          std::printf("MISMATCH pairs %u+%u budget %d o %u j %u q %d\n", k, p, budget, o, j, q);
+          return 15;
+        }
+      }
+  }
+  const netgen::Net one = netgen::build(8, k, p, rows.data(), budget);
+  std::printf("pairs 8 %u+%u budget %d: paired %zu, per input %zu\n", k, p, budget, net.ops(),
+              one.ops());
+  return 0;
+}
+
 int main() {
   const struct { int field; uint32_t k, p; } cases[] = {
       {8, 10, 4}, {8, 12, 8}, {8, 50, 5}, {8, 3, 2}, {16, 20, 8}, {16, 40, 3}, {16, 7, 5}};
@@ -78,6 +114,15 @@ int main() {
       const int rc = check(c.field, c.k, c.p, budget);
       if (rc) {
         std::printf("FAIL rc %d field %d %u+%u budget %d\n", rc, c.field, c.k, c.p, budget);
+        return rc;
+      }
+    }
+  const struct { uint32_t k, p; } pcases[] = {{50, 5}, {51, 7}, {3, 2}, {1, 4}, {12, 8}};
+  for (const auto& c : pcases)
+    for (int budget : {0, 4, 16, 32}) {
+      const int rc = check_pairs(c.k, c.p, budget);
+      if (rc) {
+        std::printf("FAIL rc %d pairs %u+%u budget %d\n", rc, c.k, c.p, budget);
         return rc;
       }
     }
