@@ -485,15 +485,23 @@ __device__ __forceinline__ void mac_pair(uint32_t (&acc)[C::p * 16], const uint3
 #pragma unroll
     for (int t = 0; t < C::kGTemps; ++t)
       if (t < C::planes.ntmp[J]) src[16 + t] = temp_source<C, J>(src, t);
-    // OP < p * 8: output OP / 8, plane OP % 8 of group g
-    if (g == 0)
-      ((acc[(OP / 8) * 16 + OP % 8] =
-            xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + OP % 8], src)),
-       ...);
-    else
-      ((acc[(OP / 8) * 16 + 8 + OP % 8] =
-            xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + 8 + OP % 8], src)),
-       ...);
+    // OP < p * 8: output OP / 8, plane OP % 8 of group g; input pair 0
+    // initialises the accumulators (as mac_input's input 0 does)
+    if constexpr (J == 0) {
+      if (g == 0)
+        ((acc[(OP / 8) * 16 + OP % 8] = xinit<C::planes.sel[OP / 8][J][OP % 8]>(src)), ...);
+      else
+        ((acc[(OP / 8) * 16 + 8 + OP % 8] = xinit<C::planes.sel[OP / 8][J][OP % 8]>(src)), ...);
+    } else {
+      if (g == 0)
+        ((acc[(OP / 8) * 16 + OP % 8] =
+              xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + OP % 8], src)),
+         ...);
+      else
+        ((acc[(OP / 8) * 16 + 8 + OP % 8] =
+              xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[(OP / 8) * 16 + 8 + OP % 8], src)),
+         ...);
+    }
   }
 }
 
