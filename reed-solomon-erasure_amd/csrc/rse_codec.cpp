@@ -338,6 +338,7 @@ struct Scratch {
   std::vector<hipStream_t> st;
   std::vector<hipEvent_t> h2d, coded, d2h;
   hipEvent_t start = nullptr;
+  hipEvent_t done = nullptr;  // run_check's completion event (RSE_OPT_SYNC_EVENT)
   uint8_t* dbuf = nullptr;
   size_t dbytes = 0;
 };
@@ -356,6 +357,7 @@ void drop_pipe_streams(Scratch& s) {
 void destroy_scratch(Scratch* s) {  // idle: its last call synchronised
   drop_pipe_streams(*s);
   if (s->start) (void)hipEventDestroy(s->start);
+  if (s->done) (void)hipEventDestroy(s->done);
   if (s->own) (void)hipStreamDestroy(s->own);
   if (s->dbuf) (void)hipFree(s->dbuf);
   if (s->wh) (void)hipHostFree(s->wh);
@@ -498,8 +500,17 @@ int run_check(Job j, hipStream_t s, int* ok) {
   j.mismatch = lease->wd;
   int rc = run_job(j, s);
   // kernels already queued may still store into the words: drain them before
-  // the lease returns them to the pool
-  const hipError_t se = hipStreamSynchronize(s);
+  // the lease returns them to the pool.  RSE_OPT_SYNC_EVENT 1: wait on an
+  // event recorded after them instead of on the whole stream (A/B)
+  hipError_t se = hipSuccess;
+  if (rse::get_option(30)) {
+    if (!lease->done) se = hipEventCreateWithFlags(&lease->done, hipEventDisableTiming);
+    if (se == hipSuccess) se = hipEventRecord(lease->done, s);
+    if (se == hipSuccess) se = hipEventSynchronize(lease->done);
+    if (se != hipSuccess) (void)hipStreamSynchronize(s);
+  } else {
+    se = hipStreamSynchronize(s);
+  }
   if (rc != RSE_OK) return rc;
   RSE_HIP(se);
   for (size_t i = 0; i < words; ++i)

@@ -789,6 +789,7 @@ struct Options {
   int64_t recon_depth = 1;        // syndrome reconstruct: inputs in flight per lane (1..4)
   int64_t recon_pairs = 1;        // syndrome reconstruct at 8 sigma rows on wave pairs
   int64_t wide_pairs = 1;         // wide GF(2^8) modules: networks over pairs of inputs
+  int64_t sync_event = 0;         // verify calls wait on an event, not the stream (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1274,6 +1275,7 @@ int set_option(int key, int64_t value) {
     case 27: g_opt.recon_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 28: g_opt.recon_pairs = value < 0 ? 0 : value > 3 ? 3 : value; return 0;
     case 29: g_opt.wide_pairs = value ? 1 : 0; return 0;
+    case 30: g_opt.sync_event = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1315,6 +1317,7 @@ int64_t get_option(int key) {
     case 27: return g_opt.recon_depth;
     case 28: return g_opt.recon_pairs;
     case 29: return g_opt.wide_pairs;
+    case 30: return g_opt.sync_event;
     default: return -1;
   }
 }

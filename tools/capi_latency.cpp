@@ -19,6 +19,10 @@ int main(int argc, char** argv) {
     if (rse_set_option(RSE_OPT_GRID_X, g)) return 7;
     std::printf("grid %ld\n", g);
   }
+  if (argc > 2) {  // RSE_OPT_SYNC_EVENT
+    if (rse_set_option(RSE_OPT_SYNC_EVENT, std::atol(argv[2]))) return 8;
+    std::printf("sync event %s\n", argv[2]);
+  }
   rse_codec* c = nullptr;
   if (rse_codec_new(RSE_FIELD_GF8, k, p, &c)) return 1;
   uint8_t* buf = nullptr;
