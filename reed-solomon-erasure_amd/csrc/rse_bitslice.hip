@@ -228,12 +228,13 @@ struct GfDev {
   }
   __device__ uint32_t inv(uint32_t a) const {  // a != 0
     if (field == 8) return ex[255 - lg[a]];
-    uint32_t r = 1, b = a;
-    for (uint32_t n = 65534u; n; n >>= 1) {
-      if (n & 1u) r = mul(r, b);
-      b = mul(b, b);
-    }
-    return r;
+    // through the norm N = a0^2 + 2 a0 a1 + 128 a1^2 in GF(2^8), as
+    // rse_kernels.hip PlanF16: (a1 x + a0)^-1 = (a1 x + a0 + 2 a1) / N (the
+    // unique inverse; 8 subfield products instead of a^(2^16-2)'s 30)
+    const uint32_t a1 = a >> 8, a0 = a & 0xFFu;
+    const uint32_t n = m8(a0, a0) ^ m8(2u, m8(a0, a1)) ^ m8(128u, m8(a1, a1));
+    const uint32_t ni = ex[255 - lg[n]];  // n != 0 for a != 0
+    return (m8(a1, ni) << 8) | m8(a0 ^ m8(2u, a1), ni);
   }
 };
 

@@ -1674,17 +1674,23 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
   }
   RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&dflags), fl_bytes + 64, st));
-  {
+  if (!dev_scan) {
     hipError_t e = hipMemcpyAsync(dflags, present, n_stripes * T, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return dev_fail(release(e));
-  }
-  if (dev_scan) {
+  } else {
+    // the flags through the lease's pinned words (an asynchronous DMA rather
+    // than the runtime's staged pageable copy), the scan's results back into
+    // the first words
     Lease lease;
     hipError_t e = lease.acquire();
-    if (e == hipSuccess) e = lease_words(lease.get(), 6);
+    if (e == hipSuccess) e = lease_words(lease.get(), 8 + (n_stripes * T + 3) / 4);
     uint32_t* res = reinterpret_cast<uint32_t*>(dflags + fl_bytes);
-    const uint32_t init[6] = {0u, 0u, 0u, 0u, ~0u, ~0u};
-    if (e == hipSuccess) e = hipMemcpyAsync(res, init, sizeof init, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      std::memcpy(lease->wh + 8, present, n_stripes * T);
+      e = hipMemcpyAsync(dflags, lease->wh + 8, n_stripes * T, hipMemcpyHostToDevice, st);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(res, 0, 4 * sizeof(uint32_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(res + 4, 0xFF, 2 * sizeof(uint32_t), st);
     if (e == hipSuccess)
       e = rse::launch_batch_scan(dflags, n_stripes, (uint32_t)k, (uint32_t)p, data_only ? 1u : 0u,
                                  res, st);
