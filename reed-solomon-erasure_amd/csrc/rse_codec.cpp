@@ -1681,13 +1681,17 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     // the flags through the lease's pinned words (an asynchronous DMA rather
     // than the runtime's staged pageable copy), the scan's results back into
     // the first words
+    // (pinned words only up to 16 MiB of flags: a lease keeps its words, and
+    // the pool keeps up to kIdleScratch leases)
     Lease lease;
+    const bool staged = n_stripes * T <= (size_t(16) << 20);
     hipError_t e = lease.acquire();
-    if (e == hipSuccess) e = lease_words(lease.get(), 8 + (n_stripes * T + 3) / 4);
+    if (e == hipSuccess) e = lease_words(lease.get(), 8 + (staged ? (n_stripes * T + 3) / 4 : 0));
     uint32_t* res = reinterpret_cast<uint32_t*>(dflags + fl_bytes);
     if (e == hipSuccess) {
-      std::memcpy(lease->wh + 8, present, n_stripes * T);
-      e = hipMemcpyAsync(dflags, lease->wh + 8, n_stripes * T, hipMemcpyHostToDevice, st);
+      if (staged) std::memcpy(lease->wh + 8, present, n_stripes * T);
+      e = hipMemcpyAsync(dflags, staged ? static_cast<const void*>(lease->wh + 8) : present,
+                         n_stripes * T, hipMemcpyHostToDevice, st);
     }
     if (e == hipSuccess) e = hipMemsetAsync(res, 0, 4 * sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(res + 4, 0xFF, 2 * sizeof(uint32_t), st);
