@@ -1071,21 +1071,29 @@ __device__ __forceinline__ void h_case(uint32_t (&v)[16], const uint32_t (&s)[NS
   }
 }
 
+// The 16 cases of a nibble as a binary tree of uniform branches on its bits
+// (LO..HI-1 the cases left): already structured control flow.  A switch came
+// out of the CFG structurizer as a chain of flag tests, ~18 branches per
+// step instead of 4 (tools/isa_probe.sh, SQ_INSTS_BRANCH).
+template <class F, bool SH, int G, int NS, int ND, int LO, int HI>
+__device__ __forceinline__ void h_tree(uint32_t (&v)[16], const uint32_t (&s)[NS * 16],
+                                       const uint32_t (&d)[ND][16], uint32_t nib) {
+  if constexpr (HI - LO == 1) {
+    h_case<F, SH, LO, G, NS, ND>(v, s, d);
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    // (opaque to the optimiser, which would otherwise fold the tree back
+    // into a switch on nib)
+    uint32_t bit = nib & (uint32_t)(MID - LO);
+    asm volatile("" : "+s"(bit));
+    if (bit) h_tree<F, SH, G, NS, ND, MID, HI>(v, s, d, nib);
+    else h_tree<F, SH, G, NS, ND, LO, MID>(v, s, d, nib);
+  }
+}
 template <class F, bool SH, int G, int NS, int ND>
 __device__ __forceinline__ void h_group(uint32_t (&v)[16], const uint32_t (&s)[NS * 16],
                                         const uint32_t (&d)[ND][16], uint32_t nib) {
-#define RSE_HCASE(n) \
-  case n:            \
-    h_case<F, SH, n, G, NS, ND>(v, s, d); \
-    break;
-  switch (nib) {
-    RSE_HCASE(0) RSE_HCASE(1) RSE_HCASE(2) RSE_HCASE(3)
-    RSE_HCASE(4) RSE_HCASE(5) RSE_HCASE(6) RSE_HCASE(7)
-    RSE_HCASE(8) RSE_HCASE(9) RSE_HCASE(10) RSE_HCASE(11)
-    RSE_HCASE(12) RSE_HCASE(13) RSE_HCASE(14) RSE_HCASE(15)
-    default: break;
-  }
-#undef RSE_HCASE
+  h_tree<F, SH, G, NS, ND, 0, 16>(v, s, d, nib);
 }
 
 // The mixing of recon_chunk by Horner's rule on the sliced rows acc (converted
@@ -1617,10 +1625,23 @@ __device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
 // != ~0 (the workgroup's next unit, same argument block) that unit's first own
 // input is loaded into cur before the mixing, so the mixing overlaps it, and
 // the call returns true.
-template <class C, bool NT, int H, int P>
+template <bool PF, class T>
+__device__ __forceinline__ T& pick_ref(T& io, T& local) {
+  if constexpr (PF) return io;
+  else return local;
+}
+template <class C, bool NT, int H, int P, bool PF = false>
 __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t off,
                                                 PairLds<P>& lds, uint32_t pair, uint32_t lane,
-                                                u32x4 (&cur)[4], bool primed, uint64_t next_off) {
+                                                u32x4 (&cur_io)[4], bool primed, uint64_t next_off) {
+  // without the prefetch the unit's vectors are its own (nothing the compiler
+  // must keep across units: 141 VGPRs, not 168 with 5 spilled)
+  u32x4 cur_local[4];
+  u32x4(&cur)[4] = pick_ref<PF>(cur_io, cur_local);
+  if constexpr (!PF) {
+    primed = false;
+    next_off = ~0ull;
+  }
   using F = typename C::Field;
   constexpr int R0 = H * kPairRows;
   const uint32_t present = a.present;
@@ -1634,8 +1655,8 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
   uint32_t acc[kPairRows * 16];
 #pragma unroll
   for (int q = 0; q < kPairRows * 16; ++q) acc[q] = 0u;
-  const uint8_t* const first = own ? recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) : nullptr;
-  if (own && !primed) load4<NT, 1024u>(cur, first + off);
+  if (own && !primed)
+    load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + off);
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
@@ -1659,7 +1680,7 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
     }
   }
   const bool prime = own && next_off != ~0ull;
-  if (prime) load4<NT, 1024u>(cur, first + next_off);
+  if (prime) load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + next_off);
   if constexpr (HornerF<F>::N == 16) {
 #pragma unroll
     for (int r = 0; r < kPairRows; ++r)
@@ -1732,13 +1753,22 @@ __device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
     const uint64_t stripe = u / upc, sub = u - stripe * upc;
     return stripe * a.stripe_stride + sub * (4096u * P) + pair * 4096u + lane * 16u;
   };
-  u32x4 cur[4];
-  bool primed = false;
-  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
-    const uint64_t nu = u + gridDim.x;
-    const uint64_t next_off = PF && nu < total ? unit_off(nu) : ~0ull;
-    if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
-    else primed = recon_pair_unit<C, NT, 0, P>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
+  if constexpr (PF) {
+    u32x4 cur[4];
+    bool primed = false;
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+      const uint64_t nu = u + gridDim.x;
+      const uint64_t next_off = nu < total ? unit_off(nu) : ~0ull;
+      if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P, true>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
+      else primed = recon_pair_unit<C, NT, 0, P, true>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
+    }
+  } else {
+    // (a fresh vector set per unit: nothing lives across units)
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+      u32x4 cur[4];
+      if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
+      else recon_pair_unit<C, NT, 0, P>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
+    }
   }
 }
 
@@ -1751,20 +1781,31 @@ __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs*
   const uint64_t upc = chunks_per_stripe * (4 / P), total = upc * n_stripes;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t pair = wave >> 1, lane = threadIdx.x & 63u;
-  u32x4 cur[4];
-  bool primed = false;
-  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
-    const uint64_t stripe = u / upc, sub = u - stripe * upc;
-    const BsReconArgs& a = desc_at(descs, stripe);
-    if (a.n_out == 0) continue;  // workgroup-uniform
-    const uint64_t off = sub * (4096u * P) + pair * 4096u + lane * 16u;
-    // the next unit's first input only when it is this stripe's (same block)
-    const uint64_t nu = u + gridDim.x, nsub = sub + gridDim.x;
-    const uint64_t next_off = PF && nu < total && nsub < upc
-                                  ? nsub * (4096u * P) + pair * 4096u + lane * 16u
-                                  : ~0ull;
-    if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane, cur, primed, next_off);
-    else primed = recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane, cur, primed, next_off);
+  if constexpr (PF) {
+    u32x4 cur[4];
+    bool primed = false;
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+      const uint64_t stripe = u / upc, sub = u - stripe * upc;
+      const BsReconArgs& a = desc_at(descs, stripe);
+      if (a.n_out == 0) continue;  // workgroup-uniform
+      const uint64_t off = sub * (4096u * P) + pair * 4096u + lane * 16u;
+      // the next unit's first input only when it is this stripe's (same block)
+      const uint64_t nu = u + gridDim.x, nsub = sub + gridDim.x;
+      const uint64_t next_off =
+          nu < total && nsub < upc ? nsub * (4096u * P) + pair * 4096u + lane * 16u : ~0ull;
+      if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P, true>(a, off, lds, pair, lane, cur, primed, next_off);
+      else primed = recon_pair_unit<C, NT, 0, P, true>(a, off, lds, pair, lane, cur, primed, next_off);
+    }
+  } else {
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+      const uint64_t stripe = u / upc, sub = u - stripe * upc;
+      const BsReconArgs& a = desc_at(descs, stripe);
+      if (a.n_out == 0) continue;  // workgroup-uniform
+      const uint64_t off = sub * (4096u * P) + pair * 4096u + lane * 16u;
+      u32x4 cur[4];
+      if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, off, lds, pair, lane, cur, false, ~0ull);
+      else recon_pair_unit<C, NT, 0, P>(a, off, lds, pair, lane, cur, false, ~0ull);
+    }
   }
 }
 
