@@ -72,7 +72,7 @@ int rse_last_device_error(void);
 /* Library version string. */
 const char *rse_version(void);
 /* Identity of the last coding kernel this thread launched, e.g. "bitslice gf8
- * 10+4 v1 nt1" (compiled-in bit-sliced), "bitslice-jit gf16 12+8" (specialised
+ * 10+4 v5 nt1" (compiled-in bit-sliced), "bitslice-jit gf16 12+8" (specialised
  * at run time), "table gf8 50+20 fused nt1"; "" before the first launch.
  * Diagnostics: profiles are attributed to the kernel that actually ran. */
 const char *rse_last_kernel(void);

@@ -21,9 +21,12 @@
 namespace rse {
 namespace {
 
-// bitslice_kernel variant (tools/tune.py sweeps): GF(2^8) 1 (scheduling
-// barrier); GF(2^16), VALU-heavier, 0 (the scheduler's own interleaving)
-constexpr int kBsDefaultVariant8 = 1, kBsDefaultVariant16 = 0;
+// bitslice_kernel variant (tools/tune.py sweeps): GF(2^8) 5 (two inputs in
+// flight per lane: 10+4 x 16 MiB 6014-6072 GB/s against 5961-5994 for 1, the
+// scheduling barrier, in three processes on two boxes, profiles/r03/s12, s13;
+// 10+2 x 1 MiB the same within noise); GF(2^16), VALU-heavier, 0 (the
+// scheduler's own interleaving)
+constexpr int kBsDefaultVariant8 = 5, kBsDefaultVariant16 = 0;
 
 // ------------------------------------------------------- compiled codecs
 // The code structs of the compiled codecs -- their parity rows (core.rs:430-436,

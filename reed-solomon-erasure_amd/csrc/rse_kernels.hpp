@@ -332,7 +332,7 @@ int set_option(int key, int64_t value);
 int64_t get_option(int key);
 void count_bitslice_launch();  // RSE_OPT_BITSLICE_LAUNCHES
 // Identity of the last coding kernel launched on this thread ("bitslice gf8
-// 10+4 v1 nt1", "table gf16 20+8 fused nt1", ...): rse_last_kernel().
+// 10+4 v5 nt1", "table gf16 20+8 fused nt1", ...): rse_last_kernel().
 void note_kernel(const char* fmt, ...);
 const char* last_kernel();
 

@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def run(counter, outdir, bench_args):
-    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "gf8_code|gf8_pipe|bitslice_kernel",
+    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "gf8_code|gf8_pipe|bitslice_kernel|bitslice_deep_kernel",
            "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-extras"] + bench_args
     out = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
