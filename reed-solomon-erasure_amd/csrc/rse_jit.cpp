@@ -465,7 +465,12 @@ bool build_with_helper(const std::string& src, const std::string& key, int slot,
   for (auto& a : args) argv.push_back(&a[0]);
   argv.push_back(nullptr);
   pid_t pid = 0;
-  if (g_unloading.load() || posix_spawn(&pid, helper.c_str(), nullptr, nullptr, argv.data(), environ) != 0) {
+  if (g_unloading.load()) {  // completes as failed; never handed to in-process hiprtc
+    unlink(src_path.c_str());
+    out->log = "library unloading";
+    return true;
+  }
+  if (posix_spawn(&pid, helper.c_str(), nullptr, nullptr, argv.data(), environ) != 0) {
     unlink(src_path.c_str());
     return false;
   }
@@ -523,7 +528,9 @@ std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
     out->ok = true;
     ++g_cache_hits;
   } else {
-    if (!build_with_helper(src, key, slot, out.get())) {
+    // at unload (the source can take seconds to generate for a wide codec, so
+    // the process may be exiting by now) the build completes as failed
+    if (!build_with_helper(src, key, slot, out.get()) && !g_unloading.load()) {
       build_in_process(src, out.get());
       if (out->ok && disk) {  // cache it (atomic: another process may read it)
         const std::string tmp = cache_dir() + "/" + key + "." + std::to_string(getpid()) + ".tmp";
