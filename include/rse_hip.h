@@ -340,6 +340,10 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_RECON_DEPTH 27       /* syndrome reconstruct: inputs in flight per lane (1..4) */
 #define RSE_OPT_SYNC_EVENT 30        /* 1: verify calls wait on an event recorded after their
                                         kernels instead of synchronising the stream (A/B; 0 default) */
+#define RSE_OPT_SPIN_WAIT 31         /* 1 (default): a verify that is one compiled check-kernel
+                                        launch signals its completion through a word of pinned host
+                                        memory, which the call polls instead of synchronising the
+                                        stream; 0: synchronise (A/B) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

@@ -41,6 +41,7 @@ template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, 
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
   bitslice_body<C, NT, SB, XC, XM, WT, W4, false, CE>(a, chunks_per_stripe);
+  if constexpr (CE) signal_done(a);
 }
 
 template <class C, int D>
@@ -450,6 +451,8 @@ static const BsShape kBsShapes[] = {
 
 }  // namespace
 
+thread_local bool t_done_armed = false;
+
 // Compute units of the current device (cached per device).
 uint32_t device_cus() {
   static std::atomic<uint32_t> cus[64];  // zero-initialised (static storage)
@@ -478,6 +481,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   hipFunction_t j16 = nullptr, j4 = nullptr;
   bool compiled = false;
   int vopt_used = -1;
+  bool chk = false;  // f16 is the compiled check kernel (it reads a.done)
   for (const BsShape& sh : kBsShapes) {
     if (a.accumulate) break;
     if (sh.field != field || sh.k != a.n_in || sh.p != a.n_out) continue;
@@ -491,7 +495,10 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                                      : (field == 16 ? kBsDefaultVariant16 : kBsDefaultVariant8);
     f16 = sh.fn[v][nt ? 1 : 0];
     if (!f16) f16 = sh.fn[v][1];
-    if (a.mode != kStore && vopt < 0 && nt) f16 = sh.chk;
+    if (a.mode != kStore && vopt < 0 && nt) {
+      f16 = sh.chk;
+      chk = true;
+    }
     vopt_used = v;
     f4 = sh.w4;
     compiled = true;
@@ -540,8 +547,19 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     note_kernel("bitslice-jit gf%d %u+%u%s%s", field, a.n_in, a.n_out, a.accumulate ? " acc" : "",
                 cps16 ? "" : " w4");
   if (cps16) {
-    const hipError_t e = launch(f16, j16, a, cps16, cps16 * a.n_stripes);
+    // a verify's completion word (run_check): armed only when this launch is
+    // the whole job, else cleared so that the kernel does not signal early
+    const bool arm = a.done && chk && a.n_vec == cps16 * kV16 && a.len == a.n_vec * 16u;
+    hipError_t e;
+    if (a.done && !arm) {
+      CodeArgs c = a;
+      c.done = c.done_count = nullptr;
+      e = launch(f16, j16, c, cps16, cps16 * a.n_stripes);
+    } else {
+      e = launch(f16, j16, a, cps16, cps16 * a.n_stripes);
+    }
     if (e != hipSuccess) return e;
+    t_done_armed = arm;
     *done = cps16 * kBsChunk;
   }
   if (cps4 && (f4 || j4)) {

@@ -145,6 +145,8 @@ struct Job {
   uint64_t stripe_stride;
   size_t n_stripes;
   bool per_stripe = false;  // CHECK modes: one mismatch word per stripe (verify_flat)
+  uint32_t* done = nullptr;        // CHECK modes: completion word (run_check)
+  uint32_t* done_count = nullptr;  //   and its device workgroup count
 };
 
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, size_t len, uint32_t* mismatch,
@@ -175,6 +177,8 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
   a.mode = mode;
   a.accumulate = acc ? 1u : 0u;
   a.per_stripe = j.per_stripe ? 1u : 0u;
+  a.done = j.done;
+  a.done_count = j.done_count;
   a.n_stripes = 0;
   hipError_t e = hipSuccess;
   for (size_t done = 0; done < j.n_stripes && e == hipSuccess;) {
@@ -339,6 +343,7 @@ struct Scratch {
   std::vector<hipEvent_t> h2d, coded, d2h;
   hipEvent_t start = nullptr;
   hipEvent_t done = nullptr;  // run_check's completion event (RSE_OPT_SYNC_EVENT)
+  uint32_t* count = nullptr;  // run_check's device workgroup count (signal_done), zero when idle
   uint8_t* dbuf = nullptr;
   size_t dbytes = 0;
 };
@@ -360,6 +365,7 @@ void destroy_scratch(Scratch* s) {  // idle: its last call synchronised
   if (s->done) (void)hipEventDestroy(s->done);
   if (s->own) (void)hipStreamDestroy(s->own);
   if (s->dbuf) (void)hipFree(s->dbuf);
+  if (s->count) (void)hipFree(s->count);
   if (s->wh) (void)hipHostFree(s->wh);
   delete s;
 }
@@ -494,16 +500,43 @@ int run_check(Job j, hipStream_t s, int* ok) {
   const size_t words = j.per_stripe ? j.n_stripes : 1;
   Lease lease;
   RSE_HIP(lease.acquire());
-  RSE_HIP(lease_words(lease.get(), words));
+  RSE_HIP(lease_words(lease.get(), words + 1));  // + the completion word
   uint32_t* wh = lease->wh;
-  std::memset(wh, 0, words * sizeof(uint32_t));  // leased: no kernel uses them now
+  std::memset(wh, 0, (words + 1) * sizeof(uint32_t));  // leased: no kernel uses them now
   j.mismatch = lease->wd;
+  // RSE_OPT_SPIN_WAIT: offer the kernel the completion word; launch_bitslice
+  // arms it when one compiled check-kernel launch is the whole verify
+  if (!j.per_stripe && rse::get_option(31)) {
+    if (!lease->count) {
+      RSE_HIP(hipMalloc(reinterpret_cast<void**>(&lease->count), sizeof(uint32_t)));
+      RSE_HIP(hipMemset(lease->count, 0, sizeof(uint32_t)));
+    }
+    j.done = lease->wd + words;
+    j.done_count = lease->count;
+  }
+  rse::t_done_armed = false;
   int rc = run_job(j, s);
+  const bool armed = rse::t_done_armed;
   // kernels already queued may still store into the words: drain them before
-  // the lease returns them to the pool.  RSE_OPT_SYNC_EVENT 1: wait on an
-  // event recorded after them instead of on the whole stream (A/B)
+  // the lease returns them to the pool.  Armed: the kernel's last workgroup
+  // stores the completion word after every verdict store (rse_device.hpp
+  // signal_done); poll it, asking the stream now and then (a launch that
+  // failed, or other work queued behind ours, ends the wait the usual way).
+  // RSE_OPT_SYNC_EVENT 1: wait on an event recorded after them instead of on
+  // the whole stream (A/B)
   hipError_t se = hipSuccess;
-  if (rse::get_option(30)) {
+  if (armed && rc == RSE_OK) {
+    const volatile uint32_t* dw = wh + words;
+    for (uint32_t n = 1; *dw == 0; ++n) {
+      __builtin_ia32_pause();
+      if ((n & 1023u) == 0 && (se = hipStreamQuery(s)) != hipErrorNotReady) break;
+    }
+    if (se == hipErrorNotReady) se = hipSuccess;
+    if (se == hipSuccess && *dw == 0) {  // finished without signalling: rezero the count
+      se = hipMemsetAsync(lease->count, 0, sizeof(uint32_t), s);
+      if (se == hipSuccess) se = hipStreamSynchronize(s);
+    }
+  } else if (rse::get_option(30)) {
     if (!lease->done) se = hipEventCreateWithFlags(&lease->done, hipEventDisableTiming);
     if (se == hipSuccess) se = hipEventRecord(lease->done, s);
     if (se == hipSuccess) se = hipEventSynchronize(lease->done);

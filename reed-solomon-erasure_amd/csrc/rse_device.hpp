@@ -151,6 +151,33 @@ __device__ __forceinline__ void flag_mismatch(uint32_t* p) {
   *reinterpret_cast<volatile uint32_t*>(p) = 1u;
 }
 
+// Completion of a one-launch verify (CodeArgs::done, armed by run_check): the
+// last workgroup to get here stores 1 into a.done, a word of pinned host
+// memory, after every workgroup's verdict stores have completed, and the host
+// spins on that word instead of waiting for the end-of-kernel signal.  Each
+// thread first waits until its own stores are acknowledged (the verdict words
+// are uncached host memory: acknowledged means visible to the host); the
+// workgroup count on the device word a.done_count (one agent-scope atomic per
+// workgroup) then makes the last workgroup's completion store come after every
+// acknowledgement.  No release fences: at agent scope they write back and
+// invalidate L2 in every wave (a 49 us verify took 188 with them); the
+// end-of-kernel release still orders everything for later work on the stream.
+// The last workgroup rezeroes the count for the next launch.  Every workgroup
+// of the launch calls this once, all threads.
+__device__ __forceinline__ void signal_done(const CodeArgs& a) {
+  if (!a.done) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(a.done_count, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (n == gridDim.x - 1) {
+      __hip_atomic_store(a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // One store per wave that saw a difference, on the word of stripe offset soff.
 __device__ __forceinline__ void flag_mismatch(bool diff, const CodeArgs& a, uint64_t soff) {
   const unsigned long long m = __ballot(diff);

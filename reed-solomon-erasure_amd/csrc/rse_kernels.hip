@@ -790,6 +790,7 @@ struct Options {
   int64_t recon_pairs = 1;        // syndrome reconstruct at 8 sigma rows on wave pairs
   int64_t wide_pairs = 1;         // wide GF(2^8) modules: networks over pairs of inputs
   int64_t sync_event = 0;         // verify calls wait on an event, not the stream (A/B)
+  int64_t spin_wait = 1;          // one-launch verifies: poll the completion word (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1089,6 +1090,8 @@ __global__ __launch_bounds__(256) void recon_plan_kernel(
     d.mode = kStore;
     d.accumulate = ib > 0 ? 1u : 0u;
     d.per_stripe = 0;
+    d.done = nullptr;
+    d.done_count = nullptr;
     for (uint32_t i = 0; i < ni; ++i) d.in[i] = sbase + (uint64_t)valid[32 * ib + i] * shard_bytes;
     for (uint32_t o = 0; o < no; ++o) {
       d.out[o] = sbase + (uint64_t)miss[16 * ob + o] * shard_bytes;
@@ -1276,6 +1279,7 @@ int set_option(int key, int64_t value) {
     case 28: g_opt.recon_pairs = value < 0 ? 0 : value > 3 ? 3 : value; return 0;
     case 29: g_opt.wide_pairs = value ? 1 : 0; return 0;
     case 30: g_opt.sync_event = value ? 1 : 0; return 0;
+    case 31: g_opt.spin_wait = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1318,6 +1322,7 @@ int64_t get_option(int key) {
     case 28: return g_opt.recon_pairs;
     case 29: return g_opt.wide_pairs;
     case 30: return g_opt.sync_event;
+    case 31: return g_opt.spin_wait;
     default: return -1;
   }
 }

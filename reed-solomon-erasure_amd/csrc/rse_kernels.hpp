@@ -47,6 +47,8 @@ struct CodeArgs {
   uint32_t accumulate;     // 1: out[r] ^= ... (ShardByShard / chunked inputs)
   uint32_t per_stripe;     // CHECK modes: 1 = mismatch[stripe] per stripe (verify_flat),
                            // 0 = one mismatch word for the launch
+  uint32_t* done;          // check kernels: completion word (rse_device.hpp signal_done)
+  uint32_t* done_count;    //   and its workgroup count; null: not armed
   // GF(2^8): coef[r][i] & 0xff.  GF(2^16): (coef_of_x << 8) | constant.
   uint16_t coef[kMaxOut][kMaxIn];
 };
@@ -217,6 +219,10 @@ hipError_t launch_recon_plan(int field, const uint16_t* d_parity, const uint8_t*
 
 // Table kernels only (launch_code minus the bit-sliced dispatch).
 hipError_t launch_table(int field, const CodeArgs& args, hipStream_t stream);
+
+// Set by launch_bitslice when it launched a check kernel with CodeArgs::done
+// armed (the launch is the whole job: the kernel signals its completion).
+extern thread_local bool t_done_armed;
 
 // Bit-sliced kernels (rse_bitslice.hip) for codecs whose parity rows are
 // compiled in or were specialised at run time (rse_jit.cpp): the whole 16 KiB

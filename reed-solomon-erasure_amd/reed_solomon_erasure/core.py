@@ -30,9 +30,18 @@ def _raise(status: int):
     raise DeviceError(status, msg, _lib.rse_last_device_error())
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(t: Optional[torch.Tensor] = None):
-    dev = t.device if t is not None else None
-    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    """torch's current stream on t's device (the current device for None or a
+    host tensor), as the address the C ABI takes."""
+    idx = t.get_device() if t is not None else -1
+    if idx < 0:
+        idx = torch.cuda.current_device()
+    if _raw_stream is not None:  # ~0.3 us against ~2 for a torch.cuda.Stream object
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(idx).cuda_stream
 
 
 def _elems(t: torch.Tensor, field: int) -> int:
@@ -66,8 +75,24 @@ def _check_flat(stripes: torch.Tensor, shard_len: int, n_stripes: int, total: in
         raise ValueError(f"stripes holds {stripes.numel()} bytes, {need} needed")
 
 
+_U8 = torch.uint8
+
+
 def _arrays(shards, field):
+    """The shards' device addresses and Rust slice lengths as C arrays.  One
+    pass over plain 1-D GF(2^8) device shards (the per-call cost of a
+    synchronous verify); anything else, including every invalid shard, goes
+    through _dev / _elems, whose errors are the API's."""
     n = len(shards)
+    if field == 8:
+        ptrs, lens = [], []
+        for s in shards:
+            if s.dtype is not _U8 or not s.is_cuda or not s.is_contiguous():
+                break
+            ptrs.append(s.data_ptr())
+            lens.append(s.numel())
+        else:
+            return (ctypes.c_void_p * max(1, n))(*ptrs), (ctypes.c_size_t * max(1, n))(*lens)
     ptrs = (ctypes.c_void_p * max(1, n))(*[_dev(s) for s in shards])
     lens = (ctypes.c_size_t * max(1, n))(*[_elems(s, field) for s in shards])
     return ptrs, lens

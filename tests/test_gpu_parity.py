@@ -325,6 +325,72 @@ def test_verify_detects_every_single_byte_corruption(R):  # tests/mod.rs:480-589
         assert r.verify(s)
 
 
+@pytest.mark.parametrize("spin", [1, 0])
+def test_verify_completion_word(R, spin):
+    """RSE_OPT_SPIN_WAIT: a verify that is one compiled check-kernel launch
+    (10+4, whole 16 KiB chunks) returns when the kernel's last workgroup stores
+    the completion word; the verdicts must match the stream-synchronised ones
+    call after call (the workgroup count rezeroes itself), at every grid size,
+    with verify_with_buffer's parity written, on shards with a 4 KiB tail (not
+    armed), and from threads verifying on their own streams at once."""
+    import threading
+    lib = R._lib.load()
+    rng = np.random.default_rng(31 + spin)
+    r = R.galois_8.ReedSolomon(10, 4)
+    lib.rse_set_option(31, spin)
+    try:
+        for n, grid in [(16384, 0), (1 << 20, 0), (3 * 16384, 1), (1 << 20, 7), (16384 + 4096, 0)]:
+            lib.rse_set_option(2, grid)
+            s = [dev(x) for x in rand_shards(rng, 14, n)]
+            r.encode(s)
+            for it in range(24):
+                i = int(rng.integers(0, 14))
+                j = int(rng.choice([0, n - 1, int(rng.integers(0, n))]))
+                bad = it % 3 != 0
+                old = s[i][j].item()
+                if bad:
+                    s[i][j] = old ^ int(rng.integers(1, 256))
+                assert r.verify(s) == (not bad), (n, grid, it)
+                if it % 4 == 1:
+                    buf = [torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(4)]
+                    assert r.verify_with_buffer(s, buf) == (not bad)
+                    want = [x.clone() for x in s]
+                    r.encode(want)
+                    assert all(torch.equal(a, b) for a, b in zip(want[10:], buf)), (n, grid, it)
+                s[i][j] = old
+            assert r.verify(s)
+        lib.rse_set_option(2, 0)
+        n = 1 << 20
+        stripes = [[dev(x) for x in rand_shards(rng, 14, n)] for _ in range(4)]
+        for st in stripes:
+            r.encode(st)
+        torch.cuda.synchronize()
+        stripes[1][12][77] ^= 1
+        stripes[3][0][n - 1] ^= 8
+        want = [True, False, True, False]
+        errors = []
+
+        def worker(t):
+            try:
+                stream = torch.cuda.Stream()
+                with torch.cuda.stream(stream):
+                    for _ in range(40):
+                        if r.verify(stripes[t]) != want[t]:
+                            errors.append(t)
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+    finally:
+        lib.rse_set_option(31, 1)
+        lib.rse_set_option(2, 0)
+
+
 # ------------------------------------------------------ shard by shard / single
 @pytest.mark.parametrize("field,k,p", [(8, 10, 4), (8, 5, 3), (16, 6, 2)])
 def test_shard_by_shard_same_as_encode(R, field, k, p):  # tests/mod.rs:1165-1317

@@ -23,6 +23,10 @@ int main(int argc, char** argv) {
     if (rse_set_option(RSE_OPT_SYNC_EVENT, std::atol(argv[2]))) return 8;
     std::printf("sync event %s\n", argv[2]);
   }
+  if (argc > 3) {  // RSE_OPT_SPIN_WAIT
+    if (rse_set_option(RSE_OPT_SPIN_WAIT, std::atol(argv[3]))) return 9;
+    std::printf("spin wait %s\n", argv[3]);
+  }
   rse_codec* c = nullptr;
   if (rse_codec_new(RSE_FIELD_GF8, k, p, &c)) return 1;
   uint8_t* buf = nullptr;
