@@ -19,7 +19,11 @@
  *  - On any error nothing is written (core.rs:673-676).
  *  - Work is enqueued on `stream` (a hipStream_t; NULL = the legacy default
  *    stream) and runs asynchronously, except verify*, whose boolean result
- *    requires a stream synchronisation before returning.  Each call runs on
+ *    requires waiting before returning: for the stream's work up to and
+ *    including the check, or (RSE_OPT_SPIN_WAIT, one compiled check-kernel
+ *    launch) for the check kernel's completion word, stored after every one of
+ *    its memory accesses has completed.  Either way the shards may be reused
+ *    once the call returns.  Each call runs on
  *    the device that owns `stream` (NULL: the current device); the caller's
  *    current device is restored on return.
  *  - A codec is immutable after rse_codec_new except for its mutex-guarded
@@ -119,7 +123,7 @@ int rse_encode_single_sep(const rse_codec *codec, size_t i_data, const void *sin
                           size_t single_len, void *const *parity, const size_t *parity_lens,
                           size_t n_parity, rse_stream_t stream);
 /* verify (core.rs:637-651): *ok = 1 iff the parity matches.  Reads k+p shards
- * once, writes nothing.  Synchronises `stream`. */
+ * once, writes nothing.  Waits for the check (see above). */
 int rse_verify(const rse_codec *codec, const void *const *shards, const size_t *lens,
                size_t n_shards, int *ok, rse_stream_t stream);
 /* verify_with_buffer (core.rs:654-669): on RSE_OK the buffer holds the correct
