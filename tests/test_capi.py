@@ -284,3 +284,29 @@ def test_code_shards_refuses_unequal_lengths():
         with pytest.raises(RSError) as ei:
             R.core.code_shards_host(8, [[1] * len(ins)] * len(outs), ins, outs)
         assert ei.value.error == Error.IncorrectShardSize
+
+
+def test_every_header_option_is_readable():
+    """Every RSE_OPT_* key include/rse_hip.h declares answers rse_get_option
+    (-1 is the answer for an unknown key), and the round-3 switches start at
+    their documented defaults: wave-pair reconstruct and paired wide networks
+    on, the event wait off, the verify completion word on."""
+    import re
+    hdr = open(os.path.join(ROOT, "include", "rse_hip.h")).read()
+    keys = {m.group(1): int(m.group(2))
+            for m in re.finditer(r"#define (RSE_OPT_[A-Z0-9_]+) (\d+)", hdr)}
+    assert len(keys) >= 30
+    for name, key in keys.items():  # KERNEL_VARIANT's default is -1 ("the default variant")
+        assert L.rse_get_option(key) != -1 or name == "RSE_OPT_KERNEL_VARIANT", name
+    assert L.rse_get_option(99) == -1
+    assert L.rse_set_option(99, 1) != 0
+    want = {"RSE_OPT_RECON_PAIRS": 1, "RSE_OPT_WIDE_PAIRS": 1, "RSE_OPT_SYNC_EVENT": 0,
+            "RSE_OPT_SPIN_WAIT": 1}
+    for name, v in want.items():
+        assert L.rse_get_option(keys[name]) == v, name
+    old = L.rse_get_option(keys["RSE_OPT_SPIN_WAIT"])
+    try:
+        assert L.rse_set_option(keys["RSE_OPT_SPIN_WAIT"], 0) == 0
+        assert L.rse_get_option(keys["RSE_OPT_SPIN_WAIT"]) == 0
+    finally:
+        L.rse_set_option(keys["RSE_OPT_SPIN_WAIT"], old)
