@@ -513,8 +513,11 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     j4 = a.accumulate ? jf.enc4_acc : jf.enc4;
     if (!j16) return hipSuccess;
   }
-  // tools/tune.py sweeps: GF(2^8) 4096 workgroups, GF(2^16) (2 waves/SIMD) 8192
-  const uint64_t g0 = grid > 0 ? (uint64_t)grid : (field == 16 ? 8192u : 4096u);
+  // tools/tune.py sweeps: GF(2^8) 4096 workgroups (16384 at <= 2 outputs: 10+2
+  // x 1 MiB +0.8-1.1 % in two processes, profiles/r03/s12, s13), GF(2^16)
+  // (2 waves/SIMD) 8192
+  const uint64_t g0 = grid > 0 ? (uint64_t)grid
+                               : (field == 16 ? 8192u : a.n_out <= 2 ? 16384u : 4096u);
   // A launch of one to two rounds of the resident workgroups (one 10+4 x 16
   // MiB stripe: 1024 chunks against 768) runs as one round of resident
   // workgroups, grid-striding over the rest, instead of a full round plus a
@@ -603,7 +606,10 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
   const uint64_t cps = n_vec / (kBsChunk / 16);
   const uint64_t total = cps * a.n_stripes;
   const int64_t grid = get_option(2);
-  uint64_t gx = grid > 0 ? (uint64_t)grid : 8192u;  // tools/tune.py --op reconstruct sweeps
+  // tools/tune.py --op reconstruct --patterns 0 sweeps: GF(2^8) 10+4 x 16 MiB at
+  // 32768 workgroups against 8192, 2 lost 5.83 against 5.72 TB/s, 4 lost 5.53
+  // against 5.27 (profiles/r03/s17/); GF(2^16) 8192
+  uint64_t gx = grid > 0 ? (uint64_t)grid : (field == 8 ? 32768u : 8192u);
   if (gx > total) gx = total;
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
   // rows needed: sigma (R and missing parity); NS = smallest compiled cover
