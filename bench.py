@@ -522,25 +522,139 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def timed_gbps(fn, nbytes, stream, reps=5):
-    """Algorithmic GB/s (1e9) of fn() over `reps` back-to-back calls, HIP
-    events on the launch stream, after one untimed call."""
+def _sync():
     import torch
-    fn()
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def timed_ms(fn, reps, stream=None):
+    """Mean milliseconds per call of `reps` back-to-back fn() calls, by HIP
+    events on the launch stream (None: the current stream)."""
+    import torch
+    _sync()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
     for _ in range(reps):
         fn()
     b.record(stream)
     torch.cuda.synchronize()
-    return round(nbytes / (a.elapsed_time(b) / reps * 1e-3) / 1e9, 1)
+    return a.elapsed_time(b) / reps
+
+
+def timed_gbps(fn, nbytes, stream, reps=5, prepare=None):
+    """Algorithmic GB/s (1e9) of fn() over `reps` back-to-back calls (HIP
+    events on the launch stream) after one untimed call.  `prepare` runs
+    between the untimed call and the timed ones (outside the timed region):
+    the reconstruct legs poison the shards the timed calls must rebuild."""
+    fn()
+    if prepare is not None:
+        prepare()
+    return round(nbytes / (timed_ms(fn, reps, stream) * 1e-3) / 1e9, 1)
+
+
+# --------------------------------------------- correctness of the extra legs
+# The driver-run bench line is the hardware record, so every reconstruct and
+# verify leg on it proves its own output: erased shards are overwritten with a
+# poison byte before the timed calls, and every rebuilt shard is compared with
+# its synthetic bytes afterwards; the verify legs see corrupted stripes that
+# must come back false.  A kernel that writes nothing fails these checks.
+POISON = 0xA5
+
+
+def poison(v, n_stripes, shards):
+    """Overwrite shards `shards` of the first `n_stripes` stripes of the
+    stripe view v[stripe, shard, byte] with POISON."""
+    for i in shards:
+        v[:n_stripes, i].fill_(POISON)
+
+
+def rebuilt_ok(v, n_stripes, shards, stripe_ids, fill):
+    """True iff shard i of stripe s holds the synthetic bytes of (SEED,
+    shard_id(stripe_ids[s], i)) for every s < n_stripes and i in `shards`.
+    `fill(t, seed, shard)` regenerates them (the device fill kernel, a
+    separate kernel from the one under test) into a scratch shard."""
+    import torch
+    tmp = torch.empty(v.shape[-1], dtype=torch.uint8, device=v.device)
+    for s in range(n_stripes):
+        for i in shards:
+            fill(tmp, SEED, shard_id(stripe_ids[s], i))
+            if not torch.equal(tmp, v[s, i]):
+                return False
+    return True
+
+
+def digests_ok(v, shards, want):
+    """Stripe 0's shards `shards` against SHA-256 digests `want` (tests/golden)."""
+    got = [hashlib.sha256(v[0, i].cpu().numpy().tobytes()).hexdigest() for i in shards]
+    return got == list(want)
+
+
+def reconstruct_leg(r, v, k, erased, elems, n_stripes, stream, fill, stripe_ids,
+                    want_digests=None, reps=5):
+    """reconstruct_data_flat of `n_stripes` stripes of the view v with data
+    shards `erased` lost (one shared pattern, core.rs:680-695), timed; the
+    erased shards are poisoned before the timed calls and checked after them:
+    every rebuilt shard of every stripe against its synthetic bytes, and
+    stripe 0's against the fixture digests when given."""
+    T = v.shape[1]
+    flat = v[:n_stripes].reshape(-1)
+    present = [i not in erased for i in range(T)]
+    gbps = timed_gbps(lambda: r.reconstruct_data_flat(flat, elems, n_stripes, present),
+                      n_stripes * (k + len(erased)) * v.shape[-1], stream, reps=reps,
+                      prepare=lambda: poison(v, n_stripes, erased))
+    out = {"GB_per_s": gbps,
+           "rebuilt_ok_all_stripes": rebuilt_ok(v, n_stripes, erased, stripe_ids, fill)}
+    if want_digests is not None:
+        out["rebuilt_stripe0_vs_digests"] = digests_ok(v, erased, want_digests)
+    return out
+
+
+def verify_leg(r, v, k, p, L, n_stripes, reps=5):
+    """verify (one synchronous call per stripe, core.rs:637-651) and
+    verify_flat (one pass) over `n_stripes` stripes, two of them corrupted --
+    one byte of a parity shard in one, of a data shard in another -- which
+    must come back false while every other stripe comes back true."""
+    bad = {n_stripes // 3: k + p - 1, (2 * n_stripes) // 3: k // 2}  # stripe -> shard
+    offs = {s: (L // 2 + 4097 * s) % L for s in bad}
+    for s, i in bad.items():
+        v[s, i, offs[s]] ^= 0x5A
+    want = [s not in bad for s in range(n_stripes)]
+    flat = v[:n_stripes].reshape(-1)
+    shards = [[v[s_, i] for i in range(k + p)] for s_ in range(n_stripes)]
+    try:
+        _sync()
+        t0 = time.perf_counter()
+        got = [r.verify(sh) for sh in shards]
+        dt = time.perf_counter() - t0
+        flat_first = [bool(x) for x in r.verify_flat(flat, L, n_stripes)]
+        res = {}
+
+        def run():
+            res["oks"] = r.verify_flat(flat, L, n_stripes)
+        ms = timed_ms(run, reps)
+        flat_got = [bool(x) for x in res["oks"]]
+    finally:
+        for s, i in bad.items():
+            v[s, i, offs[s]] ^= 0x5A
+    nbytes = n_stripes * (k + p) * L
+    corrupted = sorted(bad)
+    return ({"what": f"verify, {n_stripes} stripes, one call each (synchronous); stripes "
+                     f"{corrupted} corrupted", "corrupted_stripes": corrupted,
+             "verdicts_ok": got == want,
+             "algorithmic_GB_per_s": round(nbytes / dt / 1e9, 1)},
+            {"what": f"verify_flat, {n_stripes} stripes in one pass (reads k+p shards); stripes "
+                     f"{corrupted} corrupted", "corrupted_stripes": corrupted,
+             "verdicts_ok": flat_got == want and flat_first == want,
+             "algorithmic_GB_per_s": round(nbytes / (ms * 1e-3) / 1e9, 1)})
 
 
 def other_configs(stream):
     """BASELINE.json configs[1] (galois_8 10+2 x 1 MiB) and configs[4]
     (galois_16 20+8 x 4 MiB encode/reconstruct) on this GPU, each with stripe
-    0's parity checked against the reference digests of tests/golden."""
+    0's parity checked against the digests of tests/golden (GF(2^8): the
+    reference's own kernel; GF(2^16): the restatement), and every reconstruct
+    leg's rebuilt shards checked after poisoning."""
     import torch
     import reed_solomon_erasure as R
     from reed_solomon_erasure.core import fill_splitmix
@@ -557,34 +671,37 @@ def other_configs(stream):
         r = R.core.ReedSolomon(k, p, field)
         elems = nbytes // (field // 8)
         enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream)
-        want = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]["parity_sha256"]
-        got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
+        fs = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]
         d = {"workload": f"gf{field} {k}+{p} x {nbytes // MiB} MiB, {stripes} stripes/launch",
              "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
-             "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),
-             "parity_check_vs_reference": got == want}
+             "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4)}
+        d["parity_check_vs_reference" if field == 8 else "parity_check_vs_restatement"] = \
+            digests_ok(v, range(k, T), fs["parity_sha256"])
         if field == 16:
             # first uses of an erasure pattern (syndrome kernels, no decode-
             # pattern kernel): 8 data shards lost (bit-sliced mixing) and 4
+            ids = list(range(stripes))
             for lost in (8, 4):
                 erased = list(range(lost))
-                present = [i not in erased for i in range(T)]
-                rb = stripes * (k + lost) * nbytes
                 lib.rse_set_option(11, 0)
-                d[f"reconstruct_{lost}_erased_syndrome_GB_per_s"] = timed_gbps(
-                    lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
-                lib.rse_set_option(11, 1)
-            erased = [0, 1, 2, 3]
-            present = [i not in erased for i in range(T)]
-            rb = stripes * (k + len(erased)) * nbytes
+                try:
+                    leg = reconstruct_leg(r, v, k, erased, elems, stripes, stream, fill_splitmix,
+                                          ids, fs["data_sha256"][:lost])
+                finally:
+                    lib.rse_set_option(11, 1)
+                d[f"reconstruct_{lost}_erased_syndrome_GB_per_s"] = leg["GB_per_s"]
+                d[f"reconstruct_{lost}_erased_syndrome_rebuilt_ok"] = (
+                    leg["rebuilt_ok_all_stripes"] and leg["rebuilt_stripe0_vs_digests"])
             old = lib.rse_get_option(9)
             lib.rse_set_option(9, 2)
-            d["reconstruct_4_erased_cached_pattern_GB_per_s"] = timed_gbps(
-                lambda: r.reconstruct_data_flat(buf, elems, stripes, present), rb, stream)
-            lib.rse_set_option(9, old)
-            ok = [hashlib.sha256(v[0, i].cpu().numpy().tobytes()).hexdigest() for i in erased]
-            d["reconstruct_check_vs_reference"] = ok == g["full_size"][f"gf16_20_8_{nbytes}"][
-                "data_sha256"][:len(erased)]
+            try:
+                leg = reconstruct_leg(r, v, k, [0, 1, 2, 3], elems, stripes, stream,
+                                      fill_splitmix, ids, fs["data_sha256"][:4])
+            finally:
+                lib.rse_set_option(9, old)
+            d["reconstruct_4_erased_cached_pattern_GB_per_s"] = leg["GB_per_s"]
+            d["reconstruct_4_erased_cached_pattern_rebuilt_ok"] = (
+                leg["rebuilt_ok_all_stripes"] and leg["rebuilt_stripe0_vs_digests"])
         out[f"gf{field}_{k}_{p}"] = d
         del buf, v
         torch.cuda.empty_cache()
@@ -617,12 +734,12 @@ def wide_config(stream, g, field, k, p):
     elems = nbytes // (field // 8)
     enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream)
     want = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]["parity_sha256"]
-    got = [hashlib.sha256(v[0, k + i].cpu().numpy().tobytes()).hexdigest() for i in range(p)]
     d = {"workload": f"gf{field} {k}+{p} x 1 MiB, {stripes} stripes/launch", "kernels": kind,
          "kernel": last_kernel(), "build_seconds": round(build_s, 1),
          "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
-         "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4),
-         "parity_check_vs_reference": got == want}
+         "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4)}
+    d["parity_check_vs_reference" if field == 8 else "parity_check_vs_restatement"] = \
+        digests_ok(v, range(k, T), want)
     del buf, v
     torch.cuda.empty_cache()
     return d
@@ -633,74 +750,55 @@ def R_lib():
     return R._lib.load()
 
 
-def extra_legs(r, v, k, p, L, n_stripes, stream):
-    """Reconstruct (data shards 0 and 1 erased, BASELINE config 3) and the
-    pinned-host end-to-end encode (PCIe-inclusive; never `value`)."""
+def extra_legs(r, v, k, p, L, n_stripes, stream, stripe0=0):
+    """Reconstruct (data shards 0 and 1 erased, BASELINE config 3), verify
+    with corrupted stripes, and the pinned-host end-to-end legs
+    (PCIe-inclusive; never `value`).  Every reconstruct leg poisons the erased
+    shards before its timed calls and checks every rebuilt shard after them."""
     import torch
+    from reed_solomon_erasure.core import fill_splitmix
     out = {}
-    present = [i not in (0, 1) for i in range(k + p)]
-    flat = v[:n_stripes].reshape(-1)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     lib = R_lib()
+    ids = [stripe0 + s for s in range(n_stripes)]
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
+    fs = g["full_size"].get(f"gf8_{k}_{p}_{L}")
+    want = fs["data_sha256"][:2] if (fs and stripe0 == 0) else None
     lib.rse_set_option(11, 0)  # decode-pattern kernels off: the syndrome kernel
-    r.reconstruct_data_flat(flat, L, n_stripes, present)
-    torch.cuda.synchronize()
-    reps = 5
-    a.record(stream)
-    for _ in range(reps):
-        r.reconstruct_data_flat(flat, L, n_stripes, present)
-    b.record(stream)
-    torch.cuda.synchronize()
-    lib.rse_set_option(11, 1)
-    ms = a.elapsed_time(b) / reps
-    rb = n_stripes * (k + 2) * L
+    try:
+        leg = reconstruct_leg(r, v, k, [0, 1], L, n_stripes, stream, fill_splitmix, ids, want)
+    finally:
+        lib.rse_set_option(11, 1)
     out["reconstruct"] = {"what": "reconstruct_data, data shards 0,1 erased, first uses of the "
-                                  "pattern (bit-sliced syndrome kernel)",
-                          "stripes": n_stripes, "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
-                          "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
+                                  "pattern (bit-sliced syndrome kernel); erased shards poisoned "
+                                  "before the timed calls", "stripes": n_stripes,
+                          "MB_per_s": round(leg["GB_per_s"] * 1e9 / MiB, 1),
+                          "algorithmic_GB_per_s": leg["GB_per_s"],
+                          "rebuilt_ok_all_stripes": leg["rebuilt_ok_all_stripes"],
+                          "rebuilt_stripe0_vs_reference": leg.get("rebuilt_stripe0_vs_digests")}
     # a repeated pattern: its decode rows get their own specialised kernel
     # (rse_jit.cpp), like the reference's decode-matrix cache (core.rs:697-731);
     # RSE_OPT_JIT 2 waits for that build before timing
     old = lib.rse_get_option(9)
     lib.rse_set_option(9, 2)
     p0 = lib.rse_get_option(12)
-    r.reconstruct_data_flat(flat, L, n_stripes, present)
-    torch.cuda.synchronize()
-    a.record(stream)
-    for _ in range(reps):
-        r.reconstruct_data_flat(flat, L, n_stripes, present)
-    b.record(stream)
-    torch.cuda.synchronize()
-    lib.rse_set_option(9, old)
-    ms = a.elapsed_time(b) / reps
+    reps = 5
+    try:
+        leg = reconstruct_leg(r, v, k, [0, 1], L, n_stripes, stream, fill_splitmix, ids, want,
+                              reps=reps)
+    finally:
+        lib.rse_set_option(9, old)
     out["reconstruct_cached_pattern"] = {
         "what": "reconstruct_data, data shards 0,1 erased, repeated pattern (decode-pattern "
-                "kernel specialised at run time)", "stripes": n_stripes,
-        "pattern_kernel": lib.rse_get_option(12) - p0 == reps + 1,
-        "MB_per_s": round(rb / (ms * 1e-3) / MiB, 1),
-        "algorithmic_GB_per_s": round(rb / (ms * 1e-3) / 1e9, 1)}
-    # verify (check mode: k+p reads, no writes), stripe by stripe as the API is
+                "kernel specialised at run time); erased shards poisoned before the timed calls",
+        "stripes": n_stripes, "pattern_kernel": lib.rse_get_option(12) - p0 == reps + 1,
+        "MB_per_s": round(leg["GB_per_s"] * 1e9 / MiB, 1),
+        "algorithmic_GB_per_s": leg["GB_per_s"],
+        "rebuilt_ok_all_stripes": leg["rebuilt_ok_all_stripes"],
+        "rebuilt_stripe0_vs_reference": leg.get("rebuilt_stripe0_vs_digests")}
+    # verify (check mode: k+p reads, no writes), stripe by stripe as the API
+    # is, and the same check over every stripe in one pass (rse_verify_flat)
     n_stripes = min(n_stripes, 64)
-    flat = v[:n_stripes].reshape(-1)
-    shards = [[v[s_, i] for i in range(k + p)] for s_ in range(n_stripes)]
-    assert all(r.verify(sh) for sh in shards[:2])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ok = all(r.verify(sh) for sh in shards)
-    dt = time.perf_counter() - t0
-    out["verify"] = {"what": f"verify, {n_stripes} stripes, one call each (synchronous)",
-                     "all_ok": ok, "algorithmic_GB_per_s": round(n_stripes * (k + p) * L / dt / 1e9, 1)}
-    # the same check over every stripe in one pass (rse_verify_flat)
-    assert r.verify_flat(flat, L, n_stripes).all()
-    a.record(stream)
-    for _ in range(reps):
-        oks = r.verify_flat(flat, L, n_stripes)
-    b.record(stream)
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / reps
-    out["verify_flat"] = {"what": f"verify_flat, {n_stripes} stripes in one pass (reads k+p shards)",
-                          "all_ok": bool(oks.all()),
-                          "algorithmic_GB_per_s": round(n_stripes * (k + p) * L / (ms * 1e-3) / 1e9, 1)}
+    out["verify"], out["verify_flat"] = verify_leg(r, v, k, p, L, n_stripes, reps=reps)
     # end to end from pinned host memory: one stripe, H2D data, D2H parity
     hs = [v[0, i].cpu().pin_memory() for i in range(k)] + \
          [torch.empty(L, dtype=torch.uint8).pin_memory() for _ in range(p)]

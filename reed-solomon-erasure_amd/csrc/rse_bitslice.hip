@@ -551,8 +551,14 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
                 cps16 ? "" : " w4");
   if (cps16) {
     // a verify's completion word (run_check): armed only when this launch is
-    // the whole job, else cleared so that the kernel does not signal early
-    const bool arm = a.done && chk && a.n_vec == cps16 * kV16 && a.len == a.n_vec * 16u;
+    // the whole job, else cleared so that the kernel does not signal early.
+    // Only the plain check (kCheck) arms it: its stores are the verdict words
+    // alone, which the host reads itself.  verify_with_buffer (kCheckStore)
+    // writes parity into the caller's buffer, which other streams, devices or
+    // mapped-memory readers may read once the call returns, so it waits for
+    // the kernel's end-of-kernel release instead.
+    const bool arm = a.done && chk && a.mode == kCheck && a.n_vec == cps16 * kV16 &&
+                     a.len == a.n_vec * 16u;
     hipError_t e;
     if (a.done && !arm) {
       CodeArgs c = a;
@@ -590,6 +596,15 @@ int pair_groups() {
   const int64_t o = get_option(28);
   return o == 0 ? 0 : o == 2 ? 2 : 1;
 }
+// RSE_OPT_RECON_DEPTH (inputs in flight per lane in the syndrome kernels).  The
+// deep kernels mix by Horner's rule, so a depth above 1 applies only when the
+// mixing mode is a Horner mode (RSE_OPT_RECON_MIX >= kReconMixHorner), on the
+// shared-pattern and the per-stripe (batch) paths alike; it then selects the
+// deep Horner kernel in place of the mode's own.
+int recon_depth(int mix) {
+  return mix >= kReconMixHorner ? (int)get_option(27) : 1;
+}
+
 // index into BsShape::rec_pair / rec_desc_pair (option 28 = 3: prefetching variant)
 int pair_slot() {
   const int64_t o = get_option(28);
@@ -623,7 +638,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
       if (sh.rec[0][q] && (1u << q) >= need) slot = q;
     if (slot < 0) return hipSuccess;
     const int mix = (int)get_option(17);
-    const int depth = mix == kReconMixHorner ? (int)get_option(27) : 1;  // RSE_OPT_RECON_DEPTH
+    const int depth = recon_depth(mix);
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
     const int np = pair_groups();
@@ -690,7 +705,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
     compiled = true;
     for (uint32_t i = 0; i < k * p; ++i)
       if (parity_rows[i] != sh.m[i]) return hipSuccess;
-    const int depth = (int)get_option(27);  // RSE_OPT_RECON_DEPTH
+    const int depth = recon_depth((int)get_option(17));
     for (int q = 0; q < 4 && !sfn; ++q)
       if (sh.rec_desc[q] && (1u << q) >= need) {
         sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
@@ -699,6 +714,11 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
           sfn = sh.rec_desc_pair[pair_slot()];  // 8 sigma rows on wave pairs
           pairs = true;
         }
+        if (pairs)
+          note_kernel("bitslice-recon-batch gf%d %u+%u ns8 pairs%d", field, k, p, pair_groups());
+        else
+          note_kernel("bitslice-recon-batch gf%d %u+%u ns%d d%d", field, k, p, 1 << q,
+                      depth > 3 ? 3 : depth < 1 ? 1 : depth);
       }
     if (!sfn) return hipSuccess;
   }

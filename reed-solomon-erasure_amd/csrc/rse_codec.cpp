@@ -446,9 +446,13 @@ hipError_t lease_words(Scratch* s, size_t words) {
   return hipSuccess;
 }
 
+// The library stream of the synchronous slice hooks: a blocking stream, so its
+// work is ordered after what the caller queued on the null stream (as the
+// hooks' null-stream launches were before), while the call still waits for
+// this stream only.
 hipError_t lease_own_stream(Scratch* s, hipStream_t* out) {
   if (!s->own) {
-    const hipError_t e = hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking);
+    const hipError_t e = hipStreamCreateWithFlags(&s->own, hipStreamDefault);
     if (e != hipSuccess) return e;
   }
   *out = s->own;
@@ -1311,8 +1315,12 @@ class OnDevice {
 bool device_memory(const void* p, int* dev) {
   hipPointerAttribute_t a;
   std::memset(&a, 0, sizeof a);
+  // an unregistered host pointer is not an error here: clear the error the
+  // query leaves behind, but only when the caller had none pending (an
+  // earlier asynchronous launch failure must stay visible to them)
+  const hipError_t pending = hipPeekAtLastError();
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();  // an unregistered host pointer is not an error here
+    if (pending == hipSuccess) (void)hipGetLastError();
     return false;
   }
   if (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged) return false;

@@ -454,8 +454,10 @@ bool build_with_helper(const std::string& src, const std::string& key, int slot,
   if (helper.empty()) return false;
   const std::string& dir = private_dir();
   if (dir.empty()) return false;
-  char tag[32];
-  std::snprintf(tag, sizeof tag, ".%d", slot);
+  // the pid too: a process forked after the first build inherits the same
+  // private directory name, and parent and child must not share file paths
+  char tag[48];
+  std::snprintf(tag, sizeof tag, ".%d.%d", (int)getpid(), slot);
   const std::string src_path = dir + "/" + key + tag + ".hip";
   const std::string out_path = dir + "/" + key + tag + ".co";
   if (!write_file(src_path, src)) return false;

@@ -1,0 +1,176 @@
+"""The bench's correctness flags can fail.
+
+bench.py's reconstruct legs poison the erased shards before their timed calls
+and compare every rebuilt shard with its synthetic bytes afterwards; its verify
+legs corrupt two stripes that must come back false.  On CPU the codec is
+stubbed: a reconstruct that writes nothing, or writes wrong bytes, and a verify
+that always answers true, must turn the flags false, while a correct stand-in
+(the oracle, test infrastructure) turns them true.  The `gpu` test runs the
+same legs through the HIP library and asserts the flags are true.
+"""
+import hashlib
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import oracle as O
+
+K, P, L, N = 4, 2, 4096, 4
+
+
+def _cpu_fill(t, seed, shard):
+    t.copy_(torch.from_numpy(O.splitmix_bytes(seed, shard, t.numel())))
+
+
+def _cpu_timed_ms(fn, reps, stream=None):
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return max((time.perf_counter() - t0) / reps * 1e3, 1e-6)
+
+
+@pytest.fixture
+def cpu_bench(monkeypatch):
+    monkeypatch.setattr(bench, "timed_ms", _cpu_timed_ms)
+    monkeypatch.setattr(bench, "_sync", lambda: None)
+
+
+def _stripes():
+    """N encoded stripes (oracle) of K+P shards of L bytes: v[stripe, shard, byte]."""
+    c = O.Codec(8, K, P)
+    v = torch.zeros((N, K + P, L), dtype=torch.uint8)
+    for s in range(N):
+        sh = [O.splitmix_bytes(bench.SEED, bench.shard_id(s, i), L) for i in range(K)]
+        sh += [np.zeros(L, np.uint8) for _ in range(P)]
+        c.encode(sh)
+        v[s] = torch.from_numpy(np.stack(sh))
+    return v
+
+
+class _NoOp:
+    """Writes nothing and accepts everything."""
+
+    def reconstruct_data_flat(self, flat, elems, n, present):
+        pass
+
+    def verify(self, shards):
+        return True
+
+    def verify_flat(self, flat, L_, n):
+        return np.ones(n, bool)
+
+
+class _Zeros(_NoOp):
+    """Writes the wrong bytes (zeros) into the erased shards."""
+
+    def reconstruct_data_flat(self, flat, elems, n, present):
+        v = flat.view(n, len(present), -1)
+        for i, ok in enumerate(present):
+            if not ok:
+                v[:, i].zero_()
+
+
+class _Oracle:
+    """A correct stand-in: the CPU restatement of core.rs."""
+
+    def __init__(self):
+        self.c = O.Codec(8, K, P)
+
+    def reconstruct_data_flat(self, flat, elems, n, present):
+        v = flat.view(n, len(present), -1)
+        for s in range(n):
+            sh = [v[s, i].numpy() for i in range(len(present))]
+            self.c.reconstruct(sh, present, data_only=True)
+
+    def verify(self, shards):
+        return self.c.verify([x.numpy() for x in shards])
+
+    def verify_flat(self, flat, L_, n):
+        v = flat.view(n, K + P, L_)
+        return np.array([self.verify([v[s, i] for i in range(K + P)]) for s in range(n)])
+
+
+def _recon(codec, v, erased=(0, 1)):
+    want = [hashlib.sha256(O.splitmix_bytes(bench.SEED, bench.shard_id(0, i), L).tobytes())
+            .hexdigest() for i in erased]
+    return bench.reconstruct_leg(codec, v, K, list(erased), L, N, None, _cpu_fill,
+                                 list(range(N)), want, reps=2)
+
+
+def test_reconstruct_flags_false_for_a_kernel_that_writes_nothing(cpu_bench):
+    v = _stripes()
+    leg = _recon(_NoOp(), v)
+    assert leg["rebuilt_ok_all_stripes"] is False
+    assert leg["rebuilt_stripe0_vs_digests"] is False
+    assert bench.rebuilt_ok(v, N, [0, 1], list(range(N)), _cpu_fill) is False
+    assert (v[:, 0] == bench.POISON).all()  # the poison is what it left
+
+
+def test_reconstruct_flags_false_for_wrong_bytes(cpu_bench):
+    assert _recon(_Zeros(), _stripes())["rebuilt_ok_all_stripes"] is False
+
+
+def test_reconstruct_flags_true_for_a_correct_rebuild(cpu_bench):
+    v = _stripes()
+    leg = _recon(_Oracle(), v, (0, 2))
+    assert leg["rebuilt_ok_all_stripes"] is True
+    assert leg["rebuilt_stripe0_vs_digests"] is True
+    assert (v == _stripes()).all()
+
+
+def test_reconstruct_digest_flag():
+    """Stripe 0 against fixture digests: true for the right bytes, false
+    after a flipped byte."""
+    v = _stripes()
+    want = [hashlib.sha256(v[0, i].numpy().tobytes()).hexdigest() for i in (0, 1)]
+    assert bench.digests_ok(v, [0, 1], want)
+    v[0, 1, 7] ^= 1
+    assert not bench.digests_ok(v, [0, 1], want)
+
+
+def test_verify_flags_false_for_a_verify_that_accepts_everything(cpu_bench):
+    v = _stripes()
+    before = v.clone()
+    per_call, flat = bench.verify_leg(_NoOp(), v, K, P, L, N, reps=2)
+    assert per_call["verdicts_ok"] is False and flat["verdicts_ok"] is False
+    assert len(per_call["corrupted_stripes"]) == 2
+    assert (v == before).all()  # the corrupted bytes are restored
+
+
+def test_verify_flags_true_for_a_correct_verify(cpu_bench):
+    per_call, flat = bench.verify_leg(_Oracle(), _stripes(), K, P, L, N, reps=2)
+    assert per_call["verdicts_ok"] is True and flat["verdicts_ok"] is True
+
+
+@pytest.mark.gpu
+def test_bench_legs_on_the_gpu():
+    """The same legs through the HIP library: every flag true, on GF(2^8)
+    10+4 (syndrome kernel and repeated pattern) and GF(2^16) 20+8 at 8 lost;
+    and false for a stubbed codec on the same device buffers."""
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix
+    stream = torch.cuda.current_stream()
+    for field, k, p, nb, n, erased in ((8, 10, 4, 64 << 10, 6, [0, 1]),
+                                       (16, 20, 8, 64 << 10, 4, list(range(8)))):
+        v = torch.empty((n, k + p, nb), dtype=torch.uint8, device="cuda")
+        for s in range(n):
+            for i in range(k):
+                fill_splitmix(v[s, i], bench.SEED, bench.shard_id(s, i))
+        r = R.core.ReedSolomon(k, p, field)
+        elems = nb // (field // 8)
+        r.encode_flat(v.view(-1), elems, n)
+        leg = bench.reconstruct_leg(r, v, k, erased, elems, n, stream, fill_splitmix,
+                                    list(range(n)), reps=2)
+        assert leg["rebuilt_ok_all_stripes"] is True, (field, leg)
+        if field == 8:
+            a, b = bench.verify_leg(r, v, k, p, nb, n, reps=2)
+            assert a["verdicts_ok"] is True and b["verdicts_ok"] is True
+            assert r.verify_flat(v.view(-1), nb, n).all()  # restored
+            a, b = bench.verify_leg(_NoOp(), v, k, p, nb, n, reps=2)
+            assert a["verdicts_ok"] is False and b["verdicts_ok"] is False
+        leg = bench.reconstruct_leg(_NoOp(), v, k, erased, elems, n, stream, fill_splitmix,
+                                    list(range(n)), reps=2)
+        assert leg["rebuilt_ok_all_stripes"] is False

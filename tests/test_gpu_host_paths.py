@@ -311,6 +311,53 @@ def test_gal_mul_ffi_mixed_memory(R):
         assert (d_out.cpu().numpy() == O.gf8_mul_slice(c, x)).all()
 
 
+def test_gal_mul_ordered_after_null_stream_work(R):
+    """rse_gal_mul(_xor) on device slices still being written by work the
+    caller queued on the null stream (torch's default stream), with no
+    synchronisation in between: the library stream is a blocking stream, so
+    the hook reads the finished input and xors into the finished output."""
+    lib = R._lib.load()
+    _, _, _, low, high = O.gf8_tables()
+    n = 48 << 20
+    c = 0xB7
+    lo, hi = np.ascontiguousarray(low[c]), np.ascontiguousarray(high[c])
+    torch.cuda.synchronize()
+    with torch.cuda.stream(torch.cuda.default_stream()):
+        base = torch.arange(n, device="cuda", dtype=torch.int64)
+        d_in = ((base * 2654435761) >> 7).remainder(256).to(torch.uint8)
+        d_out = ((base * 40503) >> 3).remainder(256).to(torch.uint8)
+        for _ in range(4):  # more queued work, so the hook's launch would overtake it
+            d_in = d_in ^ ((d_in >> 1) & 0x55)
+        assert lib.rse_gal_mul_xor(_u8p(lo), _u8p(hi), d_in.data_ptr(), d_out.data_ptr(), n) == n
+    torch.cuda.synchronize()
+    x = d_in.cpu().numpy()
+    o0 = (((np.arange(n, dtype=np.int64) * 40503) >> 3) % 256).astype(np.uint8)
+    assert (d_out.cpu().numpy() == o0 ^ O.gf8_mul_slice(c, x)).all()
+
+
+def test_verify_with_buffer_read_from_another_stream(R):
+    """verify_with_buffer (core.rs:654-669) returns with the correct parity in
+    the caller's buffer: read back at once on a different non-blocking
+    stream (not ordered after the call's stream), it equals encode's."""
+    k, p, L = 10, 4, 16 << 20
+    r = R.galois_8.ReedSolomon(k, p)
+    from reed_solomon_erasure.core import fill_splitmix
+    shards = [torch.empty(L, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
+    for i in range(k):
+        fill_splitmix(shards[i], 0x5EED, 900 + i)
+    r.encode(shards)
+    want = torch.stack(shards[k:]).cpu()
+    for rep in range(3):
+        buf = [torch.full((L,), 0x3C, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        torch.cuda.synchronize()
+        assert r.verify_with_buffer(shards, buf)
+        side = torch.cuda.Stream()  # non-blocking with respect to the null stream
+        with torch.cuda.stream(side):
+            got = torch.stack(buf).to("cpu", non_blocking=False)
+        side.synchronize()
+        assert torch.equal(got, want), rep
+
+
 @pytest.mark.parametrize("kind", ["pageable", "pinned"])
 def test_field_mul_slice_on_host_slices(R, kind):
     """galois_8 mul_slice(_xor) and galois_16's Field::mul_slice(_add)
