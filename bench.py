@@ -477,6 +477,7 @@ def main(argv=None):
         extras.update(extra_legs(r, v, k, p, L, min(pool, 256), stream))
         if (k, p, L) == (10, 4, 16 * MiB):
             extras["other_configs"] = other_configs(stream)
+            extras["reference_bench_matrix"] = reference_bench_matrix(stream)
 
     if rank == 0:
         per_launch_bytes = n_local * stripe_bytes / launches
@@ -573,8 +574,12 @@ def rebuilt_ok(v, n_stripes, shards, stripe_ids, fill):
     """True iff shard i of stripe s holds the synthetic bytes of (SEED,
     shard_id(stripe_ids[s], i)) for every s < n_stripes and i in `shards`.
     `fill(t, seed, shard)` regenerates them (the device fill kernel, a
-    separate kernel from the one under test) into a scratch shard."""
+    separate kernel from the one under test) into a scratch shard; with
+    `fill` a tensor instead, the shards are compared with that saved copy
+    (v[:n_stripes, shards] taken before they were poisoned)."""
     import torch
+    if isinstance(fill, torch.Tensor):
+        return bool(torch.equal(v[:n_stripes, list(shards)], fill))
     tmp = torch.empty(v.shape[-1], dtype=torch.uint8, device=v.device)
     for s in range(n_stripes):
         for i in shards:
@@ -600,6 +605,8 @@ def reconstruct_leg(r, v, k, erased, elems, n_stripes, stream, fill, stripe_ids,
     T = v.shape[1]
     flat = v[:n_stripes].reshape(-1)
     present = [i not in erased for i in range(T)]
+    if fill is None:  # no generator for these bytes: keep a copy to compare with
+        fill = v[:n_stripes, list(erased)].clone()
     gbps = timed_gbps(lambda: r.reconstruct_data_flat(flat, elems, n_stripes, present),
                       n_stripes * (k + len(erased)) * v.shape[-1], stream, reps=reps,
                       prepare=lambda: poison(v, n_stripes, erased))
@@ -743,6 +750,225 @@ def wide_config(stream, g, field, k, p):
     del buf, v
     torch.cuda.empty_cache()
     return d
+
+
+# ------------------------------------------------- the reference's own bench
+# benches/bandwidth.rs:88-190: GF(2^8) 1 KiB blocks x {4+4, 8+8, 16+16, 32+32,
+# 64+64, 5+2, 10+4, 50+20}, and 4+4 at 2, 4, 8 and 16 KiB; encode, and
+# reconstruct after data shards 0..delete-1 are set to None (one: delete 1,
+# all: delete p, none: delete 0).  Criterion counts data bytes (k x block) per
+# iteration (bandwidth.rs:41-43, 65-67).
+REF_BENCH_SHAPES = ([(1024, k, p) for k, p in ((4, 4), (8, 8), (16, 16), (32, 32), (64, 64),
+                                               (5, 2), (10, 4), (50, 20))]
+                    + [(b, 4, 4) for b in (2048, 4096, 8192, 16384)])
+REF_BENCH_OPS = (("encode", None), ("reconstruct_one", 1), ("reconstruct_all", -1),
+                 ("reconstruct_none", 0))
+
+
+def per_call_us(fn, budget_s=0.02, min_calls=16):
+    """Mean microseconds per fn() call over >= min_calls calls and >= budget_s."""
+    fn()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        dt = time.perf_counter() - t0
+        if n >= min_calls and dt >= budget_s:
+            return dt / n * 1e6
+
+
+def _ref_rows(k, p, erased):
+    """The rows the reference codes with: the parity rows (encode, core.rs:
+    420-428), or the decode rows of the missing data shards over the first k
+    present shards (core.rs:697-731, 801-861; the LRU-cached steady state)."""
+    import numpy as np
+    from oracle import oracle as O
+    m = np.asarray(O.Codec(8, k, p).matrix(), np.uint8)
+    if erased is None:
+        return np.ascontiguousarray(m[k:]), list(range(k))
+    valid = [i for i in range(k + p) if i not in erased][:k]
+    return np.ascontiguousarray(O.matrix_invert(8, m[valid])[list(erased)]), valid
+
+
+def cpu_reference_call_us(k, p, block, erased, budget_s=0.02):
+    """The reference's simd_c kernel in code_some_slices order (oracle/_ref,
+    1 thread) per encode / reconstruct call at this shape, the repetitions
+    inside C (no per-call FFI cost); None when oracle/_ref is absent."""
+    import numpy as np
+    from oracle import oracle as O
+    if not O.ref_available():
+        return None
+    rows, ins = _ref_rows(k, p, erased)
+    data = [O.splitmix_bytes(SEED, i, block) for i in range(k + p)]
+    outs = [np.zeros(block, np.uint8) for _ in range(rows.shape[0])]
+    ref = O.ref()
+    args = (rows.ctypes.data_as(O._u8p), rows.shape[0], k, O._ptrs([data[i] for i in ins]),
+            O._ptrs(outs), block)
+    reps = 1
+    while True:
+        t0 = time.perf_counter()
+        ref.ref_gf8_code_repeat(*args, reps)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s or reps >= 1 << 22:
+            return dt / reps * 1e6
+        reps *= 4
+
+
+def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
+    """The reference's criterion matrix on this GPU, three ways per shape:
+    batched (many stripes per launch, the flat ABI: GB/s), one synchronous
+    call per stripe on device shards (what a drop-in caller of
+    ReedSolomon::encode with HBM-resident shards waits), and one call on
+    pageable host shards (the reference's own memory: H2D, kernel, D2H);
+    beside the reference's CPU kernel per call on this host.  Then a 10+4
+    shard-size sweep for the per-call crossover."""
+    import ctypes
+    import numpy as np
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix
+    from oracle import oracle as O
+    lib = R_lib()
+    st = torch.cuda.current_stream()
+    sh = st.cuda_stream
+    out = {"what": "benches/bandwidth.rs:88-190 shapes; data_MB_per_s counts k x block per "
+                   "call as criterion does; *_call_us are per synchronous call (python ctypes "
+                   "loop, ~1 us of call overhead included); cpu_reference = simd_c -O3 "
+                   "-march=haswell in core.rs loop order, 1 thread, decode rows cached",
+           "entries": []}
+
+    def one_stripe(k, p, block, src):
+        T = k + p
+        ptrs = (ctypes.c_void_p * T)(*[src[i].data_ptr() for i in range(T)])
+        lens = (ctypes.c_size_t * T)(*([block] * T))
+        host = [np.ascontiguousarray(src[i].cpu().numpy()) for i in range(T)]
+        hptrs = (ctypes.c_void_p * T)(*[h.ctypes.data for h in host])
+        return ptrs, lens, hptrs
+
+    for block, k, p in (shapes or REF_BENCH_SHAPES):
+        T = k + p
+        r = R.core.ReedSolomon(k, p, 8)
+        if block >= 4096:  # whole 4 KiB chunks: time the codec's bit-sliced
+            r.kernel_kind(wait=True)  # kernels, not the table kernels meanwhile
+        n = max(1, min(32768, (256 << 20) // (T * block)))
+        buf = torch.empty(n * T * block, dtype=torch.uint8, device="cuda")
+        fill_splitmix(buf, SEED, 0x7E57)
+        v = buf.view(n, T, block)
+        r.encode_flat(buf, block, n)
+        torch.cuda.synchronize()
+        ptrs, lens, hptrs = one_stripe(k, p, block, v[0])
+        data_bytes = k * block
+        for op, delete in REF_BENCH_OPS:
+            e = {"shape": f"{k}+{p} x {block // 1024} KiB", "op": op}
+            if op == "encode":
+                e["gpu_flat"] = {"stripes": n, "GB_per_s": timed_gbps(
+                    lambda: r.encode_flat(buf, block, n), n * T * block, stream)}
+                rows, _ = _ref_rows(k, p, None)
+                want = [np.zeros(block, np.uint8) for _ in range(p)]
+                O.code_some_slices(8, rows, [v[0, i].cpu().numpy() for i in range(k)], want)
+                e["parity_stripe0_vs_oracle"] = all(
+                    np.array_equal(v[0, k + i].cpu().numpy(), want[i]) for i in range(p))
+
+                def dev():
+                    _ck(lib.rse_encode(r._h, ptrs, lens, T, sh))
+                    st.synchronize()
+
+                def dev_async():
+                    _ck(lib.rse_encode(r._h, ptrs, lens, T, sh))
+
+                def host():
+                    _ck(lib.rse_encode_host(r._h, hptrs, lens, T, sh))
+                erased = None
+            else:
+                d = p if delete == -1 else delete
+                erased = list(range(d))
+                pres = (ctypes.c_uint8 * T)(*[0 if i in erased else 1 for i in range(T)])
+                if d:
+                    leg = reconstruct_leg(r, v, k, erased, block, n, stream, None, None)
+                    e["gpu_flat"] = {"stripes": n, "GB_per_s": leg["GB_per_s"]}
+                    e["rebuilt_ok_all_stripes"] = leg["rebuilt_ok_all_stripes"]
+
+                def dev():
+                    _ck(lib.rse_reconstruct(r._h, ptrs, lens, pres, T, sh))
+                    st.synchronize()
+
+                def dev_async():
+                    _ck(lib.rse_reconstruct(r._h, ptrs, lens, pres, T, sh))
+
+                def host():
+                    _ck(lib.rse_reconstruct_host(r._h, hptrs, lens, pres, T, sh))
+            if "gpu_flat" in e:
+                f = e["gpu_flat"]
+                alg = T if op == "encode" else k + len(erased)
+                f["data_MB_per_s"] = round(f["GB_per_s"] * 1e9 * k / alg / MiB, 1)
+            e["gpu_call_device_us"] = round(per_call_us(dev), 2)
+            t_async = per_call_us(dev_async)
+            st.synchronize()
+            e["gpu_call_device_async_us"] = round(t_async, 2)
+            e["gpu_call_host_us"] = round(per_call_us(host), 2)
+            if erased is None or erased:
+                c = cpu_reference_call_us(k, p, block, erased)
+                e["cpu_reference_call_us"] = round(c, 3) if c is not None else None
+            for key in ("gpu_call_device_us", "gpu_call_host_us", "cpu_reference_call_us"):
+                if e.get(key):
+                    e[key.replace("_us", "_data_MB_per_s")] = round(data_bytes / e[key] / MiB * 1e6, 1)
+            out["entries"].append(e)
+        del buf, v
+        torch.cuda.empty_cache()
+    out["crossover_10_4"] = (per_call_crossover(stream, crossover_sizes) if crossover_sizes
+                             else per_call_crossover(stream))
+    return out
+
+
+def _ck(rc):
+    if rc != 0:
+        raise RuntimeError(f"rse call failed with status {rc}")
+
+
+def per_call_crossover(stream, sizes=(1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10,
+                                      1 << 20, 4 << 20)):
+    """One 10+4 stripe per synchronous encode call at growing shard sizes:
+    device shards, pageable host shards and the reference CPU kernel, and the
+    smallest size at which each GPU form beats the CPU."""
+    import ctypes
+    import numpy as np
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix
+    lib = R_lib()
+    st = torch.cuda.current_stream()
+    sh = st.cuda_stream
+    k, p = 10, 4
+    T = k + p
+    r = R.core.ReedSolomon(k, p, 8)
+    rows = []
+    for L in sizes:
+        dv = torch.empty((T, L), dtype=torch.uint8, device="cuda")
+        fill_splitmix(dv, SEED, 0xC0)
+        ptrs = (ctypes.c_void_p * T)(*[dv[i].data_ptr() for i in range(T)])
+        lens = (ctypes.c_size_t * T)(*([L] * T))
+        host = [np.ascontiguousarray(dv[i].cpu().numpy()) for i in range(T)]
+        hptrs = (ctypes.c_void_p * T)(*[h.ctypes.data for h in host])
+
+        def dev():
+            _ck(lib.rse_encode(r._h, ptrs, lens, T, sh))
+            st.synchronize()
+
+        def host_call():
+            _ck(lib.rse_encode_host(r._h, hptrs, lens, T, sh))
+        row = {"shard_bytes": L, "gpu_call_device_us": round(per_call_us(dev), 2),
+               "gpu_call_host_us": round(per_call_us(host_call), 2)}
+        c = cpu_reference_call_us(k, p, L, None)
+        row["cpu_reference_call_us"] = round(c, 2) if c is not None else None
+        rows.append(row)
+        del dv
+    out = {"what": "10+4 encode, one stripe per synchronous call (device shards; pageable host "
+                   "shards; reference CPU kernel, 1 thread)", "rows": rows}
+    for key in ("gpu_call_device_us", "gpu_call_host_us"):
+        win = [x["shard_bytes"] for x in rows
+               if x["cpu_reference_call_us"] is not None and x[key] < x["cpu_reference_call_us"]]
+        out[f"{key.replace('_us', '')}_beats_cpu_from_shard_bytes"] = min(win) if win else None
+    return out
 
 
 def R_lib():

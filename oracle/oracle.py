@@ -97,6 +97,10 @@ def ref():
         L.ref_gf8_code_some_slices.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_size_t,
                                                ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_size_t]
+        if hasattr(L, "ref_gf8_code_repeat"):
+            L.ref_gf8_code_repeat.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_size_t]
         _REF = L
     return _REF
 

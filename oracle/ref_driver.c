@@ -69,3 +69,11 @@ void ref_gf8_code_some_slices(const uint8_t *rows, size_t n_out, size_t n_in,
       else ref_gf8_mul_slice_xor(c, inputs[i], outputs[r], len);
     }
 }
+
+/* `reps` back-to-back code_some_slices calls (a per-call CPU timing without
+ * the caller's per-call FFI overhead; bench.py's reference bench matrix) */
+void ref_gf8_code_repeat(const uint8_t *rows, size_t n_out, size_t n_in,
+                         const uint8_t *const *inputs, uint8_t *const *outputs, size_t len,
+                         size_t reps) {
+  for (size_t t = 0; t < reps; t++) ref_gf8_code_some_slices(rows, n_out, n_in, inputs, outputs, len);
+}

@@ -195,16 +195,18 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
 // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD),
 // P pairs per workgroup.
 // PF: the next unit's first input loaded during the mixing (A/B, option 28 = 3).
-template <class C, int P, bool PF = false>
+// DBG: A/B variants (RSE_OPT_RECON_PAIRS 4-6): 1 / 2 skip the Horner steps /
+// the data networks (tune-only timing splits, wrong bytes), 3 the compact mixing.
+template <class C, int P, bool PF = false, int DBG = 0>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_pair_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
-  bitslice_recon_pair_body<C, true, P, PF>(a, chunks_per_stripe);
+  bitslice_recon_pair_body<C, true, P, PF, DBG>(a, chunks_per_stripe);
 }
 
-template <class C, int P, bool PF = false>
+template <class C, int P, bool PF = false, int DBG = 0>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_desc_pair_kernel(
     const BsReconArgs* descs, uint64_t chunks_per_stripe, uint64_t n_stripes) {
-  bitslice_recon_desc_pair_body<C, true, P, PF>(descs, chunks_per_stripe, n_stripes);
+  bitslice_recon_desc_pair_body<C, true, P, PF, DBG>(descs, chunks_per_stripe, n_stripes);
 }
 
 // ------------------------------------------------- batched reconstruct planner
@@ -372,8 +374,10 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
-  BsRecFn rec_pair[3];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
-  BsDescFn rec_desc_pair[3];   // pair with the next unit prefetched (nullptr below 8 rows)
+  BsRecFn rec_pair[6];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
+  BsDescFn rec_desc_pair[6];   // pair with the next unit prefetched (nullptr below 8 rows),
+                               // [3] / [4]: no Horner steps / no data networks (timing
+                               // splits, wrong bytes), [5]: compact mixing (pair_slot)
 };
 
 template <class C, int NS, int MIX>
@@ -396,14 +400,14 @@ constexpr BsRecFn rec_deep_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_deep_kernel<C, NS, D>;
   else return nullptr;
 }
-template <class C, int P, bool PF = false>
+template <class C, int P, bool PF = false, int DBG = 0>
 constexpr BsRecFn rec_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C, P, PF>;
+  if constexpr (C::p >= 8) return bitslice_recon_pair_kernel<C, P, PF, DBG>;
   else return nullptr;
 }
-template <class C, int P, bool PF = false>
+template <class C, int P, bool PF = false, int DBG = 0>
 constexpr BsDescFn rec_desc_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C, P, PF>;
+  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_kernel<C, P, PF, DBG>;
   else return nullptr;
 }
 template <class C, int NS, int D>
@@ -440,8 +444,11 @@ constexpr BsDescFn rec_desc_deep_fn() {
      rec_desc_deep_fn<C, 8, 2>()},                                                     \
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
-   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>()},            \
-   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>(), rec_desc_pair_fn<C, 1, true>()}}
+   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>(),            \
+    rec_pair_fn<C, 1, false, 1>(), rec_pair_fn<C, 1, false, 2>(),                   \
+    rec_pair_fn<C, 1, false, 3>()},                                                 \
+   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>(), rec_desc_pair_fn<C, 1, true>(), \
+    nullptr, nullptr, rec_desc_pair_fn<C, 1, false, 3>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -591,7 +598,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
 // RSE_OPT_RECON_PAIRS: 0 off, 1 one pair per workgroup (its barriers sync
 // the pair only: 4.26 TB/s at 8 lost against 4.18 for two pairs per
 // workgroup, profiles/r03/s3/r8.log), 2 two pairs; returns pairs per
-// workgroup (0: off).
+// workgroup (0: off).  3-6: one pair per workgroup, A/B variants (pair_slot).
 int pair_groups() {
   const int64_t o = get_option(28);
   return o == 0 ? 0 : o == 2 ? 2 : 1;
@@ -605,10 +612,12 @@ int recon_depth(int mix) {
   return mix >= kReconMixHorner ? (int)get_option(27) : 1;
 }
 
-// index into BsShape::rec_pair / rec_desc_pair (option 28 = 3: prefetching variant)
+// index into BsShape::rec_pair / rec_desc_pair: option 28 = 3 the prefetching
+// variant, 4 / 5 the timing splits (no Horner steps / no data networks; wrong
+// bytes, tools/tune.py only), 6 the compact mixing
 int pair_slot() {
   const int64_t o = get_option(28);
-  return o == 3 ? 2 : pair_groups() - 1;
+  return o >= 3 && o <= 6 ? (int)o - 1 : pair_groups() - 1;
 }
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
@@ -643,7 +652,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
     const int np = pair_groups();
     if (slot == 3 && np && sh.rec_pair[pair_slot()] && mix >= kReconMixHorner && depth == 1) {
-      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d", field, k, p, np);
+      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d s%d", field, k, p, np, pair_slot());
       // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
       // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
       uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);

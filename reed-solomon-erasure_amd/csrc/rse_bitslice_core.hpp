@@ -1537,7 +1537,10 @@ __device__ __forceinline__ bool pair_prefetch(u32x4 (&nxt)[4], const BsReconArgs
 }
 
 // Data rounds T.. : indices 2T (role 0) and 2T + 1 (role 1).
-template <class C, bool NT, int H, int T, int P>
+// DBG (tune-only A/B variants, results not valid): 1 skips the Horner steps of
+// the mixing, 2 the data inputs' networks (mac_rows) -- to split the kernel's
+// time between its phases.
+template <class C, bool NT, int H, int T, int P, int DBG = 0>
 __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4 (&cur)[4],
                                           const BsReconArgs& a, uint64_t own, uint32_t present,
                                           uint64_t off, u32x4 (*mine)[64], u32x4 (*theirs)[64],
@@ -1565,8 +1568,8 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
         }
       }
       __syncthreads();
-      if (has_own) mac_rows<C, J, H * kPairRows>(acc, pl);
-      if (has_oth) {
+      if (DBG != 2 && has_own) mac_rows<C, J, H * kPairRows>(acc, pl);
+      if (DBG != 2 && has_oth) {
         uint32_t pp[16];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1582,13 +1585,13 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
       for (int q = 0; q < kPairRows * 16; ++q) asm volatile("" : "+v"(acc[q]));
       buf ^= 1u;
     }
-    pair_data<C, NT, H, T + 1, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+    pair_data<C, NT, H, T + 1, P, DBG>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
   }
 }
 
 // The partial sum over the wave's rows of output o (Horner's rule, 4 rows),
 // plus its sigma row if that is one of them.
-template <class C, int H>
+template <class C, int H, int DBG = 0>
 __device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
                                              const uint32_t (&acc)[kPairRows * 16],
                                              const uint32_t (&d)[2][16], uint32_t (&v)[16]) {
@@ -1597,7 +1600,7 @@ __device__ __forceinline__ void pair_partial(const BsReconArgs& a, uint32_t o,
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] = 0u;
 #pragma unroll 1
-  for (int w = 0; w < NB / 4; ++w) {
+  for (int w = 0; w < (DBG == 1 ? 0 : NB / 4); ++w) {
     const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane(a.hm[o][w]);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -1625,7 +1628,7 @@ __device__ __forceinline__ T& pick_ref(T& io, T& local) {
   if constexpr (PF) return io;
   else return local;
 }
-template <class C, bool NT, int H, int P, bool PF = false>
+template <class C, bool NT, int H, int P, bool PF = false, int DBG = 0>
 __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t off,
                                                 PairLds<P>& lds, uint32_t pair, uint32_t lane,
                                                 u32x4 (&cur_io)[4], bool primed, uint64_t next_off) {
@@ -1655,7 +1658,7 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
-  pair_data<C, NT, H, 0, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  pair_data<C, NT, H, 0, P, DBG>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
   // own syndrome rows: s_r = sigma_r ^ parity_r
 #pragma unroll
   for (int i = 0; i < kPairRows; ++i) {
@@ -1699,7 +1702,7 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
       const uint32_t po = theirs0 + m + j;
       if (m + j < half && po < n_out) {
         uint32_t v[16];
-        pair_partial<C, H>(a, po, acc, d, v);
+        pair_partial<C, H, DBG>(a, po, acc, d, v);
         u32x4(*x)[64] = lds.v[j][pair][H];
 #pragma unroll
         for (int q = 0; q < 4; ++q) x[q][lane] = (u32x4){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
@@ -1711,7 +1714,7 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
       const uint32_t o = mine0 + m + j;
       if (m + j < half && o < n_out) {
         uint32_t v[16];
-        pair_partial<C, H>(a, o, acc, d, v);
+        pair_partial<C, H, DBG>(a, o, acc, d, v);
         const u32x4(*x)[64] = lds.v[j][pair][1 - H];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1734,10 +1737,131 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
   return prime;
 }
 
+// ---- compact mixing (RSE_OPT_RECON_PAIRS 6, A/B) ----------------------------
+// The same unit with ONE copy of the mixing code for both roles: the data
+// phase is specialised per role (its networks code the role's rows), the
+// mixing takes the role at run time, runs one Horner step per loop trip (no
+// 4-step unrolling) and computes the partner's and its own partials in one
+// loop, so the Horner dispatch exists once in the kernel (instruction-cache
+// footprint), not four times.
+template <class C, bool NT, int H, int P>
+__device__ __forceinline__ void pair_inputs(const BsReconArgs& a, uint64_t off, PairLds<P>& lds,
+                                            uint32_t pair, uint32_t lane,
+                                            uint32_t (&acc)[kPairRows * 16]) {
+  using F = typename C::Field;
+  constexpr int R0 = H * kPairRows;
+  const uint32_t present = a.present;
+  const uint32_t synd = a.synd;
+  const uint64_t par_mask = H ? 0xAAAAAAAAull : 0x55555555ull;
+  const uint64_t own = ((uint64_t)present & par_mask) |
+                       ((uint64_t)((synd >> R0) & 0xFu) << (C::k + R0));
+  u32x4 cur[4];
+  if (own) load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + off);
+  uint32_t buf = 0;
+  u32x4(*mine)[64] = lds.v[0][pair][H];
+  u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
+  pair_data<C, NT, H, 0, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+#pragma unroll
+  for (int i = 0; i < kPairRows; ++i) {
+    const int J = C::k + R0 + i;
+    if ((own >> J) & 1u) {
+      u32x4 nxt[4];
+      const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t pl[16];
+      slice<F>(cur, pl);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i * 16 + q] ^= pl[q];
+      if (more) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+  }
+}
+
+template <class C, bool NT, int P>
+__device__ __forceinline__ void recon_pair_unit_compact(const BsReconArgs& a, uint64_t off,
+                                                        PairLds<P>& lds, uint32_t pair,
+                                                        uint32_t lane, uint32_t H) {
+  using F = typename C::Field;
+  constexpr int NB = HornerF<F>::N;
+  uint32_t acc[kPairRows * 16];
+#pragma unroll
+  for (int q = 0; q < kPairRows * 16; ++q) acc[q] = 0u;
+  if (H) pair_inputs<C, NT, 1, P>(a, off, lds, pair, lane, acc);
+  else pair_inputs<C, NT, 0, P>(a, off, lds, pair, lane, acc);
+  const uint32_t R0 = H * kPairRows;
+  const uint32_t sigma = a.sigma;
+  const uint32_t n_out = __builtin_amdgcn_readfirstlane(a.n_out);
+  if constexpr (NB == 16) {
+#pragma unroll
+    for (int r = 0; r < kPairRows; ++r)
+      if ((sigma >> (R0 + r)) & 1u) to_basis16(&acc[r * 16], make_int_seq<16>{});
+  }
+  uint32_t d[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[t][q] = acc[2 * t * 16 + q] ^ acc[(2 * t + 1) * 16 + q];
+  const uint32_t half = (n_out + 1) / 2;
+  const uint32_t mine0 = H * half, theirs0 = (1 - H) * half;
+  const uint32_t nib_shift = 4u * H;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t m = 0; m < half; m += 2) {
+#pragma unroll 1
+    for (uint32_t x = 0; x < 4; ++x) {  // 0, 1: the partner's outputs; 2, 3: own
+      const uint32_t j = x & 1u;
+      const bool own_out = x >= 2;
+      if (x == 2) __syncthreads();
+      const uint32_t o = (own_out ? mine0 : theirs0) + m + j;
+      if (m + j >= half || o >= n_out) continue;
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = 0u;
+#pragma unroll 1
+      for (int st = 0; st < NB; ++st) {
+        const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane(a.hm[o][st >> 2]);
+        h_group<F, true, 0, kPairRows, 2>(v, acc, d, (word >> (8 * (st & 3) + nib_shift)) & 15u);
+      }
+      const int32_t os = __builtin_amdgcn_readfirstlane(a.out_sigma[o]) - (int32_t)R0;
+#pragma unroll
+      for (int r = 0; r < kPairRows; ++r)
+        if (os == r) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] ^= acc[r * 16 + q];
+        }
+      if (!own_out) {
+        u32x4(*xw)[64] = lds.v[j][pair][H];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xw[q][lane] = (u32x4){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      } else {
+        const u32x4(*xr)[64] = lds.v[j][pair][1 - H];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4 t = xr[q][lane];
+          v[4 * q] ^= t[0];
+          v[4 * q + 1] ^= t[1];
+          v[4 * q + 2] ^= t[2];
+          v[4 * q + 3] ^= t[3];
+        }
+        if constexpr (NB == 16) from_basis16(v, make_int_seq<16>{});
+        u32x4 xs[4];
+        unslice<F>(v, xs);
+        uint8_t* dst = a.out[o];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stv<NT>(dst + off + q * 1024u, xs[q]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Units of P 4 KiB columns: unit u of a stripe (cps 16 KiB chunks) covers
 // bytes [u * 4096P, (u + 1) * 4096P); pair q its column q.  Workgroups of
 // 128P lanes.
-template <class C, bool NT, int P, bool PF = false>
+template <class C, bool NT, int P, bool PF = false, int DBG = 0>
 __device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
                                                          uint64_t chunks_per_stripe) {
   __shared__ PairLds<P> lds;
@@ -1757,18 +1881,21 @@ __device__ __forceinline__ void bitslice_recon_pair_body(const BsReconArgs& a,
       if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P, true>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
       else primed = recon_pair_unit<C, NT, 0, P, true>(a, unit_off(u), lds, pair, lane, cur, primed, next_off);
     }
+  } else if constexpr (DBG == 3) {
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x)
+      recon_pair_unit_compact<C, NT, P>(a, unit_off(u), lds, pair, lane, wave & 1u);
   } else {
     // (a fresh vector set per unit: nothing lives across units)
     for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
       u32x4 cur[4];
-      if (wave & 1u) recon_pair_unit<C, NT, 1, P>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
-      else recon_pair_unit<C, NT, 0, P>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
+      if (wave & 1u) recon_pair_unit<C, NT, 1, P, false, DBG>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
+      else recon_pair_unit<C, NT, 0, P, false, DBG>(a, unit_off(u), lds, pair, lane, cur, false, ~0ull);
     }
   }
 }
 
 // The same over per-stripe argument blocks (rse_reconstruct_batch).
-template <class C, bool NT, int P, bool PF = false>
+template <class C, bool NT, int P, bool PF = false, int DBG = 0>
 __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs* __restrict__ descs,
                                                               uint64_t chunks_per_stripe,
                                                               uint64_t n_stripes) {
@@ -1790,6 +1917,14 @@ __device__ __forceinline__ void bitslice_recon_desc_pair_body(const BsReconArgs*
           nu < total && nsub < upc ? nsub * (4096u * P) + pair * 4096u + lane * 16u : ~0ull;
       if (wave & 1u) primed = recon_pair_unit<C, NT, 1, P, true>(a, off, lds, pair, lane, cur, primed, next_off);
       else primed = recon_pair_unit<C, NT, 0, P, true>(a, off, lds, pair, lane, cur, primed, next_off);
+    }
+  } else if constexpr (DBG == 3) {
+    for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
+      const uint64_t stripe = u / upc, sub = u - stripe * upc;
+      const BsReconArgs& a = desc_at(descs, stripe);
+      if (a.n_out == 0) continue;  // workgroup-uniform
+      recon_pair_unit_compact<C, NT, P>(a, sub * (4096u * P) + pair * 4096u + lane * 16u, lds,
+                                        pair, lane, wave & 1u);
     }
   } else {
     for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {

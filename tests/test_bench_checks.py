@@ -174,3 +174,43 @@ def test_bench_legs_on_the_gpu():
         leg = bench.reconstruct_leg(_NoOp(), v, k, erased, elems, n, stream, fill_splitmix,
                                     list(range(n)), reps=2)
         assert leg["rebuilt_ok_all_stripes"] is False
+
+
+def test_reference_rows_and_cpu_call():
+    """The CPU side of the reference bench matrix: encode codes the parity
+    rows, reconstruct the decode rows of the first k present shards (core.rs:
+    801-861), and the reference kernel's per-call time is measured in C."""
+    rows, ins = bench._ref_rows(4, 4, None)
+    assert rows.shape == (4, 4) and ins == [0, 1, 2, 3]
+    rows, ins = bench._ref_rows(4, 4, [0, 1])
+    assert rows.shape == (2, 4) and ins == [2, 3, 4, 5]
+    # the decode rows rebuild the erased shards from the valid ones
+    c = O.Codec(8, 4, 4)
+    sh = [O.splitmix_bytes(1, i, 1000) for i in range(4)] + [np.zeros(1000, np.uint8)] * 4
+    sh = [np.array(x) for x in sh]
+    c.encode(sh)
+    out = [np.zeros(1000, np.uint8) for _ in range(2)]
+    O.code_some_slices(8, rows, [sh[i] for i in ins], out)
+    assert all(np.array_equal(out[j], sh[j]) for j in range(2))
+    if O.ref_available():
+        us = bench.cpu_reference_call_us(10, 4, 1024, None, budget_s=0.005)
+        assert us is not None and 0 < us < 1e4
+
+
+@pytest.mark.gpu
+def test_reference_bench_matrix_on_the_gpu():
+    """bench.py's reference bench matrix at a reduced set of shapes: every
+    column measured, parity and rebuilt shards checked, the crossover sweep
+    filled in."""
+    out = bench.reference_bench_matrix(torch.cuda.current_stream(),
+                                       shapes=[(1024, 4, 4), (4096, 10, 4)],
+                                       crossover_sizes=(1024, 65536))
+    ops = {(e["shape"], e["op"]) for e in out["entries"]}
+    assert ("4+4 x 1 KiB", "reconstruct_all") in ops and ("10+4 x 4 KiB", "encode") in ops
+    for e in out["entries"]:
+        assert e["gpu_call_device_us"] > 0 and e["gpu_call_host_us"] > 0
+        if e["op"] == "encode":
+            assert e["parity_stripe0_vs_oracle"] is True and e["gpu_flat"]["GB_per_s"] > 0
+        elif e["op"] != "reconstruct_none":
+            assert e["rebuilt_ok_all_stripes"] is True
+    assert len(out["crossover_10_4"]["rows"]) == 2

@@ -813,7 +813,9 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
         lib.rse_set_option(28, pairs)
 
 
-@pytest.mark.parametrize("pairs", [1, 2])  # RSE_OPT_RECON_PAIRS: pairs per workgroup
+# RSE_OPT_RECON_PAIRS: pairs per workgroup (1, 2); 3 the prefetching variant,
+# 6 the compact mixing (one pair per workgroup)
+@pytest.mark.parametrize("pairs", [1, 2, 3, 6])
 def test_reconstruct_wave_pairs(R, pairs):
     """GF(2^16) 20+8 syndrome reconstruct at 8 sigma rows on wave pairs
     (RSE_OPT_RECON_PAIRS, the default): each wave of a pair holds 4 syndrome
@@ -856,7 +858,8 @@ def test_reconstruct_wave_pairs(R, pairs):
                 assert (host(tb[i]).reshape(-1) == full[i]).all(), (erased, i)
             # more than 4 data shards lost: syndrome rows past the 4th, NS = 8
             if sum(1 for e in erased if e < k) > 4:
-                assert f"ns8 pairs{pairs}" in last_kernel(), (erased, last_kernel())
+                np_, slot = (2, 1) if pairs == 2 else (1, pairs - 1 if pairs >= 3 else 0)
+                assert f"ns8 pairs{np_} s{slot}" in last_kernel(), (erased, last_kernel())
         # reconstruct_batch: every stripe its own pattern, all with 8 sigma
         # rows; shards with a 4 KiB remainder (one-wave kernel) and a tail
         nbytes = 16384 * 3 + 4096 + 32
