@@ -543,12 +543,20 @@ def timed_ms(fn, reps, stream=None):
     return a.elapsed_time(b) / reps
 
 
-def timed_gbps(fn, nbytes, stream, reps=5, prepare=None):
+def timed_gbps(fn, nbytes, stream, reps=5, prepare=None, warm_s=0.0):
     """Algorithmic GB/s (1e9) of fn() over `reps` back-to-back calls (HIP
-    events on the launch stream) after one untimed call.  `prepare` runs
-    between the untimed call and the timed ones (outside the timed region):
-    the reconstruct legs poison the shards the timed calls must rebuild."""
+    events on the launch stream) after one untimed call (or untimed calls for
+    `warm_s` seconds: the VALU-bound wide kernels run at a power-managed clock
+    that settles over tens of milliseconds).  `prepare` runs between the
+    untimed calls and the timed ones (outside the timed region): the
+    reconstruct legs poison the shards the timed calls must rebuild."""
     fn()
+    if warm_s > 0:
+        _sync()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < warm_s:
+            fn()
+            _sync()
     if prepare is not None:
         prepare()
     return round(nbytes / (timed_ms(fn, reps, stream) * 1e-3) / 1e9, 1)
@@ -634,6 +642,7 @@ def verify_leg(r, v, k, p, L, n_stripes, reps=5):
         t0 = time.perf_counter()
         got = [r.verify(sh) for sh in shards]
         dt = time.perf_counter() - t0
+        capi = verify_capi(r, shards, L, want)
         flat_first = [bool(x) for x in r.verify_flat(flat, L, n_stripes)]
         res = {}
 
@@ -646,14 +655,48 @@ def verify_leg(r, v, k, p, L, n_stripes, reps=5):
             v[s, i, offs[s]] ^= 0x5A
     nbytes = n_stripes * (k + p) * L
     corrupted = sorted(bad)
-    return ({"what": f"verify, {n_stripes} stripes, one call each (synchronous); stripes "
-                     f"{corrupted} corrupted", "corrupted_stripes": corrupted,
-             "verdicts_ok": got == want,
-             "algorithmic_GB_per_s": round(nbytes / dt / 1e9, 1)},
+    per_call = {"what": f"verify, {n_stripes} stripes, one call each (synchronous, through the "
+                        f"Python mirror); stripes {corrupted} corrupted",
+                "corrupted_stripes": corrupted, "verdicts_ok": got == want,
+                "algorithmic_GB_per_s": round(nbytes / dt / 1e9, 1)}
+    if capi is not None:
+        per_call["c_abi"] = {
+            "what": "the same calls through the C ABI with prebuilt pointer arrays (what the "
+                    "reference's Rust caller binding rse_verify pays; ctypes adds ~1 us)",
+            "verdicts_ok": capi[1], "us_per_call": round(capi[0] * 1e6, 2),
+            "algorithmic_GB_per_s": round(nbytes / n_stripes / capi[0] / 1e9, 1)}
+    return (per_call,
             {"what": f"verify_flat, {n_stripes} stripes in one pass (reads k+p shards); stripes "
                      f"{corrupted} corrupted", "corrupted_stripes": corrupted,
              "verdicts_ok": flat_got == want and flat_first == want,
              "algorithmic_GB_per_s": round(nbytes / (ms * 1e-3) / 1e9, 1)})
+
+
+def verify_capi(r, shards, L, want, reps=3):
+    """Seconds per synchronous rse_verify call over the stripes `shards`
+    (best of `reps` passes) and whether every verdict equals `want`; None
+    without a device codec (the CPU tests' stand-ins)."""
+    import ctypes
+    import torch
+    if not hasattr(r, "_h") or not torch.cuda.is_available():
+        return None
+    lib = R_lib()
+    sh = torch.cuda.current_stream().cuda_stream
+    T = len(shards[0])
+    lens = (ctypes.c_size_t * T)(*([L] * T))
+    arrs = [(ctypes.c_void_p * T)(*[t.data_ptr() for t in s]) for s in shards]
+    ok = ctypes.c_int(0)
+    best, good = None, True
+    for _ in range(reps):
+        got = []
+        t0 = time.perf_counter()
+        for a in arrs:
+            _ck(lib.rse_verify(r._h, a, lens, T, ctypes.byref(ok), sh))
+            got.append(bool(ok.value))
+        dt = (time.perf_counter() - t0) / len(arrs)
+        good = good and got == want
+        best = dt if best is None else min(best, dt)
+    return best, good
 
 
 def other_configs(stream):
@@ -739,9 +782,11 @@ def wide_config(stream, g, field, k, p):
     kind = r.kernel_kind(wait=True)
     build_s = time.perf_counter() - t0
     elems = nbytes // (field // 8)
-    enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream)
+    enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream,
+                     reps=20, warm_s=0.25)
     want = g["full_size"][f"gf{field}_{k}_{p}_{nbytes}"]["parity_sha256"]
     d = {"workload": f"gf{field} {k}+{p} x 1 MiB, {stripes} stripes/launch", "kernels": kind,
+         "timing": "0.25 s of untimed launches, then 20 back to back (HIP events)",
          "kernel": last_kernel(), "build_seconds": round(build_s, 1),
          "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
          "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4)}
@@ -843,7 +888,7 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
         lens = (ctypes.c_size_t * T)(*([block] * T))
         host = [np.ascontiguousarray(src[i].cpu().numpy()) for i in range(T)]
         hptrs = (ctypes.c_void_p * T)(*[h.ctypes.data for h in host])
-        return ptrs, lens, hptrs
+        return ptrs, lens, hptrs, host  # `host` owns the memory hptrs points to
 
     for block, k, p in (shapes or REF_BENCH_SHAPES):
         T = k + p
@@ -856,7 +901,7 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
         v = buf.view(n, T, block)
         r.encode_flat(buf, block, n)
         torch.cuda.synchronize()
-        ptrs, lens, hptrs = one_stripe(k, p, block, v[0])
+        ptrs, lens, hptrs, host_shards = one_stripe(k, p, block, v[0])
         data_bytes = k * block
         for op, delete in REF_BENCH_OPS:
             e = {"shape": f"{k}+{p} x {block // 1024} KiB", "op": op}
@@ -913,7 +958,7 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
                 if e.get(key):
                     e[key.replace("_us", "_data_MB_per_s")] = round(data_bytes / e[key] / MiB * 1e6, 1)
             out["entries"].append(e)
-        del buf, v
+        del buf, v, host_shards
         torch.cuda.empty_cache()
     out["crossover_10_4"] = (per_call_crossover(stream, crossover_sizes) if crossover_sizes
                              else per_call_crossover(stream))

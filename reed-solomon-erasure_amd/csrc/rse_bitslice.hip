@@ -246,109 +246,122 @@ struct GfDev {
 
 constexpr int kPlanBlock = 64;
 
+// One lane per stripe.  The index sets are bit masks (S: missing data, R:
+// syndrome rows, M: missing parity) and the [A | I] Gauss-Jordan workspace
+// lives in LDS, lane-interleaved (element (t, x) of lane l at
+// gj[(t * 2E + x) * kPlanBlock + l], E = e_cap: conflict-free), so nothing
+// goes to scratch memory (the round-3 planner kept them in 1.2 KB of private
+// memory per lane).  Only the fields the Horner syndrome kernels read are
+// written: data / par / out pointers, out_sigma, the masks, n_out and hm
+// (the weights go straight into the Horner masks; w is never stored).  The
+// GF(2^8) log / exp tables come from `tabs` (256 + 512 bytes, host-built).
 __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
-    int field, const uint16_t* __restrict__ rows, const uint8_t* __restrict__ present, uint32_t k,
-    uint32_t p, uint32_t data_only, uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
-    BsReconArgs* descs) {
-  __shared__ uint8_t lg[256], ex[512];
-  if (threadIdx.x == 0) {  // generator 2 modulo 0x11D (build.rs:13-43)
-    uint32_t b = 1;
-    for (uint32_t l = 0; l < 255; ++l) {
-      lg[b] = (uint8_t)l;
-      ex[l] = ex[l + 255] = (uint8_t)b;
-      b <<= 1;
-      if (b & 0x100u) b ^= 0x11Du;
-    }
-    lg[0] = 0;
-    ex[510] = ex[511] = 0;
-  }
+    int field, const uint16_t* __restrict__ rows, const uint8_t* __restrict__ tabs,
+    const uint8_t* __restrict__ present, uint32_t k, uint32_t p, uint32_t data_only, uint8_t* base,
+    uint64_t shard_bytes, uint32_t n_stripes, uint32_t e_cap, BsReconArgs* descs) {
+  __shared__ uint32_t tl[(256 + 512) / 4];
+  extern __shared__ uint16_t gj[];
+  for (uint32_t i = threadIdx.x; i < (256 + 512) / 4; i += kPlanBlock)
+    tl[i] = reinterpret_cast<const uint32_t*>(tabs)[i];
   __syncthreads();
   const uint32_t s = blockIdx.x * kPlanBlock + threadIdx.x;
   if (s >= n_stripes) return;
-  const GfDev gf{lg, ex, field};
-  const uint32_t total = k + p;
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(tl);
+  const GfDev gf{lg, lg + 256, field};
+  const uint32_t total = k + p, E2 = 2 * e_cap, l = threadIdx.x;
+  auto G = [&](uint32_t t, uint32_t x) -> uint16_t& { return gj[(t * E2 + x) * kPlanBlock + l]; };
   const uint8_t* pr = present + (uint64_t)s * total;
   uint8_t* sb = base + (uint64_t)s * total * shard_bytes;
   BsReconArgs& d = descs[s];
-  uint32_t S[kMaxOut], R[kMaxOut], M[kMaxOut];
-  uint32_t ne = 0, nr = 0, nm = 0, pmask = 0;
-  bool fits = true;
+  uint32_t pmask = 0, smask = 0, rmask = 0, mmask = 0, nr = 0;
   for (uint32_t j = 0; j < k; ++j) {
-    d.data[j] = pr[j] ? sb + (uint64_t)j * shard_bytes : nullptr;
-    if (pr[j]) pmask |= 1u << j;
-    else if (ne < (uint32_t)kMaxOut) S[ne++] = j;
-    else fits = false;
+    const bool here = pr[j] != 0;
+    d.data[j] = here ? sb + (uint64_t)j * shard_bytes : nullptr;
+    if (here) pmask |= 1u << j;
+    else smask |= 1u << j;
   }
+  const uint32_t ne = (uint32_t)__builtin_popcount(smask);
   for (uint32_t r = 0; r < p; ++r) {
     if (pr[k + r]) {
-      if (nr < ne) R[nr++] = r;
+      if (nr < ne) {
+        rmask |= 1u << r;
+        ++nr;
+      }
     } else if (!data_only) {
-      M[nm++] = r;
+      mmask |= 1u << r;
     }
   }
-  for (uint32_t r = 0; r < (uint32_t)kMaxOut; ++r) {
-    d.par[r] = nullptr;
-    d.out[r] = nullptr;
-    d.out_sigma[r] = -1;
-    for (uint32_t q = 0; q < (uint32_t)kMaxOut; ++q) d.w[r][q] = 0;
-  }
+  const uint32_t nm = (uint32_t)__builtin_popcount(mmask);
   d.stripe_stride = 0;
   d.n_stripes = 1;
   d.present = pmask;
   d.sigma = d.synd = 0;
   d.n_out = 0;  // nothing to do unless completed below
-  if (!fits || nr != ne || ne + nm == 0 || ne + nm > (uint32_t)kMaxOut) return;
-  // [A | I], A = P[R][S], Gauss-Jordan
-  uint16_t w[kMaxOut][2 * kMaxOut];
-  for (uint32_t t = 0; t < ne; ++t)
-    for (uint32_t u = 0; u < ne; ++u) {
-      w[t][u] = rows[R[t] * k + S[u]];
-      w[t][ne + u] = t == u ? 1 : 0;
+  if (nr != ne || ne > e_cap || ne + nm == 0 || ne + nm > (uint32_t)kMaxOut) return;
+  // [A | I], A = P[R][S]
+  for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
+    const uint32_t r = (uint32_t)__builtin_ctz(rr);
+    for (uint32_t u = 0, ss = smask; u < ne; ++u, ss &= ss - 1u) {
+      G(t, u) = rows[r * k + (uint32_t)__builtin_ctz(ss)];
+      G(t, ne + u) = t == u ? 1 : 0;
     }
+  }
   for (uint32_t col = 0; col < ne; ++col) {
     uint32_t piv = col;
-    while (piv < ne && w[piv][col] == 0) ++piv;
+    while (piv < ne && G(piv, col) == 0) ++piv;
     if (piv == ne) return;  // singular: impossible for this code; stripe untouched
     if (piv != col)
       for (uint32_t x = 0; x < 2 * ne; ++x) {
-        const uint16_t t0 = w[col][x];
-        w[col][x] = w[piv][x];
-        w[piv][x] = t0;
+        const uint16_t t0 = G(col, x);
+        G(col, x) = G(piv, x);
+        G(piv, x) = t0;
       }
-    const uint32_t sc = gf.inv(w[col][col]);
-    for (uint32_t x = 0; x < 2 * ne; ++x) w[col][x] = (uint16_t)gf.mul(sc, w[col][x]);
+    const uint32_t sc = gf.inv(G(col, col));
+    for (uint32_t x = 0; x < 2 * ne; ++x) G(col, x) = (uint16_t)gf.mul(sc, G(col, x));
     for (uint32_t r = 0; r < ne; ++r) {
-      const uint32_t f = w[r][col];
+      const uint32_t f = G(r, col);
       if (r == col || !f) continue;
-      for (uint32_t x = 0; x < 2 * ne; ++x) w[r][x] ^= (uint16_t)gf.mul(f, w[col][x]);
+      for (uint32_t x = col; x < 2 * ne; ++x) G(r, x) ^= (uint16_t)gf.mul(f, G(col, x));
     }
   }
+  // outputs: missing data S_u = sum_t Ainv[u][t] s_t; missing parity r =
+  // sigma_r ^ sum_t (P[r][S] Ainv)[t] s_t.  Weight (o, t) goes into the
+  // Horner mask bits of syndrome row R_t (rse_kernels.hpp set_horner_masks).
+  const int nb = field == 8 ? 8 : 16;
   uint32_t o = 0;
-  for (uint32_t u = 0; u < ne; ++u, ++o) {  // missing data S[u] = sum_t Ainv[u][t] s_t
-    d.out[o] = sb + (uint64_t)S[u] * shard_bytes;
-    for (uint32_t t = 0; t < ne; ++t) d.w[o][R[t]] = w[u][ne + t];
+  for (uint32_t u = 0, ss = smask; u < ne; ++u, ++o, ss &= ss - 1u) {
+    d.out[o] = sb + (uint64_t)__builtin_ctz(ss) * shard_bytes;
+    d.out_sigma[o] = -1;
+    uint32_t hm[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
+      const uint32_t co = horner_coords(field, G(u, ne + t)), r = (uint32_t)__builtin_ctz(rr);
+      for (int j = 0; j < nb; ++j)
+        if ((co >> (nb - 1 - j)) & 1u) hm[j >> 2] |= 1u << (8 * (j & 3) + r);
+    }
+    for (int q = 0; q < 4; ++q) d.hm[o][q] = hm[q];
   }
-  for (uint32_t m = 0; m < nm; ++m, ++o) {  // missing parity r = sigma_r ^ sum_t (P[r][S] Ainv)[t] s_t
-    const uint32_t r = M[m];
+  for (uint32_t mm = mmask; mm; mm &= mm - 1u, ++o) {
+    const uint32_t r = (uint32_t)__builtin_ctz(mm);
     d.out[o] = sb + (uint64_t)(k + r) * shard_bytes;
     d.out_sigma[o] = (int32_t)r;
-    for (uint32_t t = 0; t < ne; ++t) {
+    uint32_t hm[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
       uint32_t v = 0;
-      for (uint32_t u = 0; u < ne; ++u) v ^= gf.mul(rows[r * k + S[u]], w[u][ne + t]);
-      d.w[o][R[t]] = (uint16_t)v;
+      for (uint32_t u = 0, ss = smask; u < ne; ++u, ss &= ss - 1u)
+        v ^= gf.mul(rows[r * k + (uint32_t)__builtin_ctz(ss)], G(u, ne + t));
+      const uint32_t co = horner_coords(field, v), rt = (uint32_t)__builtin_ctz(rr);
+      for (int j = 0; j < nb; ++j)
+        if ((co >> (nb - 1 - j)) & 1u) hm[j >> 2] |= 1u << (8 * (j & 3) + rt);
     }
+    for (int q = 0; q < 4; ++q) d.hm[o][q] = hm[q];
   }
-  uint32_t synd = 0, sigma = 0;
-  for (uint32_t t = 0; t < ne; ++t) {
-    synd |= 1u << R[t];
-    d.par[R[t]] = sb + (uint64_t)(k + R[t]) * shard_bytes;
+  for (uint32_t rr = rmask; rr; rr &= rr - 1u) {
+    const uint32_t r = (uint32_t)__builtin_ctz(rr);
+    d.par[r] = sb + (uint64_t)(k + r) * shard_bytes;
   }
-  sigma = synd;
-  for (uint32_t m = 0; m < nm; ++m) sigma |= 1u << M[m];
-  d.synd = synd;
-  d.sigma = sigma;
+  d.synd = rmask;
+  d.sigma = rmask | mmask;
   d.n_out = o;
-  set_horner_masks(d, field);
 }
 
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
@@ -697,13 +710,14 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
 
 hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                                        const uint16_t* parity_rows, const uint16_t* d_rows,
-                                       const uint8_t* d_present, uint32_t data_only,
-                                       uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
-                                       uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
-                                       uint64_t* done) {
+                                       const uint8_t* d_tabs, const uint8_t* d_present,
+                                       uint32_t data_only, uint8_t* base, uint64_t shard_bytes,
+                                       uint32_t n_stripes, uint32_t need, uint32_t e_cap,
+                                       BsReconArgs* d_descs, hipStream_t stream, uint64_t* done) {
   *done = 0;
   if (!get_option(5) || shard_bytes < 4096 || k == 0 || k > (uint32_t)kMaxIn ||
-      p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0)
+      p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0 || e_cap == 0 ||
+      e_cap > (uint32_t)kMaxOut)
     return hipSuccess;
   BsDescFn sfn = nullptr;
   BsDesc4Fn sfn4 = nullptr;
@@ -742,9 +756,11 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       }
     if (!jfn) return hipSuccess;
   }
+  // the planner's Gauss-Jordan workspace: e_cap x 2 e_cap halfwords per lane
+  const size_t gj_lds = (size_t)e_cap * 2u * e_cap * kPlanBlock * sizeof(uint16_t);
   hipLaunchKernelGGL(bs_recon_plan_kernel, dim3((n_stripes + kPlanBlock - 1) / kPlanBlock),
-                     dim3(kPlanBlock), 0, stream, field, d_rows, d_present, k, p, data_only, base,
-                     shard_bytes, n_stripes, d_descs);
+                     dim3(kPlanBlock), gj_lds, stream, field, d_rows, d_tabs, d_present, k, p,
+                     data_only, base, shard_bytes, n_stripes, e_cap, d_descs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int64_t grid = get_option(2);

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstring>
 #include <list>
@@ -1771,18 +1772,27 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     want_bitslice(c, sb, false, n_stripes);
     if (need > 0) {
       const Rows& rows = prow;
-      const size_t rows_bytes = rows.c.size() * 2, desc_off = (rows_bytes + 255) & ~size_t(255);
+      // workspace: the parity rows, the planner's GF(2^8) tables, the descriptors
+      static const auto tabs = [] {
+        std::array<uint8_t, rse::kPlanTabBytes> t{};
+        rse::plan_tables(t.data());
+        return t;
+      }();
+      const size_t rows_bytes = rows.c.size() * 2, tab_off = (rows_bytes + 255) & ~size_t(255);
+      const size_t desc_off = tab_off + ((rse::kPlanTabBytes + 255) & ~size_t(255));
       uint8_t* ws = nullptr;
       hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws),
                                     desc_off + n_stripes * sizeof(rse::BsReconArgs), st);
       if (e != hipSuccess) return dev_fail(release(e));
       e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ws + tab_off, tabs.data(), tabs.size(), hipMemcpyHostToDevice, st);
       uint64_t bs_done = 0;
       if (e == hipSuccess)
         e = rse::launch_bitslice_recon_batch(
             c->field, (uint32_t)k, (uint32_t)p, rows.c.data(), reinterpret_cast<uint16_t*>(ws),
-            dflags, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
-            reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
+            ws + tab_off, dflags, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
+            e_cap, reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
       hipError_t f = hipFreeAsync(ws, st);
       if (e == hipSuccess) e = f;
       if (e == hipSuccess && bs_done == sb) {

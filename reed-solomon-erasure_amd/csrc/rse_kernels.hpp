@@ -247,14 +247,33 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
 // inverse, mixing rows), then the syndrome kernels code the whole 16 KiB
 // chunks of every stripe from them, and the whole 4 KiB chunks of the rest
 // (one per wave).  d_rows: the p x k parity rows on the device (parity_rows:
-// the same on the host, to select the kernels); need: sigma rows any stripe
-// uses (max row + 1).  *done = bytes of every shard coded (0: nothing queued).
+// the same on the host, to select the kernels); d_tabs: the GF(2^8) log and
+// exp tables on the device (kPlanTabBytes, plan_tables); need: sigma rows any
+// stripe uses (max row + 1); e_cap: missing data shards any stripe has.
+// *done = bytes of every shard coded (0: nothing queued).
+constexpr size_t kPlanTabBytes = 256 + 512;
 hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                                        const uint16_t* parity_rows, const uint16_t* d_rows,
-                                       const uint8_t* d_present, uint32_t data_only,
-                                       uint8_t* base, uint64_t shard_bytes, uint32_t n_stripes,
-                                       uint32_t need, BsReconArgs* d_descs, hipStream_t stream,
-                                       uint64_t* done);
+                                       const uint8_t* d_tabs, const uint8_t* d_present,
+                                       uint32_t data_only, uint8_t* base, uint64_t shard_bytes,
+                                       uint32_t n_stripes, uint32_t need, uint32_t e_cap,
+                                       BsReconArgs* d_descs, hipStream_t stream, uint64_t* done);
+// The planner's tables: log[256] then exp[512] of GF(2^8), generator 2
+// modulo 0x11D (build.rs:13-43), exp doubled so exp[log a + log b] needs no
+// reduction; log[0] = 0 and exp[510..511] = 0 are never read for nonzero a, b.
+inline void plan_tables(uint8_t* t) {  // kPlanTabBytes bytes
+  uint8_t* lg = t;
+  uint8_t* ex = t + 256;
+  uint32_t b = 1;
+  for (uint32_t l = 0; l < 255; ++l) {
+    lg[b] = (uint8_t)l;
+    ex[l] = ex[l + 255] = (uint8_t)b;
+    b <<= 1;
+    if (b & 0x100u) b ^= 0x11Du;
+  }
+  lg[0] = 0;
+  ex[510] = ex[511] = 0;
+}
 
 // ---- run-time specialisation (rse_jit.cpp) ----------------------------------
 // Bit-sliced kernels for codecs not compiled into the library: the XOR networks

@@ -168,6 +168,7 @@ def test_bench_legs_on_the_gpu():
         if field == 8:
             a, b = bench.verify_leg(r, v, k, p, nb, n, reps=2)
             assert a["verdicts_ok"] is True and b["verdicts_ok"] is True
+            assert a["c_abi"]["verdicts_ok"] is True and a["c_abi"]["us_per_call"] > 0
             assert r.verify_flat(v.view(-1), nb, n).all()  # restored
             a, b = bench.verify_leg(_NoOp(), v, k, p, nb, n, reps=2)
             assert a["verdicts_ok"] is False and b["verdicts_ok"] is False
