@@ -74,6 +74,16 @@ struct rse_codec {
   // run-time specialisation requested (rse_jit.cpp; see want_bitslice)
   mutable std::atomic<bool> jit_requested{false};
   mutable std::atomic<uint64_t> wide_bytes{0};  // shard bytes a wide codec has coded (want_bitslice)
+  // Per device: the parity rows (p x k halfwords) and, 256-aligned after them,
+  // the device planners' GF(2^8) tables (rse::plan_tables), made on the first
+  // batched reconstruct there and kept for the codec's life (plan_consts), so
+  // a call copies neither.
+  static constexpr int kDevs = 64;
+  mutable std::atomic<uint8_t*> plan_dev[kDevs] = {};
+  ~rse_codec() {
+    for (auto& a : plan_dev)
+      if (uint8_t* q = a.load()) (void)hipFree(q);
+  }
 
   size_t esize() const { return field == 16 ? 2 : 1; }
   uint16_t mat(size_t r, size_t c) const { return field == 16 ? m16.at(r, c) : m8.at(r, c); }
@@ -564,6 +574,39 @@ Rows parity_rows(const rse_codec* c) {  // core.rs:420-428
   for (size_t i = 0; i < c->p; ++i)
     for (size_t j = 0; j < c->k; ++j) r.c[i * c->k + j] = c->mat(c->k + i, j);
   return r;
+}
+
+// Byte offset of the planner tables in a codec's plan constants.
+size_t plan_tab_off(const rse_codec* c) { return (c->p * c->k * 2 + 255) & ~size_t(255); }
+
+// The codec's plan constants on device `dev` (rse_codec::plan_dev): made once
+// per device, with a synchronous copy (the first batched reconstruct there
+// pays it); two threads racing keep one copy and free the other.
+hipError_t plan_consts(const rse_codec* c, int dev, const uint8_t** out) {
+  if (dev < 0 || dev >= rse_codec::kDevs) return hipErrorInvalidDevice;
+  if (uint8_t* q = c->plan_dev[dev].load(std::memory_order_acquire)) {
+    *out = q;
+    return hipSuccess;
+  }
+  const Rows r = parity_rows(c);
+  const size_t off = plan_tab_off(c);
+  std::vector<uint8_t> h(off + rse::kPlanTabBytes, 0);
+  std::memcpy(h.data(), r.c.data(), r.c.size() * 2);
+  rse::plan_tables(h.data() + off);
+  uint8_t* q = nullptr;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), h.size());
+  if (e == hipSuccess) e = hipMemcpy(q, h.data(), h.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (q) (void)hipFree(q);
+    return e;
+  }
+  uint8_t* expect = nullptr;
+  if (!c->plan_dev[dev].compare_exchange_strong(expect, q, std::memory_order_acq_rel)) {
+    (void)hipFree(q);
+    q = expect;
+  }
+  *out = q;
+  return hipSuccess;
 }
 
 // Codecs without compiled-in bit-sliced kernels get them built for their
@@ -1772,27 +1815,21 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     want_bitslice(c, sb, false, n_stripes);
     if (need > 0) {
       const Rows& rows = prow;
-      // workspace: the parity rows, the planner's GF(2^8) tables, the descriptors
-      static const auto tabs = [] {
-        std::array<uint8_t, rse::kPlanTabBytes> t{};
-        rse::plan_tables(t.data());
-        return t;
-      }();
-      const size_t rows_bytes = rows.c.size() * 2, tab_off = (rows_bytes + 255) & ~size_t(255);
-      const size_t desc_off = tab_off + ((rse::kPlanTabBytes + 255) & ~size_t(255));
-      uint8_t* ws = nullptr;
-      hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws),
-                                    desc_off + n_stripes * sizeof(rse::BsReconArgs), st);
+      // the parity rows and the planner's tables: the codec's device copy
+      const uint8_t* consts = nullptr;
+      int dev = 0;
+      hipError_t e = hipGetDevice(&dev);
+      if (e == hipSuccess) e = plan_consts(c, dev, &consts);
       if (e != hipSuccess) return dev_fail(release(e));
-      e = hipMemcpyAsync(ws, rows.c.data(), rows_bytes, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(ws + tab_off, tabs.data(), tabs.size(), hipMemcpyHostToDevice, st);
+      uint8_t* ws = nullptr;  // the descriptors
+      e = hipMallocAsync(reinterpret_cast<void**>(&ws), n_stripes * sizeof(rse::BsReconArgs), st);
+      if (e != hipSuccess) return dev_fail(release(e));
       uint64_t bs_done = 0;
-      if (e == hipSuccess)
-        e = rse::launch_bitslice_recon_batch(
-            c->field, (uint32_t)k, (uint32_t)p, rows.c.data(), reinterpret_cast<uint16_t*>(ws),
-            ws + tab_off, dflags, data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need,
-            e_cap, reinterpret_cast<rse::BsReconArgs*>(ws + desc_off), st, &bs_done);
+      e = rse::launch_bitslice_recon_batch(
+          c->field, (uint32_t)k, (uint32_t)p, rows.c.data(),
+          reinterpret_cast<const uint16_t*>(consts), consts + plan_tab_off(c), dflags,
+          data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need, e_cap,
+          reinterpret_cast<rse::BsReconArgs*>(ws), st, &bs_done);
       hipError_t f = hipFreeAsync(ws, st);
       if (e == hipSuccess) e = f;
       if (e == hipSuccess && bs_done == sb) {
@@ -1836,19 +1873,22 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   const size_t per_stripe = n_ib * n_ob * sizeof(CodeArgs);
   // stripes per planning group: descriptors of at most 256 MiB at a time
   const size_t grp = std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per_stripe));
-  const size_t p_bytes = prow.c.size() * sizeof(uint16_t), desc_off = (p_bytes + 255) & ~size_t(255);
-  uint8_t* ws = nullptr;
+  const uint8_t* consts = nullptr;  // the parity rows on the device (plan_consts)
+  uint8_t* ws = nullptr;            // the descriptors
   {
-    const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), desc_off + grp * per_stripe, st);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = plan_consts(c, dev, &consts);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&ws), grp * per_stripe, st);
     if (e != hipSuccess) return dev_fail(release(e));
   }
-  hipError_t e = hipMemcpyAsync(ws, prow.c.data(), p_bytes, hipMemcpyHostToDevice, st);
+  hipError_t e = hipSuccess;
   for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {
     const size_t ng = std::min(grp, n_stripes - g0);
-    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(ws), dflags + g0 * T,
+    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(consts), dflags + g0 * T,
                                (uint32_t)k, (uint32_t)T, data_only ? 1u : 0u, e_cap, nout_cap,
                                base + g0 * T * sb, sb, done, sb - done, (uint32_t)ng,
-                               reinterpret_cast<CodeArgs*>(ws + desc_off), st);
+                               reinterpret_cast<CodeArgs*>(ws), st);
   }
   const hipError_t f = hipFreeAsync(ws, st);
   const hipError_t g = release(hipSuccess);
