@@ -356,7 +356,8 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                         (default) one pair per workgroup, 2 two pairs per workgroup
                                         (compiled codecs; run-time ones use two); 0: one wave holds
                                         all 8 rows; A/B variants of the compiled codecs (one pair):
-                                        3 next unit prefetched, 6 compact mixing; 4 / 5 timing
+                                        3 next unit prefetched, 6 compact mixing, 7 two inputs
+                                        in flight per wave; 4 / 5 timing
                                         splits that skip the Horner steps / data networks (WRONG
                                         bytes: tools/tune.py only) */
 #define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch

@@ -195,8 +195,9 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
 // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD),
 // P pairs per workgroup.
 // PF: the next unit's first input loaded during the mixing (A/B, option 28 = 3).
-// DBG: A/B variants (RSE_OPT_RECON_PAIRS 4-6): 1 / 2 skip the Horner steps /
-// the data networks (tune-only timing splits, wrong bytes), 3 the compact mixing.
+// DBG: A/B variants (RSE_OPT_RECON_PAIRS 4-7): 1 / 2 skip the Horner steps /
+// the data networks (tune-only timing splits, wrong bytes), 3 the compact
+// mixing, 4 two own inputs in flight per wave.
 template <class C, int P, bool PF = false, int DBG = 0>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_pair_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
@@ -387,10 +388,11 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
-  BsRecFn rec_pair[6];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
-  BsDescFn rec_desc_pair[6];   // pair with the next unit prefetched (nullptr below 8 rows),
+  BsRecFn rec_pair[7];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
+  BsDescFn rec_desc_pair[7];   // pair with the next unit prefetched (nullptr below 8 rows),
                                // [3] / [4]: no Horner steps / no data networks (timing
-                               // splits, wrong bytes), [5]: compact mixing (pair_slot)
+                               // splits, wrong bytes), [5]: compact mixing, [6]: two own
+                               // inputs in flight per wave (pair_slot)
 };
 
 template <class C, int NS, int MIX>
@@ -459,9 +461,10 @@ constexpr BsDescFn rec_desc_deep_fn() {
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
    {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>(),            \
     rec_pair_fn<C, 1, false, 1>(), rec_pair_fn<C, 1, false, 2>(),                   \
-    rec_pair_fn<C, 1, false, 3>()},                                                 \
+    rec_pair_fn<C, 1, false, 3>(), rec_pair_fn<C, 1, false, 4>()},                  \
    {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>(), rec_desc_pair_fn<C, 1, true>(), \
-    nullptr, nullptr, rec_desc_pair_fn<C, 1, false, 3>()}}
+    nullptr, nullptr, rec_desc_pair_fn<C, 1, false, 3>(),                           \
+    rec_desc_pair_fn<C, 1, false, 4>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -532,6 +535,10 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     j16 = a.accumulate ? jf.enc_acc : jf.enc;
     j4 = a.accumulate ? jf.enc4_acc : jf.enc4;
     if (!j16) return hipSuccess;
+    if (a.mode != kStore && !a.accumulate && nt && jf.chk && get_option(4) < 0) {
+      j16 = jf.chk;  // the check kernel, which can signal the call's completion
+      chk = true;
+    }
   }
   // tools/tune.py sweeps: GF(2^8) 4096 workgroups (16384 at <= 2 outputs: 10+2
   // x 1 MiB +0.8-1.1 % in two processes, profiles/r03/s12, s13), GF(2^16)
@@ -627,10 +634,10 @@ int recon_depth(int mix) {
 
 // index into BsShape::rec_pair / rec_desc_pair: option 28 = 3 the prefetching
 // variant, 4 / 5 the timing splits (no Horner steps / no data networks; wrong
-// bytes, tools/tune.py only), 6 the compact mixing
+// bytes, tools/tune.py only), 6 the compact mixing, 7 two inputs in flight
 int pair_slot() {
   const int64_t o = get_option(28);
-  return o >= 3 && o <= 6 ? (int)o - 1 : pair_groups() - 1;
+  return o >= 3 && o <= 7 ? (int)o - 1 : pair_groups() - 1;
 }
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,

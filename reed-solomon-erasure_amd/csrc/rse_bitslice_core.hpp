@@ -1536,12 +1536,56 @@ __device__ __forceinline__ bool pair_prefetch(u32x4 (&nxt)[4], const BsReconArgs
   return true;
 }
 
+// The wave's own input two after index J, loaded into nxt (the depth-2
+// pipeline, DBG 4); returns whether there is one.
+template <class C, bool NT>
+__device__ __forceinline__ bool pair_prefetch2(u32x4 (&nxt)[4], const BsReconArgs& a, uint64_t own,
+                                               int J, uint64_t off) {
+  uint64_t rest = own & ~((2ull << J) - 1ull);
+  if (!rest) return false;
+  rest &= rest - 1ull;
+  if (!rest) return false;
+  load4<NT, 1024u>(nxt, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(rest)) + off);
+  return true;
+}
+
+// One own input of the wave: the next load(s) issued, then cur sliced into
+// pl.  Depth 1: the next own input into nxt, then cur = nxt.  Depth 2 (DBG
+// 4): nx1 already holds the next one in flight; the one after it is issued,
+// then cur = nx1, nx1 = it.
+template <class C, bool NT, int DBG>
+__device__ __forceinline__ void pair_advance(u32x4 (&cur)[4], u32x4 (&nx1)[4], uint32_t (&pl)[16],
+                                             const BsReconArgs& a, uint64_t own, int J, uint64_t off) {
+  if constexpr (DBG == 4) {
+    u32x4 nx2[4];
+    const bool more2 = pair_prefetch2<C, NT>(nx2, a, own, J, off);
+    __builtin_amdgcn_sched_barrier(0);
+    slice<typename C::Field>(cur, pl);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nx1[j];
+    if (more2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nx1[j] = nx2[j];
+    }
+  } else {
+    u32x4 nxt[4];
+    const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
+    __builtin_amdgcn_sched_barrier(0);
+    slice<typename C::Field>(cur, pl);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
+  }
+}
+
 // Data rounds T.. : indices 2T (role 0) and 2T + 1 (role 1).
 // DBG (tune-only A/B variants, results not valid): 1 skips the Horner steps of
 // the mixing, 2 the data inputs' networks (mac_rows) -- to split the kernel's
 // time between its phases.
 template <class C, bool NT, int H, int T, int P, int DBG = 0>
 __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4 (&cur)[4],
+                                          u32x4 (&nx1)[4],
                                           const BsReconArgs& a, uint64_t own, uint32_t present,
                                           uint64_t off, u32x4 (*mine)[64], u32x4 (*theirs)[64],
                                           uint32_t lane, uint32_t& buf) {
@@ -1555,17 +1599,10 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
       u32x4* const wr = mine[buf * (P * 2 * 4)];
       const u32x4* const rd = theirs[buf * (P * 2 * 4)];
       if (has_own) {
-        u32x4 nxt[4];
-        const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
-        __builtin_amdgcn_sched_barrier(0);
-        slice<typename C::Field>(cur, pl);
+        pair_advance<C, NT, DBG>(cur, nx1, pl, a, own, J, off);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           wr[j * 64 + lane] = (u32x4){pl[4 * j], pl[4 * j + 1], pl[4 * j + 2], pl[4 * j + 3]};
-        if (more) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-        }
       }
       __syncthreads();
       if (DBG != 2 && has_own) mac_rows<C, J, H * kPairRows>(acc, pl);
@@ -1585,7 +1622,7 @@ __device__ __forceinline__ void pair_data(uint32_t (&acc)[kPairRows * 16], u32x4
       for (int q = 0; q < kPairRows * 16; ++q) asm volatile("" : "+v"(acc[q]));
       buf ^= 1u;
     }
-    pair_data<C, NT, H, T + 1, P, DBG>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+    pair_data<C, NT, H, T + 1, P, DBG>(acc, cur, nx1, a, own, present, off, mine, theirs, lane, buf);
   }
 }
 
@@ -1653,28 +1690,26 @@ __device__ __forceinline__ bool recon_pair_unit(const BsReconArgs& a, uint64_t o
   uint32_t acc[kPairRows * 16];
 #pragma unroll
   for (int q = 0; q < kPairRows * 16; ++q) acc[q] = 0u;
+  u32x4 nx1[4];  // depth 2 (DBG 4): the own input after cur, in flight
   if (own && !primed)
     load4<NT, 1024u>(cur, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(own)) + off);
+  if constexpr (DBG == 4) {
+    const uint64_t rest = own & (own - 1ull);
+    if (rest) load4<NT, 1024u>(nx1, recon_ptr(a, C::k, (uint32_t)__builtin_ctzll(rest)) + off);
+  }
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
-  pair_data<C, NT, H, 0, P, DBG>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  pair_data<C, NT, H, 0, P, DBG>(acc, cur, nx1, a, own, present, off, mine, theirs, lane, buf);
   // own syndrome rows: s_r = sigma_r ^ parity_r
 #pragma unroll
   for (int i = 0; i < kPairRows; ++i) {
     const int J = C::k + R0 + i;
     if ((own >> J) & 1u) {
-      u32x4 nxt[4];
-      const bool more = pair_prefetch<C, NT>(nxt, a, own, J, off);
-      __builtin_amdgcn_sched_barrier(0);
       uint32_t pl[16];
-      slice<F>(cur, pl);
+      pair_advance<C, NT, DBG>(cur, nx1, pl, a, own, J, off);
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i * 16 + q] ^= pl[q];
-      if (more) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-      }
     }
   }
   const bool prime = own && next_off != ~0ull;
@@ -1760,7 +1795,7 @@ __device__ __forceinline__ void pair_inputs(const BsReconArgs& a, uint64_t off, 
   uint32_t buf = 0;
   u32x4(*mine)[64] = lds.v[0][pair][H];
   u32x4(*theirs)[64] = lds.v[0][pair][1 - H];
-  pair_data<C, NT, H, 0, P>(acc, cur, a, own, present, off, mine, theirs, lane, buf);
+  pair_data<C, NT, H, 0, P>(acc, cur, cur, a, own, present, off, mine, theirs, lane, buf);
 #pragma unroll
   for (int i = 0; i < kPairRows; ++i) {
     const int J = C::k + R0 + i;

@@ -357,7 +357,35 @@ struct Scratch {
   uint32_t* count = nullptr;  // run_check's device workgroup count (signal_done), zero when idle
   uint8_t* dbuf = nullptr;
   size_t dbytes = 0;
+  // rse_reconstruct_batch's device workspace (flags, scan words, per-stripe
+  // descriptors), kept between calls up to kPlanKeep bytes
+  uint8_t* pbuf = nullptr;
+  size_t pbytes = 0;
 };
+constexpr size_t kPlanKeep = size_t(128) << 20;
+
+// The lease's planner workspace of at least `bytes` (kept when at most
+// kPlanKeep; a larger one is a stream-ordered allocation on `st` for the
+// call: *owned is set and the caller frees it with hipFreeAsync).
+hipError_t lease_plan(Scratch* s, size_t bytes, hipStream_t st, uint8_t** out, bool* owned) {
+  *owned = false;
+  if (s->pbytes >= bytes) {
+    *out = s->pbuf;
+    return hipSuccess;
+  }
+  if (bytes > kPlanKeep) {
+    *owned = true;
+    return hipMallocAsync(reinterpret_cast<void**>(out), bytes, st);
+  }
+  if (s->pbuf) (void)hipFree(s->pbuf);  // idle: the previous call synchronised
+  s->pbuf = nullptr;
+  s->pbytes = 0;
+  const hipError_t e = hipMalloc(reinterpret_cast<void**>(&s->pbuf), bytes);
+  if (e != hipSuccess) return e;
+  s->pbytes = bytes;
+  *out = s->pbuf;
+  return hipSuccess;
+}
 
 void drop_pipe_streams(Scratch& s) {
   for (auto& q : s.st) (void)hipStreamDestroy(q);
@@ -376,6 +404,7 @@ void destroy_scratch(Scratch* s) {  // idle: its last call synchronised
   if (s->done) (void)hipEventDestroy(s->done);
   if (s->own) (void)hipStreamDestroy(s->own);
   if (s->dbuf) (void)hipFree(s->dbuf);
+  if (s->pbuf) (void)hipFree(s->pbuf);
   if (s->count) (void)hipFree(s->count);
   if (s->wh) (void)hipHostFree(s->wh);
   delete s;
@@ -1709,6 +1738,10 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       while (s1 < n_stripes && std::memcmp(present + s1 * T, present + s0 * T, T) == 0) ++s1;
       runs.emplace_back(s0, s1 - s0);
       if (runs.size() * 16 > n_stripes) break;
+      // per-stripe patterns show in the first stripes: stop once a prefix
+      // holds many runs at over twice the admitted density (this only picks
+      // the faster path; both give the same bytes)
+      if (runs.size() >= 64 && runs.size() * 8 > s1) break;
       s0 = s1;
     }
     size_t covered = 0;
@@ -1735,10 +1768,19 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   // The flags go to the device once (the planners read them there); a large
   // batch is validated there too, one lane per stripe.
   uint32_t need = 0, e_cap = 0, nout_cap = 0;
-  uint8_t* dflags = nullptr;  // n_stripes * T flags, then the scan's 6 result words
+  // The device workspace, the lease's (kept between calls): n_stripes * T
+  // flags, the scan's 6 result words, then (bit-sliced path) the per-stripe
+  // descriptors.  Every return after work was queued has synchronised the
+  // stream, so the lease goes back to the pool idle.
+  uint8_t* dflags = nullptr;
+  bool ws_owned = false;  // past kPlanKeep: allocated for this call
   const size_t fl_bytes = (n_stripes * T + 255) & ~size_t(255);
-  auto release = [&](hipError_t e) {  // drop dflags after the stream's work on it
-    if (dflags) (void)hipFreeAsync(dflags, st);
+  const size_t desc_off = (fl_bytes + 64 + 255) & ~size_t(255);
+  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
+  const bool bs_path = fits && sb >= 4096 && sb % 16u == 0 && aligned16(base) &&
+                       rse::get_option(RSE_OPT_BITSLICE);
+  auto release = [&](hipError_t e) {  // after the stream's work on the workspace
+    if (dflags && ws_owned) (void)hipFreeAsync(dflags, st);
     dflags = nullptr;
     return e;
   };
@@ -1758,7 +1800,11 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     }
     if (nout_cap == 0) return RSE_OK;  // nothing this call rebuilds, in any stripe
   }
-  RSE_HIP(hipMallocAsync(reinterpret_cast<void**>(&dflags), fl_bytes + 64, st));
+  Lease lease;
+  RSE_HIP(lease.acquire());
+  RSE_HIP(lease_plan(lease.get(),
+                     desc_off + (bs_path ? n_stripes * sizeof(rse::BsReconArgs) : 0), st,
+                     &dflags, &ws_owned));
   if (!dev_scan) {
     hipError_t e = hipMemcpyAsync(dflags, present, n_stripes * T, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return dev_fail(release(e));
@@ -1768,10 +1814,8 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     // the first words
     // (pinned words only up to 16 MiB of flags: a lease keeps its words, and
     // the pool keeps up to kIdleScratch leases)
-    Lease lease;
     const bool staged = n_stripes * T <= (size_t(16) << 20);
-    hipError_t e = lease.acquire();
-    if (e == hipSuccess) e = lease_words(lease.get(), 8 + (staged ? (n_stripes * T + 3) / 4 : 0));
+    hipError_t e = lease_words(lease.get(), 8 + (staged ? (n_stripes * T + 3) / 4 : 0));
     uint32_t* res = reinterpret_cast<uint32_t*>(dflags + fl_bytes);
     if (e == hipSuccess) {
       if (staged) std::memcpy(lease->wh + 8, present, n_stripes * T);
@@ -1804,14 +1848,12 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     RSE_HIP(hipStreamSynchronize(st));
     return RSE_OK;
   }
-  const bool fits = k <= (size_t)kMaxIn && p <= (size_t)kMaxOut && n_stripes <= 0xffffffffu;
   size_t done = 0;  // bytes of every shard coded so far
   // host inputs of the copies below: alive until the stream is synchronised
   const Rows prow = parity_rows(c);
   // 1. whole 16 KiB chunks on the bit-sliced syndrome kernels (compiled or
   //    run-time specialised codecs), planned per stripe on the device
-  if (fits && sb >= 4096 && sb % 16u == 0 && aligned16(base) &&
-      rse::get_option(RSE_OPT_BITSLICE)) {
+  if (bs_path) {
     want_bitslice(c, sb, false, n_stripes);
     if (need > 0) {
       const Rows& rows = prow;
@@ -1821,17 +1863,13 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = plan_consts(c, dev, &consts);
       if (e != hipSuccess) return dev_fail(release(e));
-      uint8_t* ws = nullptr;  // the descriptors
-      e = hipMallocAsync(reinterpret_cast<void**>(&ws), n_stripes * sizeof(rse::BsReconArgs), st);
-      if (e != hipSuccess) return dev_fail(release(e));
+      uint8_t* ws = dflags + desc_off;  // the descriptors
       uint64_t bs_done = 0;
       e = rse::launch_bitslice_recon_batch(
           c->field, (uint32_t)k, (uint32_t)p, rows.c.data(),
           reinterpret_cast<const uint16_t*>(consts), consts + plan_tab_off(c), dflags,
           data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need, e_cap,
           reinterpret_cast<rse::BsReconArgs*>(ws), st, &bs_done);
-      hipError_t f = hipFreeAsync(ws, st);
-      if (e == hipSuccess) e = f;
       if (e == hipSuccess && bs_done == sb) {
         e = release(hipSuccess);
         if (e == hipSuccess) e = hipStreamSynchronize(st);  // `prow` dies next

@@ -279,6 +279,18 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                     acc ? "true" : "false");
       s += buf;
     }
+    if (!acc) {
+      // the check kernel of a synchronous verify: the stored parity loaded
+      // before un-slicing, and the completion word (rse_device.hpp
+      // signal_done) that lets the call return without synchronising
+      std::snprintf(buf, sizeof buf,
+                    "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_check(\n"
+                    "    const rse::CodeArgs a, uint64_t cps) {\n"
+                    "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, false, "
+                    "false, true>(a, cps);\n  rse::signal_done(a);\n}\n",
+                    p > 4 ? 2 : 3);
+      s += buf;
+    }
     return s;
   }
   int ns[5];
@@ -906,6 +918,7 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
       } else {
         if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
         if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4, m, "rse_jit_encode4");
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.chk, m, "rse_jit_check");
       }
     } else {
       f.n_rec = recon_ns(p, f.rec_ns);

@@ -334,6 +334,7 @@ struct JitFns {
   hipFunction_t enc = nullptr;  // bitslice encode/verify (CodeArgs, chunks per stripe)
   hipFunction_t enc4 = nullptr; // ... over 4 KiB chunks, one per wave
   hipFunction_t enc_acc = nullptr, enc4_acc = nullptr;  // accumulate mode (kJitBlockAcc)
+  hipFunction_t chk = nullptr;  // the check modes' kernel, with the completion word
   int n_rec = 0;
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)

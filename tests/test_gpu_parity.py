@@ -815,7 +815,7 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
 
 # RSE_OPT_RECON_PAIRS: pairs per workgroup (1, 2); 3 the prefetching variant,
 # 6 the compact mixing (one pair per workgroup)
-@pytest.mark.parametrize("pairs", [1, 2, 3, 6])
+@pytest.mark.parametrize("pairs", [1, 2, 3, 6, 7])
 def test_reconstruct_wave_pairs(R, pairs):
     """GF(2^16) 20+8 syndrome reconstruct at 8 sigma rows on wave pairs
     (RSE_OPT_RECON_PAIRS, the default): each wave of a pair holds 4 syndrome
@@ -1530,5 +1530,37 @@ def test_wide_reconstruct_pattern_blocks(R, field, k, p, erased):
         for s_ in range(stripes):
             for i in range(k):
                 assert (got[s_, i] == full[i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old)
+
+
+@pytest.mark.parametrize("k,p", [(12, 4), (6, 3)])
+def test_jit_verify_completion_word(R, k, p):
+    """verify() of a run-time specialised codec (rse_jit.cpp rse_jit_check)
+    returns through the kernel's completion word like the compiled codecs':
+    whole 16 KiB chunks only, so one check launch is the whole call.  Clean
+    stripes verify, and a byte flipped anywhere -- first or last chunk, data
+    or parity -- is caught (a kernel that signalled before every verdict store
+    landed would miss some)."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    old = lib.rse_get_option(9)
+    lib.rse_set_option(9, 2)  # wait for the codec's module
+    try:
+        rng = np.random.default_rng(4242 + k)
+        n = 16384 * 37
+        full = rand_shards(rng, k, n) + [np.zeros(n, np.uint8) for _ in range(p)]
+        O.Codec(8, k, p).encode(full)
+        r = R.galois_8.ReedSolomon(k, p)
+        shards = [dev(x) for x in full]
+        for _ in range(3):
+            assert r.verify(shards)
+        assert last_kernel().startswith(f"bitslice-jit gf8 {k}+{p}"), last_kernel()
+        for shard, off in [(0, 0), (k - 1, n - 1), (k, 5), (k + p - 1, n - 16384), (k // 2, n // 2)]:
+            t = shards[shard]
+            t[off] ^= 0x81
+            assert not r.verify(shards), (shard, off)
+            t[off] ^= 0x81
+            assert r.verify(shards)
     finally:
         lib.rse_set_option(9, old)
