@@ -344,20 +344,26 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_RECON_DEPTH 27       /* syndrome reconstruct: inputs in flight per lane (1..4) */
 #define RSE_OPT_SYNC_EVENT 30        /* 1: verify calls wait on an event recorded after their
                                         kernels instead of synchronising the stream (A/B; 0 default) */
-#define RSE_OPT_SPIN_WAIT 31         /* 1 (default): a verify that is one compiled check-kernel
-                                        launch signals its completion through a word of pinned host
-                                        memory, which the call polls instead of synchronising the
-                                        stream; 0: synchronise (A/B) */
+#define RSE_OPT_SPIN_WAIT 31         /* 1 (default): a verify that is one check-kernel launch
+                                        (compiled or run-time specialised codecs) signals its
+                                        completion through a word of pinned host memory, which the
+                                        call polls instead of synchronising the stream; 0:
+                                        synchronise (A/B) */
+#define RSE_OPT_HOST_DIRECT 32       /* 1 (default): a *_host call on one stripe that moves at most
+                                        2 MiB goes through one pinned staging buffer (CPU copies,
+                                        one DMA each way) instead of the chunk pipeline's per-shard
+                                        copies; 0: always the pipeline (A/B) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */
 #define RSE_OPT_RECON_PAIRS 28       /* syndrome reconstruct at 8 sigma rows on wave pairs (4 rows
                                         each, planes shared through LDS, 3 waves per SIMD): 1
-                                        (default) one pair per workgroup, 2 two pairs per workgroup
+                                        (default) one pair per workgroup with two inputs in flight
+                                        per wave, 2 two pairs per workgroup
                                         (compiled codecs; run-time ones use two); 0: one wave holds
                                         all 8 rows; A/B variants of the compiled codecs (one pair):
-                                        3 next unit prefetched, 6 compact mixing, 7 two inputs
-                                        in flight per wave; 4 / 5 timing
+                                        3 next unit prefetched, 6 compact mixing, 7 one input in
+                                        flight per wave (round 3's kernel); 4 / 5 timing
                                         splits that skip the Horner steps / data networks (WRONG
                                         bytes: tools/tune.py only) */
 #define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch

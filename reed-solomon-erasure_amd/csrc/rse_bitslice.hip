@@ -195,9 +195,9 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
 // 8 sigma rows on wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing, 3 waves/SIMD),
 // P pairs per workgroup.
 // PF: the next unit's first input loaded during the mixing (A/B, option 28 = 3).
-// DBG: A/B variants (RSE_OPT_RECON_PAIRS 4-7): 1 / 2 skip the Horner steps /
-// the data networks (tune-only timing splits, wrong bytes), 3 the compact
-// mixing, 4 two own inputs in flight per wave.
+// DBG: 4 two own inputs in flight per wave (the default); A/B variants
+// (RSE_OPT_RECON_PAIRS 4-6): 1 / 2 skip the Horner steps / the data networks
+// (tune-only timing splits, wrong bytes), 3 the compact mixing.
 template <class C, int P, bool PF = false, int DBG = 0>
 __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_pair_kernel(
     const BsReconArgs a, uint64_t chunks_per_stripe) {
@@ -388,11 +388,12 @@ struct BsShape {
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
-  BsRecFn rec_pair[7];         // NS = 8 on wave pairs, [pairs per workgroup - 1], [2]: one
-  BsDescFn rec_desc_pair[7];   // pair with the next unit prefetched (nullptr below 8 rows),
-                               // [3] / [4]: no Horner steps / no data networks (timing
-                               // splits, wrong bytes), [5]: compact mixing, [6]: two own
-                               // inputs in flight per wave (pair_slot)
+  BsRecFn rec_pair[7];         // NS = 8 on wave pairs (nullptr below 8 rows), by pair_slot:
+  BsDescFn rec_desc_pair[7];   // [0] one pair per workgroup, two own inputs in flight per
+                               // wave, [1] two pairs, [2] one pair with the next unit
+                               // prefetched, [3] / [4] no Horner steps / no data networks
+                               // (timing splits, wrong bytes), [5] compact mixing, [6] [0]
+                               // with one input in flight (round 3's kernel)
 };
 
 template <class C, int NS, int MIX>
@@ -459,12 +460,12 @@ constexpr BsDescFn rec_desc_deep_fn() {
      rec_desc_deep_fn<C, 8, 2>()},                                                     \
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
-   {rec_pair_fn<C, 1>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>(),            \
+   {rec_pair_fn<C, 1, false, 4>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>(),  \
     rec_pair_fn<C, 1, false, 1>(), rec_pair_fn<C, 1, false, 2>(),                   \
-    rec_pair_fn<C, 1, false, 3>(), rec_pair_fn<C, 1, false, 4>()},                  \
-   {rec_desc_pair_fn<C, 1>(), rec_desc_pair_fn<C, 2>(), rec_desc_pair_fn<C, 1, true>(), \
-    nullptr, nullptr, rec_desc_pair_fn<C, 1, false, 3>(),                           \
-    rec_desc_pair_fn<C, 1, false, 4>()}}
+    rec_pair_fn<C, 1, false, 3>(), rec_pair_fn<C, 1>()},                            \
+   {rec_desc_pair_fn<C, 1, false, 4>(), rec_desc_pair_fn<C, 2>(),                   \
+    rec_desc_pair_fn<C, 1, true>(), nullptr, nullptr,                               \
+    rec_desc_pair_fn<C, 1, false, 3>(), rec_desc_pair_fn<C, 1>()}}
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
@@ -634,7 +635,10 @@ int recon_depth(int mix) {
 
 // index into BsShape::rec_pair / rec_desc_pair: option 28 = 3 the prefetching
 // variant, 4 / 5 the timing splits (no Horner steps / no data networks; wrong
-// bytes, tools/tune.py only), 6 the compact mixing, 7 two inputs in flight
+// bytes, tools/tune.py only), 6 the compact mixing, 7 one input in flight.
+// (Two own inputs in flight per wave, the default since round 4: GF(2^16) 20+8
+// x 4 MiB at 8 lost 4.37 against 4.25 TB/s at 128 stripes, 4.45 against 4.38
+// at 256, reconstruct_batch 8 erasures 2.77 against 2.73; profiles/r04/s4/.)
 int pair_slot() {
   const int64_t o = get_option(28);
   return o >= 3 && o <= 7 ? (int)o - 1 : pair_groups() - 1;

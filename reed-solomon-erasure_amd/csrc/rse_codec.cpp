@@ -499,6 +499,20 @@ hipError_t lease_own_stream(Scratch* s, hipStream_t* out) {
   return hipSuccess;
 }
 
+// A kept device ring of at least dbytes, if that is at most kPipeRingKeep
+// (otherwise the ring stays as it is and the caller allocates its own).
+hipError_t lease_ring(Scratch* r, size_t dbytes) {
+  if (r->dbytes < dbytes && dbytes <= kPipeRingKeep) {
+    if (r->dbuf) (void)hipFree(r->dbuf);  // idle: the previous call synchronised
+    r->dbuf = nullptr;
+    r->dbytes = 0;
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&r->dbuf), dbytes);
+    if (e != hipSuccess) return e;
+    r->dbytes = dbytes;
+  }
+  return hipSuccess;
+}
+
 // The host pipeline's streams and events for (nh, ring), and a kept ring of
 // dbytes if that is at most kPipeRingKeep.
 hipError_t lease_pipe(Scratch* r, int nh, int ring, size_t dbytes) {
@@ -527,15 +541,7 @@ hipError_t lease_pipe(Scratch* r, int nh, int ring, size_t dbytes) {
     e = hipEventCreateWithFlags(&r->start, hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
-  if (r->dbytes < dbytes && dbytes <= kPipeRingKeep) {
-    if (r->dbuf) (void)hipFree(r->dbuf);  // idle: the previous call synchronised
-    r->dbuf = nullptr;
-    r->dbytes = 0;
-    e = hipMalloc(reinterpret_cast<void**>(&r->dbuf), dbytes);
-    if (e != hipSuccess) return e;
-    r->dbytes = dbytes;
-  }
-  return hipSuccess;
+  return lease_ring(r, dbytes);
 }
 
 // Runs `j` in a check mode and returns the verdict (synchronises the stream):
@@ -1215,10 +1221,107 @@ struct HostCode {
   bool any_mem = false;
 };
 
+// Small calls: one stripe moving at most kHostDirectBytes (both ways) skips
+// the pipeline.  Its per-shard copies cost ~10 us of runtime work each for
+// pageable memory (the runtime stages every one), ~170 us for a 10+4 stripe
+// of 1 KiB shards (profiles/r04/s4/bench.log, crossover_10_4), far more than
+// the bytes.  Here the CPU copies the shards the operation reads into the
+// lease's pinned words, one DMA takes them up, the operation runs on the
+// caller's stream, one DMA brings the shards it writes back, and the CPU
+// copies them out.
+constexpr size_t kHostDirectBytes = size_t(2) << 20;
+
+int host_direct(const rse_codec* c, HostOp op, const HostStripe& hs, size_t bytes, hipStream_t user,
+                int* ok, const HostCode* code, bool* handled) {
+  *handled = false;
+  const bool low = op == HostOp::kCode;
+  if (low && code->any_mem) return RSE_OK;  // device memory among the buffers: the pipeline
+  const bool verify = op == HostOp::kVerify || op == HostOp::kVerifyBuf;
+  const int field = low ? code->field : c->field;
+  const size_t k = low ? code->rows->n_in : c->k;
+  const size_t T = low ? k + code->rows->n_out : c->total;
+  const size_t p = T - k, es = field == RSE_FIELD_GF16 ? 2 : 1;
+  const size_t nbuf = T + (op == HostOp::kVerifyBuf ? p : 0);
+  std::vector<uint32_t> up, down;
+  host_sets((uint32_t)k, (uint32_t)T, (uint32_t)p, op, low && code->accumulate, hs.present, up,
+            down);
+  if ((up.size() + down.size()) * bytes > kHostDirectBytes) return RSE_OK;
+  *handled = true;
+  if (down.empty() && !verify) return RSE_OK;  // nothing to rebuild
+  // device: shard i at dbuf + i * sz (sz: bytes rounded up to 16), then the verdict word
+  const size_t sz = (bytes + 15) & ~size_t(15), words = (nbuf * sz) / 4 + 1;
+  Lease res;
+  hipError_t e = res.acquire();
+  if (e == hipSuccess) e = lease_words(res.get(), words);
+  if (e == hipSuccess) e = lease_ring(res.get(), nbuf * sz + 256);
+  if (e == hipSuccess && res->dbytes < nbuf * sz + 256) e = hipErrorOutOfMemory;
+  if (e != hipSuccess) return dev_fail(e);
+  uint8_t* dbuf = res->dbuf;
+  uint8_t* hst = reinterpret_cast<uint8_t*>(res->wh);
+  uint32_t* dword = reinterpret_cast<uint32_t*>(dbuf + nbuf * sz);
+  auto host = [&](uint32_t i) { return static_cast<uint8_t*>(i < T ? hs.sh[i] : hs.buf[i - T]); };
+  for (uint32_t i : up) std::memcpy(hst + (size_t)i * sz, host(i), bytes);
+  // one DMA up over the span of the shards read, one down over those written
+  const size_t u0 = up.empty() ? 0 : up.front(), u1 = up.empty() ? 0 : up.back() + 1;
+  if (u1 > u0)
+    e = hipMemcpyAsync(dbuf + u0 * sz, hst + u0 * sz, (u1 - u0) * sz, hipMemcpyHostToDevice, user);
+  if (e == hipSuccess && verify) e = hipMemsetAsync(dword, 0, 4, user);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(user);
+    return dev_fail(e);
+  }
+  std::vector<uint8_t*> dev(nbuf);
+  for (size_t i = 0; i < nbuf; ++i) dev[i] = dbuf + i * sz;
+  const Rows rows = low ? Rows{} : parity_rows(c);
+  const Rows& code_rows = low ? *code->rows : rows;
+  std::vector<size_t> lens(T, bytes / es);
+  int rc = RSE_OK;
+  switch (op) {
+    case HostOp::kEncode:
+    case HostOp::kCode: {
+      Job j{field, &code_rows, dev.data(), dev.data() + k, nullptr, bytes, rse::kStore,
+            low && code->accumulate, nullptr, 0, 1};
+      rc = run_job(j, user);
+      break;
+    }
+    case HostOp::kVerify:
+    case HostOp::kVerifyBuf: {
+      const bool wb = op == HostOp::kVerifyBuf;
+      Job j{field, &rows, dev.data(), wb ? dev.data() + T : nullptr, dev.data() + k, bytes,
+            wb ? rse::kCheckStore : rse::kCheck, false, dword, 0, 1};
+      rc = run_job(j, user);
+      break;
+    }
+    case HostOp::kRecon:
+    case HostOp::kReconData:
+      rc = reconstruct_impl(c, reinterpret_cast<void* const*>(dev.data()), lens.data(), hs.present,
+                            T, op == HostOp::kReconData, user);
+      break;
+  }
+  const size_t d0 = down.empty() ? 0 : down.front(), d1 = down.empty() ? 0 : down.back() + 1;
+  if (rc == RSE_OK && d1 > d0)
+    e = hipMemcpyAsync(hst + d0 * sz, dbuf + d0 * sz, (d1 - d0) * sz, hipMemcpyDeviceToHost, user);
+  uint32_t* hword = res->wh + (words - 1);
+  if (rc == RSE_OK && e == hipSuccess && verify)
+    e = hipMemcpyAsync(hword, dword, 4, hipMemcpyDeviceToHost, user);
+  const hipError_t e2 = hipStreamSynchronize(user);
+  if (rc) return rc;
+  if (e != hipSuccess) return dev_fail(e);
+  if (e2 != hipSuccess) return dev_fail(e2);
+  for (uint32_t i : down) std::memcpy(host(i), hst + (size_t)i * sz, bytes);
+  if (verify && ok) ok[0] = *reinterpret_cast<volatile uint32_t*>(hword) == 0 ? 1 : 0;
+  return RSE_OK;
+}
+
 // Runs `op` over `bytes` of every shard of every stripe (codec ops: `c`;
 // kCode: `code`).  verify ops: ok[s] receives stripe s's verdict.
 int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& stripes,
                   size_t bytes, hipStream_t user, int* ok, const HostCode* code = nullptr) {
+  if (stripes.size() == 1 && rse::get_option(RSE_OPT_HOST_DIRECT)) {
+    bool handled = false;
+    const int rc = host_direct(c, op, stripes[0], bytes, user, ok, code, &handled);
+    if (handled || rc) return rc;
+  }
   const int64_t chunk_kib = rse::get_option(RSE_OPT_HOST_CHUNK_KIB);
   const int nh = (int)std::max<int64_t>(1, std::min<int64_t>(4, rse::get_option(RSE_OPT_HOST_H2D_STREAMS)));
   const int ring = std::max(3, nh + 2);  // slots: nh filling, one coding, one draining

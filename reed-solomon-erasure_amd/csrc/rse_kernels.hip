@@ -791,6 +791,7 @@ struct Options {
   int64_t wide_pairs = 1;         // wide GF(2^8) modules: networks over pairs of inputs
   int64_t sync_event = 0;         // verify calls wait on an event, not the stream (A/B)
   int64_t spin_wait = 1;          // one-launch verifies: poll the completion word (A/B)
+  int64_t host_direct = 1;        // small one-stripe host calls: one staging buffer (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1280,6 +1281,7 @@ int set_option(int key, int64_t value) {
     case 29: g_opt.wide_pairs = value ? 1 : 0; return 0;
     case 30: g_opt.sync_event = value ? 1 : 0; return 0;
     case 31: g_opt.spin_wait = value ? 1 : 0; return 0;
+    case 32: g_opt.host_direct = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1323,6 +1325,7 @@ int64_t get_option(int key) {
     case 29: return g_opt.wide_pairs;
     case 30: return g_opt.sync_event;
     case 31: return g_opt.spin_wait;
+    case 32: return g_opt.host_direct;
     default: return -1;
   }
 }

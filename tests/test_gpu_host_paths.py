@@ -673,3 +673,39 @@ def test_reconstruct_batch_shared_pattern_runs(R, field, k, p, lost):
             assert (d.cpu().numpy().reshape(stripes, T, -1) == flat).all()
     finally:
         lib.rse_set_option(9, old)
+
+
+@pytest.mark.parametrize("direct", [1, 0])
+@pytest.mark.parametrize("field,k,p,n", [(8, 10, 4, 4096 + 7), (16, 20, 8, 1000), (8, 4, 4, 1)])
+def test_host_direct_and_pipeline_agree(R, field, k, p, n, direct):
+    """RSE_OPT_HOST_DIRECT: a one-stripe host call moving at most 2 MiB takes
+    one pinned staging buffer (one DMA each way) instead of the pipeline's
+    per-shard copies.  Both give the oracle's bytes for encode, verify (and a
+    corrupted shard), verify_with_buffer and reconstruct, on pageable and
+    pinned shards."""
+    lib = R._lib.load()
+    old = lib.rse_get_option(32)
+    lib.rse_set_option(32, direct)
+    try:
+        rng = np.random.default_rng(7000 + n + k)
+        oc, full = oracle_full(field, k, p, n, rng)
+        r = R.core.ReedSolomon(k, p, field)
+        T = k + p
+        for pin in (False, True):
+            hs = [as_host(x if i < k else np.full_like(x, 0xEE), pin) for i, x in enumerate(full)]
+            r.encode_host(hs)
+            assert all((as_np(hs[i]) == full[i]).all() for i in range(T))
+            assert r.verify_host(hs)
+            buf = [as_host(np.zeros_like(full[0]), pin) for _ in range(p)]
+            assert r.verify_with_buffer_host(hs, buf)
+            assert all((as_np(b) == full[k + i]).all() for i, b in enumerate(buf))
+            x = as_np(hs[k - 1])
+            x[-1] ^= 0x11
+            assert not r.verify_host(hs)
+            x[-1] ^= 0x11
+            erased = sorted(rng.choice(T, p, replace=False).tolist())
+            shards = [as_host(full[i], pin) if i not in erased else None for i in range(T)]
+            r.reconstruct_host(shards)
+            assert all((as_np(shards[i]) == full[i]).all() for i in range(T)), erased
+    finally:
+        lib.rse_set_option(32, old)
