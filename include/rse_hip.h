@@ -169,8 +169,11 @@ int rse_reconstruct_data_flat(const rse_codec *codec, void *stripes, size_t shar
  * syndrome inverse) and coded by the bit-sliced syndrome kernel; the rest of
  * every shard, and other GF(2^8) codecs with k <= 32 and p <= 16, use the
  * device planner with k x k inverses and the table kernels; anything else
- * falls back to the host planner stripe by stripe (same results).  Returns
- * after the work is queued and the host inputs have been consumed. */
+ * falls back to the host planner stripe by stripe (same results).  `present`
+ * may be host memory or device memory of the stripes' device (flags a GPU
+ * scrub produced: they are then read in place, never copied, and the
+ * shared-pattern detection -- a host pass -- is skipped).  Returns after the
+ * work is queued and the host inputs have been consumed. */
 int rse_reconstruct_batch(const rse_codec *codec, void *stripes, size_t shard_len,
                           size_t n_stripes, const uint8_t *present, int data_only,
                           rse_stream_t stream);

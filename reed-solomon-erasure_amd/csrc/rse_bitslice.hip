@@ -246,16 +246,28 @@ struct GfDev {
 };
 
 constexpr int kPlanBlock = 64;
+constexpr uint32_t kPlanLanes = 8;  // lanes that plan one stripe together
+constexpr uint32_t kPlanStripes = kPlanBlock / kPlanLanes;  // stripes per workgroup
 
-// One lane per stripe.  The index sets are bit masks (S: missing data, R:
-// syndrome rows, M: missing parity) and the [A | I] Gauss-Jordan workspace
-// lives in LDS, lane-interleaved (element (t, x) of lane l at
-// gj[(t * 2E + x) * kPlanBlock + l], E = e_cap: conflict-free), so nothing
-// goes to scratch memory (the round-3 planner kept them in 1.2 KB of private
-// memory per lane).  Only the fields the Horner syndrome kernels read are
-// written: data / par / out pointers, out_sigma, the masks, n_out and hm
-// (the weights go straight into the Horner masks; w is never stored).  The
-// GF(2^8) log / exp tables come from `tabs` (256 + 512 bytes, host-built).
+// The i-th set bit of m (i < popcount(m)).
+__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t i) {
+  for (; i; --i) m &= m - 1u;
+  return (uint32_t)__builtin_ctz(m);
+}
+
+// kPlanLanes lanes per stripe (a group), kPlanStripes stripes per 64-lane
+// workgroup.  Every lane of a group derives the stripe's index sets from its
+// flags (bit masks: S missing data, R syndrome rows, M missing parity); the
+// group then shares the work: the columns of the [A | I] Gauss-Jordan
+// (A = P[R][S], in LDS, one e_cap x 2 e_cap block per stripe), the outputs'
+// Horner masks, and the descriptor's pointer arrays.  Lanes of a group are
+// lanes of one wave, so LDS reads and writes of the group happen in program
+// order: a row's factor is read by every lane before the lane owning that
+// column clears it.  Round 3's planner (one lane per stripe, its workspace in
+// scratch memory) took 223-236 us for 65536 stripes, the first round-4 one
+// (one lane per stripe, LDS) 86-93 us.  Only the fields the Horner syndrome
+// kernels read are written (data / par / out pointers, out_sigma, the masks,
+// n_out, hm); the GF(2^8) log / exp tables come from `tabs` (host-built).
 __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
     int field, const uint16_t* __restrict__ rows, const uint8_t* __restrict__ tabs,
     const uint8_t* __restrict__ present, uint32_t k, uint32_t p, uint32_t data_only, uint8_t* base,
@@ -265,22 +277,24 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
   for (uint32_t i = threadIdx.x; i < (256 + 512) / 4; i += kPlanBlock)
     tl[i] = reinterpret_cast<const uint32_t*>(tabs)[i];
   __syncthreads();
-  const uint32_t s = blockIdx.x * kPlanBlock + threadIdx.x;
+  const uint32_t grp = threadIdx.x / kPlanLanes, gl = threadIdx.x % kPlanLanes;
+  const uint32_t s = blockIdx.x * kPlanStripes + grp;
   if (s >= n_stripes) return;
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(tl);
   const GfDev gf{lg, lg + 256, field};
-  const uint32_t total = k + p, E2 = 2 * e_cap, l = threadIdx.x;
-  auto G = [&](uint32_t t, uint32_t x) -> uint16_t& { return gj[(t * E2 + x) * kPlanBlock + l]; };
+  const uint32_t total = k + p, E2 = 2 * e_cap;
+  uint16_t* gm = gj + grp * e_cap * E2;
+  auto G = [&](uint32_t t, uint32_t x) -> uint16_t& { return gm[t * E2 + x]; };
   const uint8_t* pr = present + (uint64_t)s * total;
   uint8_t* sb = base + (uint64_t)s * total * shard_bytes;
   BsReconArgs& d = descs[s];
   uint32_t pmask = 0, smask = 0, rmask = 0, mmask = 0, nr = 0;
   for (uint32_t j = 0; j < k; ++j) {
-    const bool here = pr[j] != 0;
-    d.data[j] = here ? sb + (uint64_t)j * shard_bytes : nullptr;
-    if (here) pmask |= 1u << j;
+    if (pr[j]) pmask |= 1u << j;
     else smask |= 1u << j;
   }
+  for (uint32_t j = gl; j < k; j += kPlanLanes)
+    d.data[j] = ((pmask >> j) & 1u) ? sb + (uint64_t)j * shard_bytes : nullptr;
   const uint32_t ne = (uint32_t)__builtin_popcount(smask);
   for (uint32_t r = 0; r < p; ++r) {
     if (pr[k + r]) {
@@ -292,77 +306,76 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
       mmask |= 1u << r;
     }
   }
-  const uint32_t nm = (uint32_t)__builtin_popcount(mmask);
-  d.stripe_stride = 0;
-  d.n_stripes = 1;
-  d.present = pmask;
-  d.sigma = d.synd = 0;
-  d.n_out = 0;  // nothing to do unless completed below
-  if (nr != ne || ne > e_cap || ne + nm == 0 || ne + nm > (uint32_t)kMaxOut) return;
-  // [A | I], A = P[R][S]
-  for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
-    const uint32_t r = (uint32_t)__builtin_ctz(rr);
-    for (uint32_t u = 0, ss = smask; u < ne; ++u, ss &= ss - 1u) {
-      G(t, u) = rows[r * k + (uint32_t)__builtin_ctz(ss)];
-      G(t, ne + u) = t == u ? 1 : 0;
-    }
+  const uint32_t nm = (uint32_t)__builtin_popcount(mmask), n_out = ne + nm;
+  const bool ok = nr == ne && ne <= e_cap && n_out > 0 && n_out <= (uint32_t)kMaxOut;
+  if (gl == 0) {
+    d.stripe_stride = 0;
+    d.n_stripes = 1;
+    d.present = pmask;
+    d.sigma = d.synd = 0;
+    d.n_out = 0;  // nothing to do unless completed below
   }
+  if (!ok) return;
+  // [A | I], A = P[R][S]: the group fills it element by element
+  for (uint32_t i = gl; i < ne * 2 * ne; i += kPlanLanes) {
+    const uint32_t t = i / (2 * ne), x = i % (2 * ne);
+    G(t, x) = x < ne ? rows[nth_bit(rmask, t) * k + nth_bit(smask, x)] : (x - ne == t ? 1 : 0);
+  }
+  // Gauss-Jordan: lane gl owns columns x = gl, gl + kPlanLanes, ... of row
+  // operations; the pivot row is found by every lane (same reads, same answer)
   for (uint32_t col = 0; col < ne; ++col) {
     uint32_t piv = col;
     while (piv < ne && G(piv, col) == 0) ++piv;
-    if (piv == ne) return;  // singular: impossible for this code; stripe untouched
+    if (piv == ne) return;  // singular: impossible for this code; stripe left at n_out = 0
     if (piv != col)
-      for (uint32_t x = 0; x < 2 * ne; ++x) {
+      for (uint32_t x = gl; x < 2 * ne; x += kPlanLanes) {
         const uint16_t t0 = G(col, x);
         G(col, x) = G(piv, x);
         G(piv, x) = t0;
       }
     const uint32_t sc = gf.inv(G(col, col));
-    for (uint32_t x = 0; x < 2 * ne; ++x) G(col, x) = (uint16_t)gf.mul(sc, G(col, x));
+    for (uint32_t x = col + gl; x < 2 * ne; x += kPlanLanes) G(col, x) = (uint16_t)gf.mul(sc, G(col, x));
     for (uint32_t r = 0; r < ne; ++r) {
-      const uint32_t f = G(r, col);
+      const uint32_t f = G(r, col);  // read by every lane before any lane writes row r
       if (r == col || !f) continue;
-      for (uint32_t x = col; x < 2 * ne; ++x) G(r, x) ^= (uint16_t)gf.mul(f, G(col, x));
+      for (uint32_t x = col + gl; x < 2 * ne; x += kPlanLanes)
+        G(r, x) ^= (uint16_t)gf.mul(f, G(col, x));
     }
   }
-  // outputs: missing data S_u = sum_t Ainv[u][t] s_t; missing parity r =
-  // sigma_r ^ sum_t (P[r][S] Ainv)[t] s_t.  Weight (o, t) goes into the
-  // Horner mask bits of syndrome row R_t (rse_kernels.hpp set_horner_masks).
+  // outputs, lane gl the outputs o = gl, gl + kPlanLanes, ...: missing data
+  // S_u = sum_t Ainv[u][t] s_t; missing parity r = sigma_r ^ sum_t (P[r][S]
+  // Ainv)[t] s_t.  Weight (o, t) sets the Horner mask bits of syndrome row R_t
+  // (rse_kernels.hpp set_horner_masks).
   const int nb = field == 8 ? 8 : 16;
-  uint32_t o = 0;
-  for (uint32_t u = 0, ss = smask; u < ne; ++u, ++o, ss &= ss - 1u) {
-    d.out[o] = sb + (uint64_t)__builtin_ctz(ss) * shard_bytes;
-    d.out_sigma[o] = -1;
-    uint32_t hm[4] = {0u, 0u, 0u, 0u};
-    for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
-      const uint32_t co = horner_coords(field, G(u, ne + t)), r = (uint32_t)__builtin_ctz(rr);
-      for (int j = 0; j < nb; ++j)
-        if ((co >> (nb - 1 - j)) & 1u) hm[j >> 2] |= 1u << (8 * (j & 3) + r);
-    }
-    for (int q = 0; q < 4; ++q) d.hm[o][q] = hm[q];
-  }
-  for (uint32_t mm = mmask; mm; mm &= mm - 1u, ++o) {
-    const uint32_t r = (uint32_t)__builtin_ctz(mm);
-    d.out[o] = sb + (uint64_t)(k + r) * shard_bytes;
-    d.out_sigma[o] = (int32_t)r;
+  for (uint32_t o = gl; o < n_out; o += kPlanLanes) {
+    const bool dat = o < ne;
+    const uint32_t r = dat ? 0u : nth_bit(mmask, o - ne);
+    d.out[o] = sb + (uint64_t)(dat ? nth_bit(smask, o) : k + r) * shard_bytes;
+    d.out_sigma[o] = dat ? -1 : (int32_t)r;
     uint32_t hm[4] = {0u, 0u, 0u, 0u};
     for (uint32_t t = 0, rr = rmask; t < ne; ++t, rr &= rr - 1u) {
       uint32_t v = 0;
-      for (uint32_t u = 0, ss = smask; u < ne; ++u, ss &= ss - 1u)
-        v ^= gf.mul(rows[r * k + (uint32_t)__builtin_ctz(ss)], G(u, ne + t));
+      if (dat) {
+        v = G(o, ne + t);
+      } else {
+        for (uint32_t u = 0, ss = smask; u < ne; ++u, ss &= ss - 1u)
+          v ^= gf.mul(rows[r * k + (uint32_t)__builtin_ctz(ss)], G(u, ne + t));
+      }
       const uint32_t co = horner_coords(field, v), rt = (uint32_t)__builtin_ctz(rr);
       for (int j = 0; j < nb; ++j)
         if ((co >> (nb - 1 - j)) & 1u) hm[j >> 2] |= 1u << (8 * (j & 3) + rt);
     }
     for (int q = 0; q < 4; ++q) d.hm[o][q] = hm[q];
   }
-  for (uint32_t rr = rmask; rr; rr &= rr - 1u) {
-    const uint32_t r = (uint32_t)__builtin_ctz(rr);
+  for (uint32_t t = gl; t < ne; t += kPlanLanes) {
+    const uint32_t r = nth_bit(rmask, t);
     d.par[r] = sb + (uint64_t)(k + r) * shard_bytes;
   }
-  d.synd = rmask;
-  d.sigma = rmask | mmask;
-  d.n_out = o;
+  if (gl == 0) {
+    d.synd = rmask;
+    d.sigma = rmask | mmask;
+    d.n_out = n_out;
+  }
 }
 
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
@@ -767,9 +780,9 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       }
     if (!jfn) return hipSuccess;
   }
-  // the planner's Gauss-Jordan workspace: e_cap x 2 e_cap halfwords per lane
-  const size_t gj_lds = (size_t)e_cap * 2u * e_cap * kPlanBlock * sizeof(uint16_t);
-  hipLaunchKernelGGL(bs_recon_plan_kernel, dim3((n_stripes + kPlanBlock - 1) / kPlanBlock),
+  // the planner's Gauss-Jordan workspace: e_cap x 2 e_cap halfwords per stripe
+  const size_t gj_lds = (size_t)e_cap * 2u * e_cap * kPlanStripes * sizeof(uint16_t);
+  hipLaunchKernelGGL(bs_recon_plan_kernel, dim3((n_stripes + kPlanStripes - 1) / kPlanStripes),
                      dim3(kPlanBlock), gj_lds, stream, field, d_rows, d_tabs, d_present, k, p,
                      data_only, base, shard_bytes, n_stripes, e_cap, d_descs);
   hipError_t e = hipGetLastError();

@@ -1828,13 +1828,29 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   const size_t k = c->k, p = c->p, T = c->total, sb = shard_len * c->esize();
   uint8_t* base = static_cast<uint8_t*>(stripes);
   hipStream_t st = (hipStream_t)stream;
+  // The flags may live in device memory (a scrubber that found the damage on
+  // the GPU): then they are never copied; the scan and the planners read them
+  // where they are, and the shared-pattern detection below (a host pass) is
+  // skipped.  Paths that need them on the host copy them there.
+  int fdev = -1;
+  const bool dev_flags = device_memory(present, &fdev);
+  std::vector<uint8_t> hflags;  // host copy of device flags, made on demand
+  auto host_flags = [&](size_t n) -> const uint8_t* {
+    if (!dev_flags) return present;
+    if (hflags.size() < n * T) {
+      hflags.resize(n * T);
+      if (hipMemcpy(hflags.data(), present, n * T, hipMemcpyDeviceToHost) != hipSuccess)
+        return nullptr;
+    }
+    return hflags.data();
+  };
   // Runs of consecutive stripes with one erasure pattern (a lost disk: every
   // stripe misses the same shards) go through the shared-pattern path: one
   // plan per run, and the pattern's own kernel once it has one (core.rs:
   // 697-731 caches the pattern; used twice, it is specialised), instead of a
   // plan and a mixing per stripe.  Used when the runs are long (at most one
   // run per 16 stripes on average).  Every run is validated before any runs.
-  {
+  if (!dev_flags) {
     std::vector<std::pair<size_t, size_t>> runs;  // [first, count)
     for (size_t s0 = 0; s0 < n_stripes;) {
       size_t s1 = s0 + 1;
@@ -1889,9 +1905,11 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   };
   if (shard_len == 0) {  // stripe 0 fails: EmptyShard, or TooFewShardsPresent (none present)
     uint32_t nd, ne, no;
-    return batch_stripe(present, k, p, data_only != 0, shard_len, &nd, &ne, &no);
+    const uint8_t* f0 = host_flags(1);
+    if (!f0) return dev_fail(hipGetLastError());
+    return batch_stripe(f0, k, p, data_only != 0, shard_len, &nd, &ne, &no);
   }
-  const bool dev_scan = n_stripes >= kDeviceScanStripes;
+  const bool dev_scan = dev_flags || n_stripes >= kDeviceScanStripes;
   if (!dev_scan) {
     for (size_t s = 0; s < n_stripes; ++s) {
       uint32_t nd, ne, no;
@@ -1908,6 +1926,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   RSE_HIP(lease_plan(lease.get(),
                      desc_off + (bs_path ? n_stripes * sizeof(rse::BsReconArgs) : 0), st,
                      &dflags, &ws_owned));
+  const uint8_t* dfl = dev_flags ? present : dflags;  // the flags the device reads
   if (!dev_scan) {
     hipError_t e = hipMemcpyAsync(dflags, present, n_stripes * T, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return dev_fail(release(e));
@@ -1917,10 +1936,10 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     // the first words
     // (pinned words only up to 16 MiB of flags: a lease keeps its words, and
     // the pool keeps up to kIdleScratch leases)
-    const bool staged = n_stripes * T <= (size_t(16) << 20);
+    const bool staged = !dev_flags && n_stripes * T <= (size_t(16) << 20);
     hipError_t e = lease_words(lease.get(), 8 + (staged ? (n_stripes * T + 3) / 4 : 0));
     uint32_t* res = reinterpret_cast<uint32_t*>(dflags + fl_bytes);
-    if (e == hipSuccess) {
+    if (e == hipSuccess && !dev_flags) {
       if (staged) std::memcpy(lease->wh + 8, present, n_stripes * T);
       e = hipMemcpyAsync(dflags, staged ? static_cast<const void*>(lease->wh + 8) : present,
                          n_stripes * T, hipMemcpyHostToDevice, st);
@@ -1928,7 +1947,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     if (e == hipSuccess) e = hipMemsetAsync(res, 0, 4 * sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(res + 4, 0xFF, 2 * sizeof(uint32_t), st);
     if (e == hipSuccess)
-      e = rse::launch_batch_scan(dflags, n_stripes, (uint32_t)k, (uint32_t)p, data_only ? 1u : 0u,
+      e = rse::launch_batch_scan(dfl, n_stripes, (uint32_t)k, (uint32_t)p, data_only ? 1u : 0u,
                                  res, st);
     if (e == hipSuccess)
       e = hipMemcpyAsync(lease->wh, res, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
@@ -1970,7 +1989,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       uint64_t bs_done = 0;
       e = rse::launch_bitslice_recon_batch(
           c->field, (uint32_t)k, (uint32_t)p, rows.c.data(),
-          reinterpret_cast<const uint16_t*>(consts), consts + plan_tab_off(c), dflags,
+          reinterpret_cast<const uint16_t*>(consts), consts + plan_tab_off(c), dfl,
           data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need, e_cap,
           reinterpret_cast<rse::BsReconArgs*>(ws), st, &bs_done);
       if (e == hipSuccess && bs_done == sb) {
@@ -1996,11 +2015,16 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       rse::recon_plan_lds((uint32_t)k, (uint32_t)T, e_cap, nout_cap) > rse::kReconPlanLdsMax) {
     // past the device planner's LDS budget: the host planner, stripe by stripe
     (void)release(hipSuccess);
+    const uint8_t* hfl = host_flags(n_stripes);
+    if (!hfl) {
+      (void)hipStreamSynchronize(st);
+      return dev_fail(hipGetLastError());
+    }
     std::vector<void*> ptrs(T);
     std::vector<size_t> lens(T, (sb - done) / c->esize());
     for (size_t s = 0; s < n_stripes; ++s) {
       for (size_t i = 0; i < T; ++i) ptrs[i] = base + (s * T + i) * sb + done;
-      int rc = reconstruct_impl(c, ptrs.data(), lens.data(), present + s * T, T, data_only != 0, st);
+      int rc = reconstruct_impl(c, ptrs.data(), lens.data(), hfl + s * T, T, data_only != 0, st);
       if (rc) {
         (void)hipStreamSynchronize(st);  // step 1's copies read `prow`
         return rc;
@@ -2026,7 +2050,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   hipError_t e = hipSuccess;
   for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {
     const size_t ng = std::min(grp, n_stripes - g0);
-    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(consts), dflags + g0 * T,
+    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(consts), dfl + g0 * T,
                                (uint32_t)k, (uint32_t)T, data_only ? 1u : 0u, e_cap, nout_cap,
                                base + g0 * T * sb, sb, done, sb - done, (uint32_t)ng,
                                reinterpret_cast<CodeArgs*>(ws), st);

@@ -312,8 +312,19 @@ class ReedSolomon:
                           present, data_only: bool = False) -> None:
         """reconstruct (or reconstruct_data) of `n_stripes` flat stripes, each
         with its OWN erasure pattern: `present` is n_stripes x (k+p) flags.
-        Per-stripe planning (core.rs:733-923) runs as a HIP kernel."""
+        Per-stripe planning (core.rs:733-923) runs as a HIP kernel.  A
+        contiguous bool / uint8 device tensor of flags is read in place."""
         T = self.total_shard_count()
+        if isinstance(present, torch.Tensor) and present.is_cuda:
+            if (tuple(present.shape) != (n_stripes, T) or not present.is_contiguous()
+                    or present.dtype not in (torch.bool, torch.uint8)):
+                raise RSError(Error.InvalidShardFlags)
+            _check_flat(stripes, shard_len, n_stripes, T, self.field)
+            _raise(_lib.rse_reconstruct_batch(
+                self._h, _dev(stripes), shard_len, n_stripes,
+                ctypes.cast(present.data_ptr(), ctypes.POINTER(ctypes.c_uint8)),
+                1 if data_only else 0, _stream(stripes)))
+            return
         flags = np.ascontiguousarray(np.asarray(
             present.cpu() if isinstance(present, torch.Tensor) else present, dtype=bool))
         if flags.shape != (n_stripes, T):

@@ -521,7 +521,8 @@ def test_flat_small_shards_many_stripes(R, field, k, p, n, stripes):
     (8, 12, 4, 2 * 16384, 7, 1, 0),        # run-time specialised codec
     (16, 6, 3, 8192 * 3, 4, 1, 0),         # run-time specialised GF(2^16) codec
 ])
-def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, hp):
+@pytest.mark.parametrize("dflags", [False, True])
+def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, hp, dflags):
     """rse_reconstruct_batch: every stripe with its own erasure pattern, against
     the oracle's reconstruct of each stripe (core.rs:680/690 semantics).  bs:
     the whole 16 KiB chunks run on the bit-sliced syndrome kernels from
@@ -529,7 +530,8 @@ def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, h
     rest on the table kernels from descriptors the device planner writes
     (either field, any k and p).  hp: stripes planned on the host per call
     (RSE_OPT_HOST_PLANNED_STRIPES) -- none unless the batch is past the
-    device planner's LDS budget."""
+    device planner's LDS budget.  dflags: the flags handed over in device
+    memory (read in place: the device scan, no copy)."""
     rng = np.random.default_rng(field * 1000 + k * 31 + p)
     lib = R._lib.load()
     old_jit = lib.rse_get_option(9)
@@ -563,7 +565,8 @@ def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, h
         d = dev(buf)
         n0 = lib.rse_get_option(6)
         h0 = lib.rse_get_option(25)
-        r.reconstruct_batch(d, n, stripes, present, data_only=data_only)
+        flags = torch.from_numpy(present).cuda() if dflags else present
+        r.reconstruct_batch(d, n, stripes, flags, data_only=data_only)
         got = host(d).reshape(stripes, T, n * es)
         assert lib.rse_get_option(6) - n0 == bs, data_only
         rebuilds = (~present[:, :k]).any() if data_only else (~present).any()

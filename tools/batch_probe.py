@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--erasures", type=int, default=4)
     ap.add_argument("--calls", type=int, default=20)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--device-flags", action="store_true", help="flags in HBM (read in place)")
     a = ap.parse_args()
     lib = R._lib.load()
     for kv in a.set:
@@ -46,6 +47,8 @@ def main():
     for s in range(S):
         pres[s, rng.choice(T, a.erasures, replace=False)] = False
     miss = (~pres[:, :k]).sum(axis=1)
+    if a.device_flags:
+        pres = torch.from_numpy(pres).cuda()
     nbytes = int((miss > 0).sum() * k + miss.sum()) * L
     r.reconstruct_batch(buf, elems, S, pres, data_only=True)
     torch.cuda.synchronize()
@@ -61,7 +64,8 @@ def main():
         wall.append(time.perf_counter() - t0)
         gpu.append(ev[0].elapsed_time(ev[1]) * 1e-3)
     print(f"reconstruct_batch GF(2^{a.field}) {k}+{p} x {a.shard_kib} KiB x {S}, "
-          f"{a.erasures} erasures per stripe, {nbytes / 1e9:.2f} GB per call")
+          f"{a.erasures} erasures per stripe, {nbytes / 1e9:.2f} GB per call, flags in "
+          f"{'HBM' if a.device_flags else 'host memory'}")
     for w, g in zip(wall, gpu):
         print(f"  wall {w * 1e3:7.3f} ms ({nbytes / w / 1e9:7.1f} GB/s)   events "
               f"{g * 1e3:7.3f} ms ({nbytes / g / 1e9:7.1f} GB/s)")
