@@ -32,6 +32,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-erasure_amd"))
 sys.path.insert(0, ROOT)
+# run-time specialised kernels (rse_jit.cpp): the code objects prebuilt on the
+# host into the tree's cache (tools/prebuild_all.sh) load in milliseconds; a
+# module whose source differs is rebuilt (the key hashes the whole source)
+os.environ.setdefault("RSE_JIT_CACHE_DIR", os.path.join(ROOT, "jitcache"))
 
 METRIC = "device-resident encode MB/s (data+parity), 10+4 × 16 MiB shards, 1/2/4/8 GPU"
 MiB = 1 << 20
@@ -885,8 +889,24 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
     out = {"what": "benches/bandwidth.rs:88-190 shapes; data_MB_per_s counts k x block per "
                    "call as criterion does; *_call_us are per synchronous call (python ctypes "
                    "loop, ~1 us of call overhead included); cpu_reference = simd_c -O3 "
-                   "-march=haswell in core.rs loop order, 1 thread, decode rows cached",
+                   "-march=haswell in core.rs loop order, 1 thread, decode rows cached; "
+                   "run-time kernel builds waited for (RSE_OPT_JIT 2): steady state, as the "
+                   "reference's repeated calls with their decode rows cached",
            "entries": []}
+    jit_old = lib.rse_get_option(9)
+    lib.rse_set_option(9, 2)
+    try:
+        _matrix_rows(lib, stream, st, sh, out, one_stripe_fn(), shapes)
+    finally:
+        lib.rse_set_option(9, jit_old)
+    out["crossover_10_4"] = (per_call_crossover(stream, crossover_sizes) if crossover_sizes
+                             else per_call_crossover(stream))
+    return out
+
+
+def one_stripe_fn():
+    import ctypes
+    import numpy as np
 
     def one_stripe(k, p, block, src):
         T = k + p
@@ -895,12 +915,22 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
         host = [np.ascontiguousarray(src[i].cpu().numpy()) for i in range(T)]
         hptrs = (ctypes.c_void_p * T)(*[h.ctypes.data for h in host])
         return ptrs, lens, hptrs, host  # `host` owns the memory hptrs points to
+    return one_stripe
 
+
+def _matrix_rows(lib, stream, st, sh, out, one_stripe, shapes):
+    """reference_bench_matrix's rows, one per (shape, op)."""
+    import ctypes
+    import numpy as np
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix, last_kernel
+    from oracle import oracle as O
     for block, k, p in (shapes or REF_BENCH_SHAPES):
         T = k + p
         r = R.core.ReedSolomon(k, p, 8)
-        if block >= 4096:  # whole 4 KiB chunks: time the codec's bit-sliced
-            r.kernel_kind(wait=True)  # kernels, not the table kernels meanwhile
+        r.kernel_kind(wait=True)  # time the codec's bit-sliced kernels, not the
+        # table kernels while they build (1 and 2 KiB shards: RSE_OPT_SUB_CHUNKS)
         n = max(1, min(32768, (256 << 20) // (T * block)))
         buf = torch.empty(n * T * block, dtype=torch.uint8, device="cuda")
         fill_splitmix(buf, SEED, 0x7E57)
@@ -913,7 +943,8 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
             e = {"shape": f"{k}+{p} x {block // 1024} KiB", "op": op}
             if op == "encode":
                 e["gpu_flat"] = {"stripes": n, "GB_per_s": timed_gbps(
-                    lambda: r.encode_flat(buf, block, n), n * T * block, stream)}
+                    lambda: r.encode_flat(buf, block, n), n * T * block, stream),
+                    "kernel": last_kernel()}
                 rows, _ = _ref_rows(k, p, None)
                 want = [np.zeros(block, np.uint8) for _ in range(p)]
                 O.code_some_slices(8, rows, [v[0, i].cpu().numpy() for i in range(k)], want)
@@ -936,7 +967,8 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
                 pres = (ctypes.c_uint8 * T)(*[0 if i in erased else 1 for i in range(T)])
                 if d:
                     leg = reconstruct_leg(r, v, k, erased, block, n, stream, None, None)
-                    e["gpu_flat"] = {"stripes": n, "GB_per_s": leg["GB_per_s"]}
+                    e["gpu_flat"] = {"stripes": n, "GB_per_s": leg["GB_per_s"],
+                                     "kernel": last_kernel()}
                     e["rebuilt_ok_all_stripes"] = leg["rebuilt_ok_all_stripes"]
 
                 def dev():
@@ -966,9 +998,6 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
             out["entries"].append(e)
         del buf, v, host_shards
         torch.cuda.empty_cache()
-    out["crossover_10_4"] = (per_call_crossover(stream, crossover_sizes) if crossover_sizes
-                             else per_call_crossover(stream))
-    return out
 
 
 def _ck(rc):

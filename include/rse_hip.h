@@ -356,6 +356,9 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                         2 MiB goes through one pinned staging buffer (CPU copies,
                                         one DMA each way) instead of the chunk pipeline's per-shard
                                         copies; 0: always the pipeline (A/B) */
+#define RSE_OPT_SUB_CHUNKS 33        /* 1 (default): shards of exactly 1 or 2 KiB run on the
+                                        bit-sliced kernels, a 4 KiB chunk taking 4 or 2 stripes'
+                                        shards; 0: the table kernels (A/B) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

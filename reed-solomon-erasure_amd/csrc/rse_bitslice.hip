@@ -37,10 +37,10 @@ constexpr int kBsDefaultVariant8 = 5, kBsDefaultVariant16 = 0;
 #include "rse_bs_tables.inc"
 
 template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false,
-          bool CE = false>
+          bool CE = false, uint32_t SUB = 0>
 __global__ __launch_bounds__(kBsBlock, C::p > 4 ? 2 : 3) void bitslice_kernel(
     const CodeArgs a, uint64_t chunks_per_stripe) {
-  bitslice_body<C, NT, SB, XC, XM, WT, W4, false, CE>(a, chunks_per_stripe);
+  bitslice_body<C, NT, SB, XC, XM, WT, W4, false, CE, SUB>(a, chunks_per_stripe);
   if constexpr (CE) signal_done(a);
 }
 
@@ -393,6 +393,7 @@ struct BsShape {
                       // write-through (sc1) stores ([8][0] sc1, [8][1] sc1 nt), 9 = 1
                       // without shared subexpressions (GF(2^16); = 1 for GF(2^8))
   BsFn w4;            // 4 KiB chunks, one per wave (variant 1's scheme, nt)
+  BsFn sub[2];        // the same over 1 / 2 KiB shards, 4 / 2 stripes per chunk (SUB)
   BsFn chk;           // the default variant for the check modes (verify): the
                       // stored parity loaded before un-slicing (store_outputs CE)
   BsRecFn rec[4][4];  // [RSE_OPT_RECON_MIX: kReconMix*][sigma rows NS = 1, 2, 4, 8]
@@ -458,6 +459,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
      bitslice_kernel<C, true, true, false, false, true>},                          \
     {nullptr, bitslice_kernel<CP, true, true, false>}},                            \
    bitslice_kernel<C, true, true, false, false, false, true>,                      \
+   {bitslice_kernel<C, true, true, false, false, false, true, false, 1024u>,       \
+    bitslice_kernel<C, true, true, false, false, false, true, false, 2048u>},      \
    bitslice_kernel<C, true, C::NP == 8, false, false, false, false, true>,         \
    {{rec_fn<C, 1, 0>(), rec_fn<C, 2, 0>(), rec_fn<C, 4, 0>(), rec_fn<C, 8, 0>()},  \
     {rec_fn<C, 1, 1>(), rec_fn<C, 2, 1>(), rec_fn<C, 4, 1>(), rec_fn<C, 8, 1>()},  \
@@ -511,11 +514,14 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
   *handled = false;
   *done = 0;
   constexpr uint64_t kV16 = kBsChunk / 16, kV4 = 4096 / 16;  // vectors per chunk
+  // shards of exactly 1 or 2 KiB: 4 or 2 stripes per 4 KiB chunk (SUB)
+  const bool subm = (a.len == 1024u || a.len == 2048u) && a.n_vec * 16u == a.len &&
+                    get_option(33) != 0;
   // accumulate: store mode on a wide codec's block kernels (kJitBlock) only
-  if (a.n_vec < kV4 || (a.accumulate && a.mode != kStore)) return hipSuccess;
+  if ((a.n_vec < kV4 && !subm) || (a.accumulate && a.mode != kStore)) return hipSuccess;
   // the kernels for these coefficients: compiled in, or specialised at run time
-  BsFn f16 = nullptr, f4 = nullptr;
-  hipFunction_t j16 = nullptr, j4 = nullptr;
+  BsFn f16 = nullptr, f4 = nullptr, fs = nullptr;
+  hipFunction_t j16 = nullptr, j4 = nullptr, js = nullptr;
   bool compiled = false;
   int vopt_used = -1;
   bool chk = false;  // f16 is the compiled check kernel (it reads a.done)
@@ -538,6 +544,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     }
     vopt_used = v;
     f4 = sh.w4;
+    fs = sh.sub[a.len == 2048u];
     compiled = true;
     break;
   }
@@ -548,6 +555,7 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
       return e;
     j16 = a.accumulate ? jf.enc_acc : jf.enc;
     j4 = a.accumulate ? jf.enc4_acc : jf.enc4;
+    js = a.accumulate ? nullptr : jf.sub[a.len == 2048u];
     if (!j16) return hipSuccess;
     if (a.mode != kStore && !a.accumulate && nt && jf.chk && get_option(4) < 0) {
       j16 = jf.chk;  // the check kernel, which can signal the call's completion
@@ -582,6 +590,24 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
     void* argv[] = {const_cast<CodeArgs*>(&args), &cps_arg};
     return hipModuleLaunchKernel(j, (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, argv, nullptr);
   };
+  if (subm) {
+    // one launch codes every byte: 4096 / len stripes per chunk, a chunk per
+    // wave; never the whole call's completion signal (not a check kernel)
+    if (!fs && !js) return hipSuccess;
+    const uint64_t spc = 4096u / a.len, chunks = (a.n_stripes + spc - 1) / spc;
+    if (compiled)
+      note_kernel("bitslice gf%d %u+%u v%d nt1 sub%u", field, a.n_in, a.n_out, vopt_used,
+                  a.len / 1024u);
+    else
+      note_kernel("bitslice-jit gf%d %u+%u sub%u", field, a.n_in, a.n_out, a.len / 1024u);
+    CodeArgs c = a;
+    c.done = c.done_count = nullptr;
+    const hipError_t e = launch(fs, js, c, 0, (chunks + 3) / 4);
+    if (e != hipSuccess) return e;
+    *done = a.len;
+    *handled = true;
+    return hipSuccess;
+  }
   // whole 16 KiB chunks, then whole 4 KiB chunks of the rest (one per wave)
   const uint64_t cps16 = a.n_vec / kV16, cps4 = (a.n_vec - cps16 * kV16) / kV4;
   if (compiled)

@@ -255,10 +255,14 @@ __device__ __forceinline__ void mac_input(uint32_t (&acc)[N], const uint32_t (&p
 // part of its latency (a one-stripe verify: 60 -> 52 us per 10+4 x 16 MiB
 // call).  A separate instantiation for the check kernels: in the store-mode
 // kernel the reordered code cost the headline encode 1.2 % (same box A/B).
+// ok: this lane's bytes belong to the launch (false only for the lanes of a
+// stripe-interleaved chunk past the last stripe, SUB below): no store, no
+// verdict.
 template <class C, bool NT, bool WT = false, uint32_t S = kBsBlock * 16, int O0 = 0,
           class A = CodeArgs, bool CE = false>
 __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const A& a,
-                                              uint64_t off, uint32_t mode, bool& diff) {
+                                              uint64_t off, uint32_t mode, bool& diff,
+                                              bool ok = true) {
 #pragma unroll
   for (int o = 0; o < C::p; ++o) {
     uint32_t pl[16];
@@ -271,10 +275,11 @@ __device__ __forceinline__ void store_outputs(uint32_t (&acc)[C::p * 16], const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t o16 = off + j * S;
-      if (mode != kCheck) stv_policy<NT, WT>(a.out[O0 + o] + o16, v[j]);
+      if (mode != kCheck && ok) stv_policy<NT, WT>(a.out[O0 + o] + o16, v[j]);
       if (mode != kStore) {
         if (!CE) w[j] = ldv<NT>(a.cmp[O0 + o] + o16);
-        diff |= (w[j].x != v[j].x) | (w[j].y != v[j].y) | (w[j].z != v[j].z) | (w[j].w != v[j].w);
+        diff |= ok & ((w[j].x != v[j].x) | (w[j].y != v[j].y) | (w[j].z != v[j].z) |
+                      (w[j].w != v[j].w));
       }
     }
   }
@@ -331,23 +336,41 @@ __device__ __forceinline__ void code_inputs(uint32_t (&acc)[C::p * 16], u32x4 (&
 //  ACC: accumulate mode (a.accumulate): the outputs' current bytes are
 //      loaded and sliced into the accumulators first -- the blocks of a wide
 //      codec's parity matrix, input chunk after input chunk (rse_jit.cpp).
+//  SUB: shards of exactly 1 KiB or 2 KiB (W4 only): a wave's "4 KiB chunk"
+//      is 4096 / SUB consecutive stripes' shards.  64 * SUB / 4096 lanes take
+//      each stripe, lane vectors SUB / 4 bytes apart (each load instruction:
+//      runs of SUB / 4 contiguous bytes per stripe), so the reference's own
+//      1-2 KiB blocks (benches/bandwidth.rs:88-190) run on the bit-sliced
+//      networks too.  The bit-slicing never mixes bytes of different lane
+//      vector positions, so lanes of different stripes are independent; lanes
+//      past the last stripe load the last stripe's bytes and store nothing.
+//      chunks_per_stripe is unused (the chunk count follows from n_stripes).
 template <class C, bool NT, bool SB, bool XC, bool XM = false, bool WT = false, bool W4 = false,
-          bool ACC = false, bool CE = false>
+          bool ACC = false, bool CE = false, uint32_t SUB = 0>
 __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks_per_stripe) {
   static_assert(!(XC && W4), "cross-chunk prefetch is for 16 KiB chunks");
   static_assert(!(XC && ACC), "cross-chunk prefetch is for store mode");
-  constexpr uint32_t S = W4 ? 1024u : kBsBlock * 16u;
+  static_assert(SUB == 0 || (W4 && (SUB == 1024u || SUB == 2048u)),
+                "stripe-interleaved chunks: 1 or 2 KiB shards, one chunk per wave");
+  constexpr uint32_t S = SUB ? SUB / 4u : W4 ? 1024u : kBsBlock * 16u;
   constexpr uint64_t CH = W4 ? 4096u : kBsChunk;
-  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  constexpr uint32_t SPC = SUB ? 4096u / SUB : 1u, LPS = 64u / SPC;  // stripes / chunk, lanes / stripe
+  const uint64_t total = SUB ? (a.n_stripes + SPC - 1) / SPC : chunks_per_stripe * a.n_stripes;
   const uint64_t steps = W4 ? (total + 3) / 4 : total;
   const uint32_t sub = W4 ? threadIdx.x >> 6 : 0u;  // wave-uniform
-  const uint32_t lane_off = (W4 ? (threadIdx.x & 63u) : threadIdx.x) * 16u;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane_off = (SUB ? lane % LPS : W4 ? lane : threadIdx.x) * 16u;
   const uint32_t G = gridDim.x;
   const uint32_t wg = (XM && G % 8u == 0) ? (blockIdx.x % 8u) * (G / 8u) + blockIdx.x / 8u
                                            : blockIdx.x;
   const uint32_t mode = a.mode;
   bool diff = false;
   auto chunk_off = [&](uint64_t c) {
+    if constexpr (SUB) {
+      uint64_t stripe = c * SPC + lane / LPS;
+      if (stripe >= a.n_stripes) stripe = a.n_stripes - 1;  // loaded, never stored
+      return stripe * a.stripe_stride + lane_off;
+    }
     const uint64_t stripe = c / chunks_per_stripe, chunk = c - stripe * chunks_per_stripe;
     return stripe * a.stripe_stride + chunk * CH + lane_off;
   };
@@ -373,9 +396,10 @@ __device__ __forceinline__ void bitslice_body(const CodeArgs& a, uint64_t chunks
       }
     }
     code_inputs<C, NT, SB, XC, 0, S, ACC>(acc, cur, a, off, next_off);
-    store_outputs<C, NT, WT, S, 0, CodeArgs, CE>(acc, a, off, mode, diff);
-    if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe
-      flag_mismatch(a.mismatch + c / chunks_per_stripe);
+    const bool ok = SUB == 0 || c * SPC + lane / LPS < a.n_stripes;
+    store_outputs<C, NT, WT, S, 0, CodeArgs, CE>(acc, a, off, mode, diff, ok);
+    if (a.per_stripe && diff) {  // verify_flat: this chunk's stripe (SUB: this lane's)
+      flag_mismatch(a.mismatch + (SUB ? c * SPC + lane / LPS : c / chunks_per_stripe));
       diff = false;
     }
   }
@@ -594,7 +618,7 @@ __device__ __forceinline__ void wide_rounds(uint32_t (&acc)[C::p * 16], u32x4 (&
 // workgroup, ~32 KiB per CU at 2 workgroups -- ~8 MiB over the chip, which at
 // ~2 us of loaded HBM latency caps the read rate near 4 TB/s whatever the
 // VALU does (Little's law); D inputs per wave raise that cap D-fold.
-template <class C, int W, int WI, int D, int R, class A>
+template <class C, int W, int WI, int D, int R, class A, uint32_t S = 1024u>
 __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
                                                  u32x4 (&buf)[D + 1][4], const A& a, uint64_t off,
                                                  uint64_t next_off, WidePlanes<W>& lds, uint32_t& g,
@@ -603,9 +627,9 @@ __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
   if constexpr (R < NR) {
     constexpr int mine = R * W + WI, ahead = R + D;
     if constexpr (ahead < NR) {
-      if constexpr (ahead * W + WI < K) load4<false, 1024u>(buf[ahead % (D + 1)], a.in[ahead * W + WI] + off);
+      if constexpr (ahead * W + WI < K) load4<false, S>(buf[ahead % (D + 1)], a.in[ahead * W + WI] + off);
     } else if constexpr ((ahead - NR) * W + WI < K) {
-      if (next_off != ~0ull) load4<false, 1024u>(buf[ahead % (D + 1)], a.in[(ahead - NR) * W + WI] + next_off);
+      if (next_off != ~0ull) load4<false, S>(buf[ahead % (D + 1)], a.in[(ahead - NR) * W + WI] + next_off);
     }
     __builtin_amdgcn_sched_barrier(0);
     uint4(&set)[W][4][64] = lds[g & 1u];
@@ -619,23 +643,32 @@ __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
     __syncthreads();
     wide_code_round<C, W, R, 0>(acc, set, lane);
     ++g;
-    wide_rounds_deep<C, W, WI, D, R + 1, A>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_deep<C, W, WI, D, R + 1, A, S>(acc, buf, a, off, next_off, lds, g, lane);
   }
 }
 
 // Wave WI of W; C its share of the outputs (O0 the first).  All W waves call
 // this with the same `lds` (one workgroup-wide array).  D: inputs in flight
 // per wave (wide_rounds_deep); 1 is wide_rounds.
-template <class C, int O0, int W, int WI, int D, class A>
+// SUB: 1 or 2 KiB shards, a chunk = 4096 / SUB consecutive stripes' shards
+// (bitslice_body's SUB).
+template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0>
 __device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& lds) {
   const WideHdr& h = a.h;
   constexpr int K = C::k, NR = (K + W - 1) / W;
-  const uint64_t total = h.chunks_per_stripe * h.n_stripes;
-  const uint32_t lane = threadIdx.x & 63u, lane_off = lane * 16u;
+  constexpr uint32_t S = SUB ? SUB / 4u : 1024u;
+  constexpr uint32_t SPC = SUB ? 4096u / SUB : 1u, LPS = 64u / SPC;
+  const uint64_t total = SUB ? (h.n_stripes + SPC - 1) / SPC : h.chunks_per_stripe * h.n_stripes;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = (SUB ? lane % LPS : lane) * 16u;
   const uint32_t mode = h.mode;
   bool diff = false;
   uint32_t g = 0;
   auto chunk_off = [&](uint64_t c) {
+    if constexpr (SUB) {
+      uint64_t stripe = c * SPC + lane / LPS;
+      if (stripe >= h.n_stripes) stripe = h.n_stripes - 1;  // loaded, never stored
+      return stripe * h.stripe_stride + lane_off;
+    }
     const uint64_t stripe = c / h.chunks_per_stripe, chunk = c - stripe * h.chunks_per_stripe;
     return stripe * h.stripe_stride + chunk * 4096u + lane_off;
   };
@@ -644,14 +677,14 @@ __device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& ld
     const uint64_t off0 = chunk_off(blockIdx.x);
 #pragma unroll
     for (int j = 0; j < D; ++j)
-      if (j < NR && j * W + WI < K) load4<false, 1024u>(buf[j], a.in[j * W + WI] + off0);
+      if (j < NR && j * W + WI < K) load4<false, S>(buf[j], a.in[j * W + WI] + off0);
   }
   for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
     const uint64_t off = chunk_off(c);
     const uint64_t next = c + gridDim.x;
     const uint64_t next_off = next < total ? chunk_off(next) : ~0ull;
     uint32_t acc[C::p * 16];
-    wide_rounds_deep<C, W, WI, D, 0, A>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_deep<C, W, WI, D, 0, A, S>(acc, buf, a, off, next_off, lds, g, lane);
     if constexpr (NR % (D + 1) != 0) {  // the next chunk's rounds j into slots j
       u32x4 t[D][4];
 #pragma unroll
@@ -663,9 +696,10 @@ __device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& ld
 #pragma unroll
         for (int q = 0; q < 4; ++q) buf[j][q] = t[j][q];
     }
-    store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
+    store_outputs<C, true, false, S, O0, A>(acc, a, off, mode, diff,
+                                            SUB == 0 || c * SPC + lane / LPS < h.n_stripes);
     if (h.per_stripe && diff) {
-      flag_mismatch(h.mismatch + (c / h.chunks_per_stripe));
+      flag_mismatch(h.mismatch + (SUB ? c * SPC + lane / LPS : c / h.chunks_per_stripe));
       diff = false;
     }
   }

@@ -208,6 +208,12 @@ hipError_t run_chunk(const Job& j, size_t o0, size_t no, size_t i0, size_t ni, u
   return e;
 }
 
+// Shard lengths the bit-sliced kernels code (some of): at least one 4 KiB
+// chunk, or exactly 1 or 2 KiB (4 / 2 stripes per chunk, RSE_OPT_SUB_CHUNKS).
+bool bitslice_len(size_t len) {
+  return len >= 4096 || ((len == 1024 || len == 2048) && rse::get_option(RSE_OPT_SUB_CHUNKS));
+}
+
 // Executes a Job; `scratch` provides per-output buffers when a CHECK job must
 // be split over several input chunks (full sums are needed before comparing).
 int run_job(const Job& j, hipStream_t s) {
@@ -216,7 +222,7 @@ int run_job(const Job& j, hipStream_t s) {
   // a wide codec's (or pattern's) rows with their one-module kernel built:
   // every whole 4 KiB chunk in one launch (each input read once, each output
   // written once), the rest of every shard below
-  if (!j.accumulate && j.len_bytes >= 4096 && j.stripe_stride % 16u == 0 &&
+  if (!j.accumulate && bitslice_len(j.len_bytes) && j.stripe_stride % 16u == 0 &&
       rse::get_option(RSE_OPT_BITSLICE) && rse::wide_eligible((uint32_t)n_in, (uint32_t)n_out) &&
       j.n_stripes <= 0xffffffffu) {
     bool al = true;
@@ -656,7 +662,7 @@ hipError_t plan_consts(const rse_codec* c, int dev, const uint8_t** out) {
 // for a codec that streams data, not for one used a few times.
 constexpr uint64_t kWideJitBytes = 1ull << 30;
 void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_t n_stripes = 1) {
-  if (len_bytes < 4096 || c->jit_requested.load(std::memory_order_relaxed)) return;
+  if (!bitslice_len(len_bytes) || c->jit_requested.load(std::memory_order_relaxed)) return;
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||
                     rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   if (wide && !now && rse::get_option(RSE_OPT_JIT) < 2) {
@@ -953,15 +959,20 @@ thread_local int64_t g_host_planned = 0;      // RSE_OPT_HOST_PLANNED_STRIPES
 // for) it on first use.  True if the pattern kernel is ready for this plan.
 // Wide codecs (k > 32) and patterns with more than 8 rows get block kernels
 // instead (jit_register_blocks; run_job launches them once all are ready),
-// for shards of 1 MiB or more (each block is seconds of hiprtc).
-bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes) {
+// when a call codes 1 MiB of every shard or more (each block is seconds of
+// hiprtc; `volume`: the bytes per shard over all stripes of the call).
+// Shards of 16 KiB or more qualify, and of exactly 1 or 2 KiB (bitslice_len:
+// the SUB kernels; at 4-16 KiB the syndrome kernels' 4 KiB chunks serve).
+bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes,
+                    size_t volume = 0) {
   const int64_t mode = rse::get_option(RSE_OPT_JIT);
   if (mode == 0 || !rse::get_option(RSE_OPT_JIT_PATTERNS) || !rse::get_option(RSE_OPT_BITSLICE) ||
-      len_bytes < rse::bitslice_chunk_bytes() || (mode < 2 && plan.pattern_uses < 2))
+      (len_bytes < rse::bitslice_chunk_bytes() && !(len_bytes < 4096 && bitslice_len(len_bytes))) ||
+      (mode < 2 && plan.pattern_uses < 2))
     return false;
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;
   if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
-    if (mode < 2 && len_bytes < (1u << 20)) return false;
+    if (mode < 2 && std::max(len_bytes, volume) < (1u << 20)) return false;
     if (rse::wide_eligible(k, n)) {  // run_job launches it
       if (!rse::jit_register_wide(c->field, k, n, plan.rows.c.data(), true)) return false;
       return rse::jit_wide_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
@@ -1024,7 +1035,7 @@ int flat_reconstruct(const rse_codec* c, uint8_t* base, size_t shard_len, size_t
   int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, data_only, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
   const uint64_t stride = (uint64_t)c->total * sb;
-  if (pattern_kernel(c, plan, sb)) {
+  if (pattern_kernel(c, plan, sb, sb * n_stripes)) {
     ++g_pattern_launches;
     return run_plan_tail(c, plan, 0, stride, n_stripes, s);
   }

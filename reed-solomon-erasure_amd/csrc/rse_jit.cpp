@@ -235,29 +235,36 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     char buf[512];
     std::snprintf(buf, sizeof buf,
                   "struct WideArgs {\n  rse::WideHdr h;\n  const uint8_t* in[%u];\n"
-                  "  uint8_t* out[%u];\n  const uint8_t* cmp[%u];\n};\n"
-                  // at least 2 waves per SIMD (256 VGPRs): __launch_bounds__ of a
-                  // 64-thread group would give 64 VGPRs and spill
-                  "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
-                  "    amdgpu_waves_per_eu(%d))) void rse_jit_wide(const WideArgs a) {\n"
-                  "  __shared__ rse::WidePlanes<%d> lds;\n"
-                  "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
-                  k, p, p, 64 * W, 64 * W, wide_waves_per_eu(p), W);
+                  "  uint8_t* out[%u];\n  const uint8_t* cmp[%u];\n};\n",
+                  k, p, p);
     s += buf;
-    for (int w = 0; w < W; ++w) {
-      uint32_t o0, n;
-      wide_share(p, w, &o0, &n);
-      if (shared)
-        std::snprintf(buf, sizeof buf,
-                      "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d>(a, lds); "
-                      "break;\n",
-                      w, w, o0, W, w, (int)get_option(26));
-      else
-        std::snprintf(buf, sizeof buf,
-                      "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
+    // rse_jit_wide over 4 KiB chunks; with the LDS bodies also _s1 / _s2 over
+    // 1 / 2 KiB shards, 4 / 2 stripes per chunk (wide_body_lds_deep SUB)
+    for (int q = 0; q <= (shared ? 2 : 0); ++q) {
+      std::snprintf(buf, sizeof buf,
+                    // at least 2 waves per SIMD (256 VGPRs): __launch_bounds__ of a
+                    // 64-thread group would give 64 VGPRs and spill
+                    "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
+                    "    amdgpu_waves_per_eu(%d))) void rse_jit_wide%s(const WideArgs a) {\n"
+                    "  __shared__ rse::WidePlanes<%d> lds;\n"
+                    "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
+                    64 * W, 64 * W, wide_waves_per_eu(p), q == 0 ? "" : q == 1 ? "_s1" : "_s2", W);
       s += buf;
+      for (int w = 0; w < W; ++w) {
+        uint32_t o0, n;
+        wide_share(p, w, &o0, &n);
+        if (shared)
+          std::snprintf(buf, sizeof buf,
+                        "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d, "
+                        "WideArgs, %du>(a, lds); break;\n",
+                        w, w, o0, W, w, (int)get_option(26), 1024 * q);
+        else
+          std::snprintf(buf, sizeof buf,
+                        "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
+        s += buf;
+      }
+      s += "    default: break;\n  }\n}\n";
     }
-    s += "    default: break;\n  }\n}\n";
     return s;
   }
   // GF(2^8) temporaries only above 4 outputs (2 waves/SIMD: room for them; at
@@ -290,6 +297,16 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                     "false, true>(a, cps);\n  rse::signal_done(a);\n}\n",
                     p > 4 ? 2 : 3);
       s += buf;
+      // 1 / 2 KiB shards: 4 / 2 stripes per 4 KiB chunk (bitslice_body SUB)
+      for (int q = 1; q <= 2; ++q) {
+        std::snprintf(buf, sizeof buf,
+                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode_s%d(\n"
+                      "    const rse::CodeArgs a, uint64_t cps) {\n"
+                      "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, true, "
+                      "false, false, %du>(a, cps);\n}\n",
+                      p > 4 ? 2 : 3, q, 1024 * q);
+        s += buf;
+      }
     }
     return s;
   }
@@ -801,8 +818,10 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
                        uint64_t len, uint64_t stripe_stride, uint32_t n_stripes, uint32_t mode,
                        uint32_t* mismatch, bool per_stripe, hipStream_t stream, uint64_t* done) {
   *done = 0;
+  // shards of exactly 1 or 2 KiB: 4 or 2 stripes per 4 KiB chunk (SUB)
+  const int subq = (len == 1024u || len == 2048u) && get_option(33) != 0 ? (int)(len / 1024u) : 0;
   const uint64_t cps = len / 4096u;
-  if (cps == 0 || n_stripes == 0) return hipSuccess;
+  if ((cps == 0 && !subq) || n_stripes == 0) return hipSuccess;
   Entry* e = find_entry(field, k, p, rows, k, kJitWide);
   if (!e || status_of(e, get_option(9) >= 2) != 2) return hipSuccess;
   const std::shared_ptr<const Compiled> c = e->built[kEnc].get();
@@ -812,9 +831,10 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   hipFunction_t fn = nullptr;
   {
     std::lock_guard<std::mutex> g(e->mu);
+    const Entry::Loaded* have = nullptr;
     for (auto& d : e->loaded)
-      if (d.dev == dev) fn = d.fns.wide;
-    if (!fn) {
+      if (d.dev == dev) have = &d;
+    if (!have) {
       hipModule_t m = nullptr;
       he = hipModuleLoadData(&m, c->code.data());
       if (he == hipSuccess) he = hipModuleGetFunction(&fn, m, "rse_jit_wide");
@@ -824,9 +844,20 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
       }
       Entry::Loaded l{dev};
       l.fns.wide = fn;
+      // the 1 / 2 KiB kernels exist in modules of the LDS bodies only
+      // (make_source); a missing one is not an error of this call
+      for (int q = 0; q < 2; ++q)
+        if (hipModuleGetFunction(&l.fns.wide_sub[q], m, q ? "rse_jit_wide_s2" : "rse_jit_wide_s1") !=
+            hipSuccess) {
+          l.fns.wide_sub[q] = nullptr;
+          (void)hipGetLastError();
+        }
       e->loaded.push_back(l);
+      have = &e->loaded.back();
     }
+    fn = subq ? have->fns.wide_sub[subq - 1] : have->fns.wide;
   }
+  if (!fn) return hipSuccess;  // no 1 / 2 KiB kernel: the table kernels
   // argument block: header, then the k input, p output and p compare pointers
   std::vector<uint8_t> buf(sizeof(WideHdr) + sizeof(void*) * (k + 2 * (size_t)p), 0);
   WideHdr h{};
@@ -846,7 +877,7 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   size_t size = buf.size();
   void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                    HIP_LAUNCH_PARAM_END};
-  const uint64_t total = cps * n_stripes;
+  const uint64_t total = subq ? (n_stripes + 4u / subq - 1) / (4u / subq) : cps * n_stripes;
   const int64_t grid = get_option(2);
   // tools/tune.py grid sweeps, 128 stripes x 1 MiB (profiles/r04/s2/): GF(2^16)
   // 40+12 16384 workgroups 5.29 TB/s against 5.05 at 4096; GF(2^8) 50+20 flat
@@ -854,12 +885,15 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   uint64_t gx = grid > 0 ? (uint64_t)grid : field == 16 ? 16384u : 8192u;
   if (gx > total) gx = total;
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
-  note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, wide_waves(p));
+  if (subq)
+    note_kernel("bitslice-wide gf%d %u+%u w%d sub%d", field, k, p, wide_waves(p), subq);
+  else
+    note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, wide_waves(p));
   he = hipModuleLaunchKernel(fn, (uint32_t)gx, 1, 1, 64u * (uint32_t)wide_waves(p), 1, 1, 0,
                              stream, nullptr, extra);
   if (he != hipSuccess) return he;
   count_bitslice_launch();
-  *done = cps * 4096u;
+  *done = subq ? len : cps * 4096u;
   return hipSuccess;
 }
 
@@ -919,6 +953,8 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
         if (he == hipSuccess) he = hipModuleGetFunction(&f.enc, m, "rse_jit_encode");
         if (he == hipSuccess) he = hipModuleGetFunction(&f.enc4, m, "rse_jit_encode4");
         if (he == hipSuccess) he = hipModuleGetFunction(&f.chk, m, "rse_jit_check");
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.sub[0], m, "rse_jit_encode_s1");
+        if (he == hipSuccess) he = hipModuleGetFunction(&f.sub[1], m, "rse_jit_encode_s2");
       }
     } else {
       f.n_rec = recon_ns(p, f.rec_ns);

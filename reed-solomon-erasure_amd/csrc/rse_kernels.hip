@@ -792,6 +792,7 @@ struct Options {
   int64_t sync_event = 0;         // verify calls wait on an event, not the stream (A/B)
   int64_t spin_wait = 1;          // one-launch verifies: poll the completion word (A/B)
   int64_t host_direct = 1;        // small one-stripe host calls: one staging buffer (A/B)
+  int64_t sub_chunks = 1;         // 1 / 2 KiB shards on the bit-sliced kernels (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1282,6 +1283,7 @@ int set_option(int key, int64_t value) {
     case 30: g_opt.sync_event = value ? 1 : 0; return 0;
     case 31: g_opt.spin_wait = value ? 1 : 0; return 0;
     case 32: g_opt.host_direct = value ? 1 : 0; return 0;
+    case 33: g_opt.sub_chunks = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1326,6 +1328,7 @@ int64_t get_option(int key) {
     case 30: return g_opt.sync_event;
     case 31: return g_opt.spin_wait;
     case 32: return g_opt.host_direct;
+    case 33: return g_opt.sub_chunks;
     default: return -1;
   }
 }

@@ -335,12 +335,14 @@ struct JitFns {
   hipFunction_t enc4 = nullptr; // ... over 4 KiB chunks, one per wave
   hipFunction_t enc_acc = nullptr, enc4_acc = nullptr;  // accumulate mode (kJitBlockAcc)
   hipFunction_t chk = nullptr;  // the check modes' kernel, with the completion word
+  hipFunction_t sub[2] = {};    // ... over 1 / 2 KiB shards, 4 / 2 stripes per 4 KiB chunk
   int n_rec = 0;
   int rec_ns[5] = {};           // sigma rows of rec[i], ascending
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
   hipFunction_t rec_desc[5] = {};  // ... over per-stripe BsReconArgs (descs, cps, n_stripes)
   hipFunction_t rec_desc4[5] = {}; // ... over 4 KiB chunks, one per wave (descs, cps4, n, base)
   hipFunction_t wide = nullptr;    // kJitWide: rse_jit_wide (WideArgs)
+  hipFunction_t wide_sub[2] = {};  // ... over 1 / 2 KiB shards (rse_jit_wide_s1 / _s2)
 };
 // Kernels of `stage` (0: encode/verify, 1: reconstruct) for a launch whose
 // coefficients rows[o * stride + i] equal a registered codec's parity rows,

@@ -1567,3 +1567,74 @@ def test_jit_verify_completion_word(R, k, p):
             assert r.verify(shards)
     finally:
         lib.rse_set_option(9, old)
+
+
+@pytest.mark.parametrize("field,k,p", [
+    (8, 10, 4), (8, 10, 2), (16, 20, 8),   # compiled codecs
+    (8, 4, 4), (8, 8, 8), (8, 5, 2), (16, 6, 3),  # run-time specialised
+    (8, 50, 20), (8, 16, 16), (16, 40, 12),  # wide codecs (one module)
+])
+@pytest.mark.parametrize("kib", [1, 2])
+def test_sub_chunk_shards(R, field, k, p, kib):
+    """RSE_OPT_SUB_CHUNKS: shards of exactly 1 or 2 KiB (benches/bandwidth.rs:
+    88-190's blocks) on the bit-sliced kernels, 4 or 2 stripes per 4 KiB chunk.
+    Ragged stripe counts (the last chunk's lanes past the last stripe load and
+    store nothing: a guard stripe after the batch stays as it was), parity
+    against the oracle stripe by stripe and against the table kernels
+    (option 33 = 0), verify_flat's per-stripe verdicts from the lanes of
+    shared chunks, and reconstruct_data_flat."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    es = field // 8
+    nb = kib * 1024
+    n = nb // es
+    T = k + p
+    oc = O.Codec(field, k, p)
+    old9, old33 = lib.rse_get_option(9), lib.rse_get_option(33)
+    try:
+        lib.rse_set_option(9, 2)  # run-time builds waited for
+        r = R.core.ReedSolomon(k, p, field)
+        assert r.kernel_kind(wait=True).startswith("bitslice")
+        for stripes in (1, 3, 6, 1001):
+            rng = np.random.default_rng(stripes * 7 + k + p + kib + field)
+            buf = rng.integers(0, 256, (stripes + 1) * T * nb, dtype=np.uint8)
+            d = dev(buf)
+            r.encode_flat(d, n, stripes)
+            kern = last_kernel()
+            assert f"sub{kib}" in kern and kern.startswith("bitslice"), kern
+            got = host(d).reshape(stripes + 1, T, nb)
+            assert (got[stripes] == buf.reshape(stripes + 1, T, nb)[stripes]).all()  # guard
+            assert (got[:, :k] == buf.reshape(stripes + 1, T, nb)[:, :k]).all()
+            for s_ in sorted({0, 1, stripes // 2, stripes - 2, stripes - 1} - {-1}):
+                want = [got[s_, i].copy() for i in range(k)] + [np.zeros(nb, np.uint8)
+                                                               for _ in range(p)]
+                oc.encode(want)
+                for i in range(p):
+                    assert (got[s_, k + i] == want[k + i]).all(), (stripes, s_, i, kern)
+            # the table kernels write the same bytes
+            lib.rse_set_option(33, 0)
+            d2 = dev(buf)
+            r.encode_flat(d2, n, stripes)
+            assert "sub" not in last_kernel(), last_kernel()
+            assert (host(d2) == host(d)).all()
+            lib.rse_set_option(33, 1)
+            # per-stripe verdicts from lanes that share chunks
+            good = host(d)
+            v = good.reshape(stripes + 1, T, nb).copy()
+            want_ok = np.ones(stripes, bool)
+            for s_ in sorted({stripes - 1, stripes // 3}):
+                v[s_, int(rng.integers(0, T)), int(rng.integers(0, nb))] ^= 0x5A
+                want_ok[s_] = False
+            dv = dev(v.reshape(-1))
+            assert (r.verify_flat(dv, n, stripes) == want_ok).all()
+            assert r.verify_flat(d, n, stripes).all()
+            # rebuild two lost data shards of every stripe
+            lost = [1, k - 1] if k > 2 else [0]
+            dd = d.view(stripes + 1, T, nb)
+            for e in lost:
+                dd[:stripes, e].fill_(0)
+            r.reconstruct_data_flat(d, n, stripes, [i not in lost for i in range(T)])
+            assert (host(d) == good).all()
+    finally:
+        lib.rse_set_option(9, old9)
+        lib.rse_set_option(33, old33)

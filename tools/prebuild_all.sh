@@ -1,0 +1,25 @@
+#!/bin/bash
+# Prebuilds, on the host CPU, every run-time specialised module bench.py loads
+# (its wide codecs, the reference bench matrix's codecs and decode patterns,
+# the GF(2^16) cached-pattern leg) into the tree's jitcache/, so a GPU run
+# loads them in milliseconds.  Rerun after any change to the JIT sources
+# (rse_bitslice_core.hpp and the headers rse_jit.cpp embeds): the cache key
+# hashes the whole source, so stale entries are simply never hit.
+cd "$(dirname "$0")/.." || exit 1
+export RSE_JIT_CACHE_DIR=$PWD/jitcache
+mkdir -p jitcache
+pat=()
+seq_csv() { python3 -c "print(','.join(str(i) for i in range($1)))"; }
+# benches/bandwidth.rs:88-190 shapes (bench.py REF_BENCH_SHAPES): erase shard 0,
+# and data shards 0..p-1
+for kp in 4:4 8:8 16:16 32:32 64:64 5:2 10:4 50:20; do
+  k=${kp%:*}; p=${kp#*:}
+  pat+=(--pattern "8:$k:$p:1024:0" --pattern "8:$k:$p:1024:$(seq_csv "$p")")
+done
+pat+=(--pattern "8:4:4:2048:0" --pattern "8:4:4:2048:0,1,2,3")
+pat+=(--pattern "16:20:8:4194304:0,1,2,3")  # other_configs gf16_20_8 cached pattern
+exec python3 tools/prebuild_jit.py \
+  --codec 8:50:20 --codec 16:40:12 --codec 16:100:30 \
+  --codec 8:4:4 --codec 8:8:8 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 --codec 8:5:2 \
+  --codec 8:12:4 --codec 16:6:3 \
+  "${pat[@]}"
