@@ -359,6 +359,11 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_SUB_CHUNKS 33        /* 1 (default): shards of exactly 1 or 2 KiB run on the
                                         bit-sliced kernels, a 4 KiB chunk taking 4 or 2 stripes'
                                         shards; 0: the table kernels (A/B) */
+#define RSE_OPT_SUBFIELD 34          /* 1 (default): a GF(2^16) codec (read at rse_codec_new) or
+                                        coding pass whose coefficients all lie in the GF(2^8)
+                                        subfield -- every codec of at most 256 shards -- codes
+                                        each byte in GF(2^8): the same bytes, half the work;
+                                        0: GF(2^16) kernels (A/B) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

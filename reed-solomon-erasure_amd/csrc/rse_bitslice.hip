@@ -485,7 +485,8 @@ constexpr BsDescFn rec_desc_deep_fn() {
 static const BsShape kBsShapes[] = {
     BS(Bs8_10_4, Bs8_10_4, 8),        // BASELINE headline: galois_8 10+4
     BS(Bs8_10_2, Bs8_10_2, 8),        // benches/bandwidth.rs 10+2
-    BS(Bs16_20_8, Bs16_20_8Plain, 16),  // BASELINE configs[4]: galois_16 20+8
+    BS(Bs8_20_8, Bs8_20_8Plain, 8),   // BASELINE configs[4]: galois_16 20+8 (subfield)
+    BS(Bs16_20_8, Bs16_20_8Plain, 16),  // the same in GF(2^16) (RSE_OPT_SUBFIELD 0)
 };
 #undef BS
 

@@ -60,6 +60,18 @@ struct Rows {
 
 struct rse_codec {
   int field;
+  // The field the kernels code in.  GF(2^16) codecs of at most 256 shards
+  // have every matrix entry in the GF(2^8) subfield (the Vandermonde points
+  // 0..k+p-1 are subfield elements, galois_16.rs:97-107 nth(), and the
+  // subfield is closed under the products and inverses of core.rs:430-436
+  // and 697-731).  A subfield constant c multiplies an element a1 x + a0 as
+  // (c a1) x + c a0 (galois_16.rs:20-52: no reduction term), i.e. each byte
+  // of the element by itself in GF(2^8) (the base field is galois_8's).  So
+  // every coding pass of such a codec -- encode, verify, every decode pattern
+  // -- is the GF(2^8) pass with the same coefficients over the same bytes:
+  // kfield 8 (RSE_OPT_SUBFIELD), half the XOR work of the 16 x 16 bit
+  // matrices.  Otherwise kfield = field.
+  int kfield;
   size_t k, p, total;
   rse::Matrix<rse::Gf8Field> m8;   // field == 8
   rse::Matrix<rse::Gf16Field> m16;  // field == 16
@@ -219,6 +231,18 @@ bool bitslice_len(size_t len) {
 int run_job(const Job& j, hipStream_t s) {
   const size_t n_out = j.rows->n_out, n_in = j.rows->n_in;
   if (n_out == 0 || j.len_bytes == 0) return RSE_OK;
+  // GF(2^16) coefficients all in the GF(2^8) subfield (the low-level entry
+  // points; codecs already arrive as kfield 8): the GF(2^8) pass, byte by
+  // byte (rse_codec::kfield)
+  if (j.field == RSE_FIELD_GF16 && rse::get_option(RSE_OPT_SUBFIELD)) {
+    bool sub = true;
+    for (size_t q = 0; q < j.rows->c.size() && sub; ++q) sub = j.rows->c[q] < 256;
+    if (sub) {
+      Job g = j;
+      g.field = RSE_FIELD_GF8;
+      return run_job(g, s);
+    }
+  }
   // a wide codec's (or pattern's) rows with their one-module kernel built:
   // every whole 4 KiB chunk in one launch (each input read once, each output
   // written once), the rest of every shard below
@@ -670,14 +694,14 @@ void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_
     if (c->wide_bytes.fetch_add(b, std::memory_order_relaxed) + b < kWideJitBytes) return;
   }
   c->jit_requested.store(true, std::memory_order_relaxed);
-  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return;
+  if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
   if (wide && rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p))
-    rse::jit_register_wide(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
+    rse::jit_register_wide(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else if (wide)
-    rse::jit_register_blocks(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
+    rse::jit_register_blocks(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else
-    rse::jit_register(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
+    rse::jit_register(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), rse::kJitCodec);
 }
 
 Rows single_column(const rse_codec* c, size_t i_data) {  // code_single_slice, core.rs:492-509
@@ -924,7 +948,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
     a.par[R[t]] = shards[k + R[t]];
   }
   for (size_t r : M) a.sigma |= 1u << r;
-  rse::set_horner_masks(a, c->field);
+  rse::set_horner_masks(a, c->kfield);
   a.stripe_stride = stripe_stride;
   std::vector<uint16_t> rows(p * k);
   for (size_t r = 0; r < p; ++r)
@@ -940,7 +964,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
     for (size_t r = 0; r < p; ++r)
       if (b.par[r]) b.par[r] += adv;
     for (uint32_t q = 0; q < b.n_out; ++q) b.out[q] += adv;
-    RSE_HIP(rse::launch_bitslice_recon(c->field, (uint32_t)k, (uint32_t)p, rows.data(), b,
+    RSE_HIP(rse::launch_bitslice_recon(c->kfield, (uint32_t)k, (uint32_t)p, rows.data(), b,
                                        len_bytes / 16u, s, &handled));
     if (!handled) return RSE_OK;  // first batch decides; nothing launched
   }
@@ -974,14 +998,14 @@ bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes,
   if (n > rse::kJitMaxOut || k > (uint32_t)kMaxIn) {
     if (mode < 2 && std::max(len_bytes, volume) < (1u << 20)) return false;
     if (rse::wide_eligible(k, n)) {  // run_job launches it
-      if (!rse::jit_register_wide(c->field, k, n, plan.rows.c.data(), true)) return false;
-      return rse::jit_wide_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+      if (!rse::jit_register_wide(c->kfield, k, n, plan.rows.c.data(), true)) return false;
+      return rse::jit_wide_status(c->kfield, k, n, plan.rows.c.data(), mode >= 2) == 2;
     }
-    if (!rse::jit_register_blocks(c->field, k, n, plan.rows.c.data(), true)) return false;
-    return rse::jit_blocks_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+    if (!rse::jit_register_blocks(c->kfield, k, n, plan.rows.c.data(), true)) return false;
+    return rse::jit_blocks_status(c->kfield, k, n, plan.rows.c.data(), mode >= 2) == 2;
   }
-  if (!rse::jit_register(c->field, k, n, plan.rows.c.data(), rse::kJitPattern)) return false;
-  return rse::jit_status(c->field, k, n, plan.rows.c.data(), mode >= 2) == 2;
+  if (!rse::jit_register(c->kfield, k, n, plan.rows.c.data(), rse::kJitPattern)) return false;
+  return rse::jit_status(c->kfield, k, n, plan.rows.c.data(), mode >= 2) == 2;
 }
 
 // Codes plan.rows over [off, len) of every shard (the table kernels).
@@ -993,7 +1017,7 @@ int run_plan_tail(const rse_codec* c, const ReconPlan& plan, size_t off, uint64_
   std::vector<uint8_t*> out(plan.out);
   for (auto& q : in) q += off;
   for (auto& q : out) q += off;
-  Job j{c->field, &plan.rows, in.data(), out.data(), nullptr, len - off, rse::kStore, false,
+  Job j{c->kfield, &plan.rows, in.data(), out.data(), nullptr, len - off, rse::kStore, false,
         nullptr, stripe_stride, n_stripes};
   return run_job(j, s);
 }
@@ -1060,7 +1084,7 @@ int encode_sep_impl(const rse_codec* c, const void* const* data, const size_t* d
   want_bitslice(c, data_lens[0] * c->esize());
   const Rows rows = parity_rows(c);
   if (host) return host_code(c->field, rows, data, parity, data_lens[0] * c->esize(), false, s);
-  Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(data),
+  Job j{c->kfield, &rows, reinterpret_cast<const uint8_t* const*>(data),
         reinterpret_cast<uint8_t* const*>(parity), nullptr, data_lens[0] * c->esize(),
         rse::kStore, false, nullptr, 0, 1};
   return run_job(j, s);
@@ -1082,7 +1106,7 @@ int encode_single_sep_impl(const rse_codec* c, size_t i_data, const void* single
     return host_code(c->field, rows, hin, parity, single_len * c->esize(), i_data != 0, s);
   }
   const uint8_t* in[1] = {static_cast<const uint8_t*>(single)};
-  Job j{c->field, &rows, in, reinterpret_cast<uint8_t* const*>(parity), nullptr,
+  Job j{c->kfield, &rows, in, reinterpret_cast<uint8_t* const*>(parity), nullptr,
         single_len * c->esize(), rse::kStore, i_data != 0, nullptr, 0, 1};
   return run_job(j, s);
 }
@@ -1114,7 +1138,7 @@ int verify_impl(const rse_codec* c, const void* const* shards, const size_t* len
   if (rc) return rc;
   want_bitslice(c, lens[0] * c->esize());
   const Rows rows = parity_rows(c);
-  Job j{c->field, &rows, reinterpret_cast<const uint8_t* const*>(shards),
+  Job j{c->kfield, &rows, reinterpret_cast<const uint8_t* const*>(shards),
         with_buffer ? reinterpret_cast<uint8_t* const*>(buffer) : nullptr,
         reinterpret_cast<const uint8_t* const*>(shards) + c->k, lens[0] * c->esize(),
         with_buffer ? rse::kCheckStore : rse::kCheck, false, nullptr, 0, 1};
@@ -1614,6 +1638,10 @@ int rse_codec_new(int field, size_t data_shards, size_t parity_shards, rse_codec
         for (size_t j = 0; j < c->k; ++j) top.at(r, j) = v.at(r, j);
       if (!top.invert(inv)) return RSE_ERR_SINGULAR_MATRIX;
       c->m16 = v.multiply(inv);
+      bool sub = rse::get_option(RSE_OPT_SUBFIELD) != 0;
+      for (size_t r = 0; r < c->total && sub; ++r)
+        for (size_t j = 0; j < c->k && sub; ++j) sub = c->m16.at(r, j) < 256;
+      c->kfield = sub ? RSE_FIELD_GF8 : RSE_FIELD_GF16;
     } else {
       auto v = rse::Matrix<rse::Gf8Field>::vandermonde(c->total, c->k);
       rse::Matrix<rse::Gf8Field> top(c->k, c->k), inv;
@@ -1621,6 +1649,7 @@ int rse_codec_new(int field, size_t data_shards, size_t parity_shards, rse_codec
         for (size_t j = 0; j < c->k; ++j) top.at(r, j) = v.at(r, j);
       if (!top.invert(inv)) return RSE_ERR_SINGULAR_MATRIX;
       c->m8 = v.multiply(inv);
+      c->kfield = RSE_FIELD_GF8;
     }
     *out = c.release();
     return RSE_OK;
@@ -1637,17 +1666,17 @@ size_t rse_codec_total_shard_count(const rse_codec* c) { return c ? c->total : 0
 
 int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
-  if (rse::bitslice_compiled(c->field, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
+  if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const Rows rows = parity_rows(c);
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||
                     rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   const bool one = rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
-  switch (wide ? (one ? rse::jit_wide_status(c->field, (uint32_t)c->k, (uint32_t)c->p,
+  switch (wide ? (one ? rse::jit_wide_status(c->kfield, (uint32_t)c->k, (uint32_t)c->p,
                                              rows.c.data(), wait != 0)
-                      : rse::jit_blocks_status(c->field, (uint32_t)c->k, (uint32_t)c->p,
+                      : rse::jit_blocks_status(c->kfield, (uint32_t)c->k, (uint32_t)c->p,
                                                rows.c.data(), wait != 0))
-               : rse::jit_status(c->field, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
+               : rse::jit_status(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(),
                                  wait != 0)) {
     case 2: return RSE_KERNELS_SPECIALISED;
     case 1: return RSE_KERNELS_SPECIALISING;
@@ -1755,7 +1784,7 @@ int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t 
   for (size_t r = 0; r < c->p; ++r) out[r] = base + (c->k + r) * sb;
   want_bitslice(c, sb, false, n_stripes);
   const Rows rows = parity_rows(c);
-  Job j{c->field, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
+  Job j{c->kfield, &rows, in.data(), out.data(), nullptr, sb, rse::kStore, false, nullptr,
         (uint64_t)c->total * sb, n_stripes};
   return run_job(j, (hipStream_t)stream);
 }
@@ -1773,7 +1802,7 @@ int rse_verify_flat(const rse_codec* c, const void* stripes, size_t shard_len, s
   for (size_t r = 0; r < c->p; ++r) cmp[r] = base + (c->k + r) * sb;
   want_bitslice(c, sb, false, n_stripes);
   const Rows rows = parity_rows(c);
-  Job j{c->field, &rows, in.data(), nullptr, cmp.data(), sb, rse::kCheck, false, nullptr,
+  Job j{c->kfield, &rows, in.data(), nullptr, cmp.data(), sb, rse::kCheck, false, nullptr,
         (uint64_t)c->total * sb, n_stripes, true};
   std::vector<int> res;
   try {
@@ -1999,7 +2028,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       uint8_t* ws = dflags + desc_off;  // the descriptors
       uint64_t bs_done = 0;
       e = rse::launch_bitslice_recon_batch(
-          c->field, (uint32_t)k, (uint32_t)p, rows.c.data(),
+          c->kfield, (uint32_t)k, (uint32_t)p, rows.c.data(),
           reinterpret_cast<const uint16_t*>(consts), consts + plan_tab_off(c), dfl,
           data_only ? 1u : 0u, base, sb, (uint32_t)n_stripes, need, e_cap,
           reinterpret_cast<rse::BsReconArgs*>(ws), st, &bs_done);
@@ -2061,7 +2090,7 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   hipError_t e = hipSuccess;
   for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {
     const size_t ng = std::min(grp, n_stripes - g0);
-    e = rse::launch_recon_plan(c->field, reinterpret_cast<const uint16_t*>(consts), dfl + g0 * T,
+    e = rse::launch_recon_plan(c->kfield, reinterpret_cast<const uint16_t*>(consts), dfl + g0 * T,
                                (uint32_t)k, (uint32_t)T, data_only ? 1u : 0u, e_cap, nout_cap,
                                base + g0 * T * sb, sb, done, sb - done, (uint32_t)ng,
                                reinterpret_cast<CodeArgs*>(ws), st);

@@ -793,6 +793,7 @@ struct Options {
   int64_t spin_wait = 1;          // one-launch verifies: poll the completion word (A/B)
   int64_t host_direct = 1;        // small one-stripe host calls: one staging buffer (A/B)
   int64_t sub_chunks = 1;         // 1 / 2 KiB shards on the bit-sliced kernels (A/B)
+  int64_t subfield = 1;           // GF(2^16) codecs of <= 256 shards code in GF(2^8) (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1284,6 +1285,7 @@ int set_option(int key, int64_t value) {
     case 31: g_opt.spin_wait = value ? 1 : 0; return 0;
     case 32: g_opt.host_direct = value ? 1 : 0; return 0;
     case 33: g_opt.sub_chunks = value ? 1 : 0; return 0;
+    case 34: g_opt.subfield = value ? 1 : 0; return 0;
     default: return -1;
   }
 }
@@ -1329,6 +1331,7 @@ int64_t get_option(int key) {
     case 31: return g_opt.spin_wait;
     case 32: return g_opt.host_direct;
     case 33: return g_opt.sub_chunks;
+    case 34: return g_opt.subfield;
     default: return -1;
   }
 }

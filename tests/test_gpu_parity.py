@@ -31,6 +31,26 @@ def R():
     return R
 
 
+@pytest.fixture
+def subfield(R, request):
+    """RSE_OPT_SUBFIELD for one test (read when a codec is created): 1, the
+    default, codes GF(2^16) codecs of at most 256 shards in the GF(2^8)
+    subfield; 0 keeps their GF(2^16) kernels, which codecs past 256 shards
+    need, so the kernel tests run both.  GF(2^8) cases run once."""
+    lib = R._lib.load()
+    cs = request.node.callspec.params
+    field = cs.get("field", 16)
+    if request.param == 0 and (field == 8 or cs.get("k", 0) + cs.get("p", 0) > 256):
+        pytest.skip("GF(2^8), or past 256 shards: GF(2^16) kernels either way")
+    old = lib.rse_get_option(34)
+    lib.rse_set_option(34, request.param)
+    yield request.param
+    lib.rse_set_option(34, old)
+
+
+SUBFIELD = pytest.mark.parametrize("subfield", [1, 0], indirect=True, ids=["sub", "gf16"])
+
+
 def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8)).cuda()
 
@@ -522,7 +542,8 @@ def test_flat_small_shards_many_stripes(R, field, k, p, n, stripes):
     (16, 6, 3, 8192 * 3, 4, 1, 0),         # run-time specialised GF(2^16) codec
 ])
 @pytest.mark.parametrize("dflags", [False, True])
-def test_reconstruct_batch_per_stripe_patterns(R, field, k, p, n, stripes, bs, hp, dflags):
+@SUBFIELD
+def test_reconstruct_batch_per_stripe_patterns(R, subfield, field, k, p, n, stripes, bs, hp, dflags):
     """rse_reconstruct_batch: every stripe with its own erasure pattern, against
     the oracle's reconstruct of each stripe (core.rs:680/690 semantics).  bs:
     the whole 16 KiB chunks run on the bit-sliced syndrome kernels from
@@ -612,7 +633,8 @@ def test_reconstruct_batch_many_stripes_and_errors(R):
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
 @pytest.mark.parametrize("chunks,extra", [(1, 0), (3, 16), (2, 2), (6, 1717),
                                           (0, 4096), (1, 12336), (2, 8194)])  # 4 KiB chunks
-def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra):
+@SUBFIELD
+def test_bitslice_matches_table_kernels_and_oracle(R, subfield, field, k, p, chunks, extra):
     """The bit-sliced kernels (compiled-in parity rows) against the table
     kernels and the oracle: encode (whole 16 KiB chunks bit-sliced, the rest
     table-coded), verify (check mode) and multi-stripe flat encode."""
@@ -667,7 +689,8 @@ def test_bitslice_matches_table_kernels_and_oracle(R, field, k, p, chunks, extra
 
 
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
-def test_bitslice_kernel_variants(R, field, k, p):
+@SUBFIELD
+def test_bitslice_kernel_variants(R, subfield, field, k, p):
     """Every compiled bit-sliced encode variant (plain, scheduling barrier,
     cross-chunk prefetch, LDS-DMA rings of 3 and 2 slots) x nt, in store and
     check modes, over several stripes and workgroup counts so that workgroups
@@ -714,7 +737,8 @@ def test_bitslice_kernel_variants(R, field, k, p):
 
 
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4), (8, 10, 2)])
-def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
+@SUBFIELD
+def test_bitslice_reconstruct_every_erasure_count(R, subfield, field, k, p):
     """Syndrome reconstruct on the bit-sliced kernels (compiled parity rows,
     runtime erasure pattern) against the oracle: every number of erased
     shards 1..p, data and/or parity, reconstruct and reconstruct_data, a
@@ -770,7 +794,8 @@ def test_bitslice_reconstruct_every_erasure_count(R, field, k, p):
 
 
 @pytest.mark.parametrize("field,k,p", [(16, 20, 8), (8, 10, 4)])
-def test_reconstruct_every_mixing_mode(R, field, k, p):
+@SUBFIELD
+def test_reconstruct_every_mixing_mode(R, subfield, field, k, p):
     """The three e x e mixings of the syndrome reconstruct (RSE_OPT_RECON_MIX
     0 v_perm tables, 1 doubling chains, 2 Horner's rule -- the default) give
     the oracle's bytes on the same patterns: every syndrome row in use (rows
@@ -819,7 +844,8 @@ def test_reconstruct_every_mixing_mode(R, field, k, p):
 # RSE_OPT_RECON_PAIRS: pairs per workgroup (1, 2); 3 the prefetching variant,
 # 6 the compact mixing (one pair per workgroup)
 @pytest.mark.parametrize("pairs", [1, 2, 3, 6, 7])
-def test_reconstruct_wave_pairs(R, pairs):
+@SUBFIELD
+def test_reconstruct_wave_pairs(R, subfield, pairs):
     """GF(2^16) 20+8 syndrome reconstruct at 8 sigma rows on wave pairs
     (RSE_OPT_RECON_PAIRS, the default): each wave of a pair holds 4 syndrome
     rows, data planes are exchanged through LDS and the outputs' partial sums
@@ -893,7 +919,8 @@ JIT_CODECS = [(8, 12, 4), (8, 6, 3), (8, 4, 2), (8, 32, 8), (8, 1, 1), (8, 17, 5
 
 
 @pytest.mark.parametrize("field,k,p", JIT_CODECS)
-def test_run_time_specialised_bitslice(R, field, k, p):
+@SUBFIELD
+def test_run_time_specialised_bitslice(R, subfield, field, k, p):
     """Codecs without compiled-in bit-sliced kernels get them specialised at
     run time (hiprtc, rse_jit.cpp).  With RSE_OPT_JIT 2 the first launch waits
     for the build, so every call below runs the specialised kernels (checked
@@ -969,7 +996,8 @@ def test_run_time_specialised_bitslice(R, field, k, p):
     (8, 12, 4, [[1, 2, 3], [0, 15]]),
     (8, 32, 8, [[0, 8, 16, 24, 32, 33, 39]]),
 ])
-def test_decode_pattern_kernels(R, field, k, p, erasures):
+@SUBFIELD
+def test_decode_pattern_kernels(R, subfield, field, k, p, erasures):
     """Repeated erasure patterns get their composed decode rows specialised
     into a bit-sliced kernel at run time (RSE_OPT_JIT 2: built on first use
     and waited for).  reconstruct, reconstruct_data and the flat many-stripe
@@ -1043,7 +1071,8 @@ def test_decode_pattern_kernels(R, field, k, p, erasures):
     (8, 7, 3, 777),               # table kernels, byte path (stride not 16-aligned)
     (8, 40, 20, 300),             # k > 32: sums materialised, then compared per stripe
 ])
-def test_verify_flat_per_stripe(R, field, k, p, n):
+@SUBFIELD
+def test_verify_flat_per_stripe(R, subfield, field, k, p, n):
     """rse_verify_flat: one pass over many stripes, one verdict per stripe
     (core.rs:637-651 applied stripe by stripe), with corruptions in data and
     parity shards, in bit-sliced chunks and in tails, and clean stripes."""
@@ -1421,7 +1450,7 @@ def test_wide_codec_unbalanced_waves(R):
     old = lib.rse_get_option(19)
     try:
         assert lib.rse_set_option(19, 0) == 0
-        test_wide_codec_kernels(R, 8, 7, 11, 1)
+        test_wide_codec_kernels(R, 1, 8, 7, 11, 1)
         from reed_solomon_erasure.core import last_kernel
         assert last_kernel().startswith("bitslice-wide gf8 7+11 w2"), last_kernel()
     finally:
@@ -1429,7 +1458,8 @@ def test_wide_codec_unbalanced_waves(R):
 
 
 @pytest.mark.parametrize("field,k,p,modules", WIDE_CODECS)
-def test_wide_codec_kernels(R, field, k, p, modules):
+@SUBFIELD
+def test_wide_codec_kernels(R, subfield, field, k, p, modules):
     """Wide codecs (k > 32 or p > 8) on their run-time specialised kernels:
     one module whose workgroup's waves each code <= 8 outputs over all k
     inputs of the same 4 KiB chunk (every input read once, every output
@@ -1461,7 +1491,8 @@ def test_wide_codec_kernels(R, field, k, p, modules):
         assert lib.rse_get_option(6) - n0 == blocks
         from reed_solomon_erasure.core import last_kernel
         if modules == 1:
-            assert last_kernel().startswith(f"bitslice-wide gf{field} {k}+{p}"), last_kernel()
+            kf = 8 if field == 8 or subfield else 16  # every codec here has <= 256 shards
+            assert last_kernel().startswith(f"bitslice-wide gf{kf} {k}+{p}"), last_kernel()
         for i in range(p):
             assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
         assert r.verify(t)
@@ -1605,7 +1636,8 @@ def test_sub_chunk_shards(R, field, k, p, kib):
             got = host(d).reshape(stripes + 1, T, nb)
             assert (got[stripes] == buf.reshape(stripes + 1, T, nb)[stripes]).all()  # guard
             assert (got[:, :k] == buf.reshape(stripes + 1, T, nb)[:, :k]).all()
-            for s_ in sorted({0, 1, stripes // 2, stripes - 2, stripes - 1} - {-1}):
+            for s_ in sorted(x for x in {0, 1, stripes // 2, stripes - 2, stripes - 1}
+                             if 0 <= x < stripes):
                 want = [got[s_, i].copy() for i in range(k)] + [np.zeros(nb, np.uint8)
                                                                for _ in range(p)]
                 oc.encode(want)

@@ -271,3 +271,40 @@ def test_oracle_error_precedence():  # tests/mod.rs:97-116, 1058-1163, macros.rs
         c3.encode_sep(sh[:2], sh[3:])
     with E(6):
         c3.encode_sep(sh[:3], sh[2:])
+
+
+@pytest.mark.parametrize("k,p", [(3, 2), (20, 8), (40, 12), (100, 30), (200, 56)])
+def test_gf16_codecs_of_256_shards_code_in_the_gf8_subfield(k, p):
+    """rse_codec.cpp kfield / RSE_OPT_SUBFIELD: a GF(2^16) codec of at most
+    256 shards has every encoding-matrix entry in the GF(2^8) subfield (its
+    Vandermonde points 0..k+p-1 are, galois_16.rs:97-107), equal to the
+    GF(2^8) codec's matrix; a subfield constant multiplies each byte of an
+    element on its own (galois_16.rs:20-52), so encode and every decode
+    pattern give the GF(2^8) codec's bytes.  Checked on the oracle (the
+    restatement of the reference): matrices, multiplication by every subfield
+    constant, encode and a reconstruct."""
+    m16, m8 = O.Codec(16, k, p).matrix(), O.Codec(8, k, p).matrix()
+    assert (m16[..., 0] == 0).all() and (m16[..., 1] == m8).all()
+    rng = np.random.default_rng(k * 7 + p)
+    for c in range(256):
+        a = tuple(int(x) for x in rng.integers(0, 256, 2))
+        assert O.gf16_mul((0, c), a) == (O.gf8_mul(c, a[0]), O.gf8_mul(c, a[1]))
+    n = 64
+    s16 = [rng.integers(0, 256, 2 * n, dtype=np.uint8) for _ in range(k)] + \
+          [np.zeros(2 * n, np.uint8) for _ in range(p)]
+    s8 = [x.copy() for x in s16]
+    O.Codec(16, k, p).encode(s16)
+    O.Codec(8, k, p).encode(s8)
+    for i in range(k, k + p):
+        assert (s16[i] == s8[i]).all(), i
+    lost = sorted(rng.choice(k + p, p, replace=False).tolist())
+    r16 = [np.zeros(2 * n, np.uint8) if i in lost else s16[i].copy() for i in range(k + p)]
+    O.Codec(16, k, p).reconstruct(r16, [i not in lost for i in range(k + p)])
+    for i in lost:
+        assert (r16[i] == s8[i]).all(), i
+
+
+def test_gf16_codecs_past_256_shards_leave_the_subfield():
+    """Past 256 shards the Vandermonde points leave GF(2^8): GF(2^16) proper."""
+    m = O.Codec(16, 250, 7).matrix()
+    assert (m[..., 0] != 0).any()
