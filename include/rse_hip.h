@@ -364,13 +364,17 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                         subfield -- every codec of at most 256 shards -- codes
                                         each byte in GF(2^8): the same bytes, half the work;
                                         0: GF(2^16) kernels (A/B) */
+#define RSE_OPT_JIT_MAX_PATTERNS 35  /* decode-pattern modules built per process (default 64);
+                                        past it, patterns run on the syndrome / table kernels */
+#define RSE_OPT_JIT_MAX_PATTERN_BLOCKS 36 /* blocks of wide decode patterns per process (64) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */
 #define RSE_OPT_RECON_PAIRS 28       /* syndrome reconstruct at 8 sigma rows on wave pairs (4 rows
-                                        each, planes shared through LDS, 3 waves per SIMD): 1
-                                        (default) one pair per workgroup with two inputs in flight
-                                        per wave, 2 two pairs per workgroup
+                                        each, planes shared through LDS, 3 waves per SIMD): 8
+                                        (default) by field -- GF(2^8) as 2, GF(2^16) as 1; 1 one
+                                        pair per workgroup with two inputs in flight per wave, 2
+                                        two pairs per workgroup
                                         (compiled codecs; run-time ones use two); 0: one wave holds
                                         all 8 rows; A/B variants of the compiled codecs (one pair):
                                         3 next unit prefetched, 6 compact mixing, 7 one input in

@@ -660,8 +660,15 @@ hipError_t launch_bitslice(int field, const CodeArgs& a, bool nt, int64_t grid,
 // the pair only: 4.26 TB/s at 8 lost against 4.18 for two pairs per
 // workgroup, profiles/r03/s3/r8.log), 2 two pairs; returns pairs per
 // workgroup (0: off).  3-6: one pair per workgroup, A/B variants (pair_slot).
-int pair_groups() {
+// 8 (the default): by field -- GF(2^8) two pairs per workgroup (20+8 x 4 MiB
+// at 8 lost, 256 stripes: 4.96 TB/s against 4.73 for the depth-2 pair and
+// 4.79 for round 3's, profiles/r04/s8/r8ab.log), GF(2^16) the depth-2 pair.
+int64_t pair_option(int field) {
   const int64_t o = get_option(28);
+  return o == 8 ? (field == 8 ? 2 : 1) : o;
+}
+int pair_groups(int field) {
+  const int64_t o = pair_option(field);
   return o == 0 ? 0 : o == 2 ? 2 : 1;
 }
 // RSE_OPT_RECON_DEPTH (inputs in flight per lane in the syndrome kernels).  The
@@ -679,9 +686,9 @@ int recon_depth(int mix) {
 // (Two own inputs in flight per wave, the default since round 4: GF(2^16) 20+8
 // x 4 MiB at 8 lost 4.37 against 4.25 TB/s at 128 stripes, 4.45 against 4.38
 // at 256, reconstruct_batch 8 erasures 2.77 against 2.73; profiles/r04/s4/.)
-int pair_slot() {
-  const int64_t o = get_option(28);
-  return o >= 3 && o <= 7 ? (int)o - 1 : pair_groups() - 1;
+int pair_slot(int field) {
+  const int64_t o = pair_option(field);
+  return o >= 3 && o <= 7 ? (int)o - 1 : pair_groups(field) - 1;
 }
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
@@ -714,16 +721,16 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const int depth = recon_depth(mix);
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
     // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
-    const int np = pair_groups();
-    if (slot == 3 && np && sh.rec_pair[pair_slot()] && mix >= kReconMixHorner && depth == 1) {
-      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d s%d", field, k, p, np, pair_slot());
+    const int np = pair_groups(field);
+    if (slot == 3 && np && sh.rec_pair[pair_slot(field)] && mix >= kReconMixHorner && depth == 1) {
+      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d s%d", field, k, p, np, pair_slot(field));
       // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
       // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
       uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);
       const uint64_t units = total * (4 / np);
       if (gp > units) gp = units;
       if (gp > 0x7fffffffu) gp = 0x7fffffffu;
-      hipLaunchKernelGGL(sh.rec_pair[pair_slot()], dim3((uint32_t)gp), dim3(128 * np), 0, stream,
+      hipLaunchKernelGGL(sh.rec_pair[pair_slot(field)], dim3((uint32_t)gp), dim3(128 * np), 0, stream,
                          a, cps);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -784,12 +791,12 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
       if (sh.rec_desc[q] && (1u << q) >= need) {
         sfn = depth > 1 ? sh.rec_desc_deep[depth > 2 ? 1 : 0][q] : sh.rec_desc[q];
         sfn4 = sh.rec_desc4[q];
-        if (q == 3 && pair_groups() && sh.rec_desc_pair[pair_slot()] && depth == 1) {
-          sfn = sh.rec_desc_pair[pair_slot()];  // 8 sigma rows on wave pairs
+        if (q == 3 && pair_groups(field) && sh.rec_desc_pair[pair_slot(field)] && depth == 1) {
+          sfn = sh.rec_desc_pair[pair_slot(field)];  // 8 sigma rows on wave pairs
           pairs = true;
         }
         if (pairs)
-          note_kernel("bitslice-recon-batch gf%d %u+%u ns8 pairs%d", field, k, p, pair_groups());
+          note_kernel("bitslice-recon-batch gf%d %u+%u ns8 pairs%d", field, k, p, pair_groups(field));
         else
           note_kernel("bitslice-recon-batch gf%d %u+%u ns%d d%d", field, k, p, 1 << q,
                       depth > 3 ? 3 : depth < 1 ? 1 : depth);
@@ -816,7 +823,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   if (e != hipSuccess) return e;
   const int64_t grid = get_option(2);
   auto grid_for = [&](uint64_t steps) {
-    uint64_t gx = grid > 0 ? (uint64_t)grid : pairs ? 32768u * (2 / pair_groups()) : 8192u;
+    uint64_t gx = grid > 0 ? (uint64_t)grid : pairs ? 32768u * (2 / pair_groups(field)) : 8192u;
     if (gx > steps) gx = steps;
     return gx > 0x7fffffffu ? (uint64_t)0x7fffffffu : gx;
   };
@@ -824,7 +831,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   uint64_t cps = shard_bytes / kBsChunk, ns = n_stripes;
   uint64_t cps4 = (shard_bytes - cps * kBsChunk) / 4096u, base4 = cps * kBsChunk;
   if (cps) {
-    const int np = pairs ? pair_groups() : 2;
+    const int np = pairs ? pair_groups(field) : 2;
     const uint64_t gx = grid_for(cps * ns * (pairs ? 4 / np : 1));
     if (sfn) {
       hipLaunchKernelGGL(sfn, dim3((uint32_t)gx), dim3(pairs ? 128 * np : kBsBlock), 0, stream,

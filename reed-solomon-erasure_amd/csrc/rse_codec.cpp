@@ -731,16 +731,16 @@ int decode_matrix(const rse_codec* c, const std::vector<size_t>& valid,
   *uses = 1;
   const size_t k = c->k;
   bool ok;
-  if (c->field == 16) {
+  if (c->kfield == 16) {
     rse::Matrix<rse::Gf16Field> sub(k, k), inv;
     for (size_t r = 0; r < k; ++r)
       for (size_t j = 0; j < k; ++j) sub.at(r, j) = c->m16.at(valid[r], j);
     ok = sub.invert(inv);
     out = inv.d;
-  } else {
+  } else {  // GF(2^8), or a GF(2^16) codec in the subfield (kfield): the same inverse
     rse::Matrix<rse::Gf8Field> sub(k, k), inv;
     for (size_t r = 0; r < k; ++r)
-      for (size_t j = 0; j < k; ++j) sub.at(r, j) = c->m8.at(valid[r], j);
+      for (size_t j = 0; j < k; ++j) sub.at(r, j) = c->mat(valid[r], j);
     ok = sub.invert(inv);
     out = inv.d;
   }

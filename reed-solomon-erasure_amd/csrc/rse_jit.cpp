@@ -102,14 +102,16 @@ int queue_of(const Entry& e, int stage) {
   return (e.kind == kJitBlock || e.kind == kJitBlockAcc || e.kind == kJitWide) ? kBlkQueue : stage;
 }
 std::atomic<int64_t> g_built{0};
-int g_patterns = 0;  // decode-pattern entries (capped: kMaxPatterns)
-constexpr int kMaxPatterns = 64;
+int g_patterns = 0;  // decode-pattern entries (capped: max_patterns)
+// per process: RSE_OPT_JIT_MAX_PATTERNS (default 64) decode-pattern modules,
+// RSE_OPT_JIT_MAX_PATTERN_BLOCKS (64) blocks of wide decode patterns
+int max_patterns() { return (int)std::min<int64_t>(get_option(35), 1 << 30); }
+int max_pattern_blocks() { return (int)std::min<int64_t>(get_option(36), 1 << 30); }
 int g_blocks = 0;  // wide-codec block entries (capped: kMaxBlocks)
 constexpr int kMaxBlocks = 256;
 // blocks of wide decode patterns: a separate budget, so patterns can never
 // use up the codecs' own (and never queue more than a few patterns' builds)
 int g_pattern_blocks = 0;
-constexpr int kMaxPatternBlocks = 64;
 constexpr int kMaxPendingPatternBlocks = 16;
 int g_pending_pattern_blocks = 0;  // queued, not yet built
 constexpr size_t kMaxPendingPatternJobs = 8;
@@ -748,7 +750,7 @@ int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKin
   // decode patterns are an optimisation: never queue without bound -- except
   // under RSE_OPT_JIT 2, where the caller waits for this very build
   if (kind == kJitPattern &&
-      (g_patterns >= kMaxPatterns ||
+      (g_patterns >= max_patterns() ||
        (get_option(9) < 2 && g_jobs[kEnc].size() >= kMaxPendingPatternJobs)))
     return 0;
   if ((kind == kJitBlock || kind == kJitBlockAcc) && g_blocks >= kMaxBlocks) return 0;
@@ -768,7 +770,7 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
     need += !find_locked(field, ni, no, rows + (size_t)o0 * k + i0, k, kind);
   });
   if (need == 0) return 1;
-  if (pattern ? (g_pattern_blocks + need > kMaxPatternBlocks ||
+  if (pattern ? (g_pattern_blocks + need > max_pattern_blocks() ||
                  g_pending_pattern_blocks + need > kMaxPendingPatternBlocks)
               : g_blocks + need > kMaxBlocks)
     return 0;
@@ -799,7 +801,7 @@ int jit_register_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows, b
   std::lock_guard<std::mutex> g(g_mu);
   if (find_locked(field, k, p, rows, k, kJitWide)) return 1;
   const int cost = (int)(((k + kMaxIn - 1) / kMaxIn) * ((p + kJitMaxOut - 1) / kJitMaxOut));
-  if (pattern ? (g_pattern_blocks + cost > kMaxPatternBlocks ||
+  if (pattern ? (g_pattern_blocks + cost > max_pattern_blocks() ||
                  g_pending_pattern_blocks + 1 > kMaxPendingPatternBlocks)
               : g_blocks + cost > kMaxBlocks)
     return 0;

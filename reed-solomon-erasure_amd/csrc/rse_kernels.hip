@@ -787,13 +787,15 @@ struct Options {
   int64_t jit_exact = 1;          // run-time networks: exact-decomposition temporaries
   int64_t wide_depth = 1;         // wide modules: inputs in flight per wave (1..4)
   int64_t recon_depth = 1;        // syndrome reconstruct: inputs in flight per lane (1..4)
-  int64_t recon_pairs = 1;        // syndrome reconstruct at 8 sigma rows on wave pairs
+  int64_t recon_pairs = 8;        // syndrome reconstruct at 8 sigma rows on wave pairs (8: by field)
   int64_t wide_pairs = 1;         // wide GF(2^8) modules: networks over pairs of inputs
   int64_t sync_event = 0;         // verify calls wait on an event, not the stream (A/B)
   int64_t spin_wait = 1;          // one-launch verifies: poll the completion word (A/B)
   int64_t host_direct = 1;        // small one-stripe host calls: one staging buffer (A/B)
   int64_t sub_chunks = 1;         // 1 / 2 KiB shards on the bit-sliced kernels (A/B)
   int64_t subfield = 1;           // GF(2^16) codecs of <= 256 shards code in GF(2^8) (A/B)
+  int64_t jit_max_patterns = 64;  // decode-pattern modules per process
+  int64_t jit_max_pattern_blocks = 64;  // blocks of wide decode patterns per process
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1279,13 +1281,15 @@ int set_option(int key, int64_t value) {
     case 23: g_opt.jit_exact = value ? 1 : 0; return 0;
     case 26: g_opt.wide_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 27: g_opt.recon_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
-    case 28: g_opt.recon_pairs = value < 0 ? 0 : value > 7 ? 7 : value; return 0;
+    case 28: g_opt.recon_pairs = value < 0 ? 0 : value > 8 ? 8 : value; return 0;
     case 29: g_opt.wide_pairs = value ? 1 : 0; return 0;
     case 30: g_opt.sync_event = value ? 1 : 0; return 0;
     case 31: g_opt.spin_wait = value ? 1 : 0; return 0;
     case 32: g_opt.host_direct = value ? 1 : 0; return 0;
     case 33: g_opt.sub_chunks = value ? 1 : 0; return 0;
     case 34: g_opt.subfield = value ? 1 : 0; return 0;
+    case 35: g_opt.jit_max_patterns = value < 0 ? 0 : value; return 0;
+    case 36: g_opt.jit_max_pattern_blocks = value < 0 ? 0 : value; return 0;
     default: return -1;
   }
 }
@@ -1332,6 +1336,8 @@ int64_t get_option(int key) {
     case 32: return g_opt.host_direct;
     case 33: return g_opt.sub_chunks;
     case 34: return g_opt.subfield;
+    case 35: return g_opt.jit_max_patterns;
+    case 36: return g_opt.jit_max_pattern_blocks;
     default: return -1;
   }
 }

@@ -300,7 +300,7 @@ def test_every_header_option_is_readable():
         assert L.rse_get_option(key) != -1 or name == "RSE_OPT_KERNEL_VARIANT", name
     assert L.rse_get_option(99) == -1
     assert L.rse_set_option(99, 1) != 0
-    want = {"RSE_OPT_RECON_PAIRS": 1, "RSE_OPT_WIDE_PAIRS": 1, "RSE_OPT_SYNC_EVENT": 0,
+    want = {"RSE_OPT_RECON_PAIRS": 8, "RSE_OPT_WIDE_PAIRS": 1, "RSE_OPT_SYNC_EVENT": 0,
             "RSE_OPT_SPIN_WAIT": 1, "RSE_OPT_HOST_DIRECT": 1}
     for name, v in want.items():
         assert L.rse_get_option(keys[name]) == v, name
