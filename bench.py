@@ -613,7 +613,7 @@ def digests_ok(v, shards, want):
 
 
 def reconstruct_leg(r, v, k, erased, elems, n_stripes, stream, fill, stripe_ids,
-                    want_digests=None, reps=5):
+                    want_digests=None, reps=5, warm_s=0.0):
     """reconstruct_data_flat of `n_stripes` stripes of the view v with data
     shards `erased` lost (one shared pattern, core.rs:680-695), timed; the
     erased shards are poisoned before the timed calls and checked after them:
@@ -626,7 +626,7 @@ def reconstruct_leg(r, v, k, erased, elems, n_stripes, stream, fill, stripe_ids,
         fill = v[:n_stripes, list(erased)].clone()
     gbps = timed_gbps(lambda: r.reconstruct_data_flat(flat, elems, n_stripes, present),
                       n_stripes * (k + len(erased)) * v.shape[-1], stream, reps=reps,
-                      prepare=lambda: poison(v, n_stripes, erased))
+                      prepare=lambda: poison(v, n_stripes, erased), warm_s=warm_s)
     out = {"GB_per_s": gbps,
            "rebuilt_ok_all_stripes": rebuilt_ok(v, n_stripes, erased, stripe_ids, fill)}
     if want_digests is not None:
@@ -739,14 +739,16 @@ def other_configs(stream):
             digests_ok(v, range(k, T), fs["parity_sha256"])
         if field == 16:
             # first uses of an erasure pattern (syndrome kernels, no decode-
-            # pattern kernel): 8 data shards lost (bit-sliced mixing) and 4
+            # pattern kernel): 8 data shards lost (bit-sliced mixing) and 4;
+            # timed as the wide legs: 0.25 s of untimed calls, then 10
+            d["reconstruct_timing"] = "0.25 s of untimed calls, then 10 back to back (HIP events)"
             ids = list(range(stripes))
             for lost in (8, 4):
                 erased = list(range(lost))
                 lib.rse_set_option(11, 0)
                 try:
                     leg = reconstruct_leg(r, v, k, erased, elems, stripes, stream, fill_splitmix,
-                                          ids, fs["data_sha256"][:lost])
+                                          ids, fs["data_sha256"][:lost], reps=10, warm_s=0.25)
                 finally:
                     lib.rse_set_option(11, 1)
                 d[f"reconstruct_{lost}_erased_syndrome_GB_per_s"] = leg["GB_per_s"]
@@ -756,7 +758,8 @@ def other_configs(stream):
             lib.rse_set_option(9, 2)
             try:
                 leg = reconstruct_leg(r, v, k, [0, 1, 2, 3], elems, stripes, stream,
-                                      fill_splitmix, ids, fs["data_sha256"][:4])
+                                      fill_splitmix, ids, fs["data_sha256"][:4], reps=10,
+                                      warm_s=0.25)
             finally:
                 lib.rse_set_option(9, old)
             d["reconstruct_4_erased_cached_pattern_GB_per_s"] = leg["GB_per_s"]

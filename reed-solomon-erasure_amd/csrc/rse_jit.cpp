@@ -63,6 +63,7 @@ struct Compiled {
   std::string code;  // gfx950 code object
   std::string log;
   double ms = 0;
+  int wide_w = 0;  // kJitWide: waves per workgroup the module was generated for
 };
 
 // Two modules per codec, built in this order: the encode/verify kernel
@@ -195,8 +196,8 @@ int wide_waves_per_eu(uint32_t) {
   const int64_t o = get_option(20);  // RSE_OPT_WIDE_OCCUPANCY
   return o ? (int)o : 2;
 }
-void wide_share(uint32_t p, int w, uint32_t* o0, uint32_t* n) {
-  const uint32_t W = (uint32_t)wide_waves(p), base = p / W, extra = p % W;
+void wide_share(uint32_t p, int W_, int w, uint32_t* o0, uint32_t* n) {
+  const uint32_t W = (uint32_t)W_, base = p / W, extra = p % W;
   *o0 = w * base + std::min<uint32_t>(w, extra);
   *n = base + (w < (int)extra ? 1u : 0u);
 }
@@ -204,7 +205,7 @@ void wide_share(uint32_t p, int w, uint32_t* o0, uint32_t* n) {
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage, JitKind kind) {
+                        int stage, JitKind kind, int* wide_w = nullptr) {
   std::string s;
   s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * (field == 16 ? 16 : 8));
   // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
@@ -215,15 +216,17 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
        "using __hip_internal::int32_t;\n";
   s += kJitSource;
   if (kind == kJitWide) {
-    // one code struct per wave's share of the outputs, and the kernel
+    // one code struct per wave's share of the outputs, and the kernel (the
+    // launch takes W from the build: the options may change meanwhile)
     const int W = wide_waves(p);
+    if (wide_w) *wide_w = W;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS
     // kernels code a round's inputs two at a time, so W must be even
     const bool pairs = field == 8 && shared && W % 2 == 0 && get_option(29) != 0;
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
-      wide_share(p, w, &o0, &n);
+      wide_share(p, W, w, &o0, &n);
       std::vector<uint16_t> sub(rows.begin() + (size_t)o0 * k, rows.begin() + (size_t)(o0 + n) * k);
       char name[32];
       std::snprintf(name, sizeof name, "JitWide%d", w);
@@ -254,7 +257,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       s += buf;
       for (int w = 0; w < W; ++w) {
         uint32_t o0, n;
-        wide_share(p, w, &o0, &n);
+        wide_share(p, W, w, &o0, &n);
         if (shared)
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d, "
@@ -553,7 +556,7 @@ void build_in_process(const std::string& src, Compiled* out) {
 
 std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
   auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind);
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w);
   const auto t0 = std::chrono::steady_clock::now();
   const std::string key = hash_key(src);
   const bool disk = get_option(15) != 0 && !cache_dir().empty();
@@ -887,12 +890,13 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   uint64_t gx = grid > 0 ? (uint64_t)grid : field == 16 ? 16384u : 8192u;
   if (gx > total) gx = total;
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+  const int W = c->wide_w;  // the module's own workgroup shape
   if (subq)
-    note_kernel("bitslice-wide gf%d %u+%u w%d sub%d", field, k, p, wide_waves(p), subq);
+    note_kernel("bitslice-wide gf%d %u+%u w%d sub%d", field, k, p, W, subq);
   else
-    note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, wide_waves(p));
-  he = hipModuleLaunchKernel(fn, (uint32_t)gx, 1, 1, 64u * (uint32_t)wide_waves(p), 1, 1, 0,
-                             stream, nullptr, extra);
+    note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, W);
+  he = hipModuleLaunchKernel(fn, (uint32_t)gx, 1, 1, 64u * (uint32_t)W, 1, 1, 0, stream, nullptr,
+                             extra);
   if (he != hipSuccess) return he;
   count_bitslice_launch();
   *done = subq ? len : cps * 4096u;

@@ -1177,15 +1177,31 @@ size_t recon_plan_lds(uint32_t k, uint32_t T, uint32_t e_cap, uint32_t nout_cap)
 }
 
 // One lane per stripe: the per-stripe counts of the host loop in
-// rse_reconstruct_batch, reduced over the wave before one atomic each.
+// rse_reconstruct_batch, reduced over the wave before one atomic each.  With
+// at most kScanStageT flags per stripe the workgroup first copies its 256
+// stripes' flags into LDS, consecutive bytes per lane (a lane reading its own
+// stripe's flags from HBM is k + p dependent loads, 28 round trips at 20+8:
+// 39 us for 65536 stripes, profiles/r04/s9/b4k_trace/), then scans from LDS.
+constexpr uint32_t kScanStageT = 128;
 __global__ __launch_bounds__(256) void batch_scan_kernel(const uint8_t* __restrict__ present,
                                                          uint64_t n, uint32_t k, uint32_t p,
                                                          uint32_t data_only, uint32_t* res) {
-  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint8_t fl[256 * kScanStageT];
+  const uint32_t T = k + p;
+  const uint64_t s0 = (uint64_t)blockIdx.x * blockDim.x, s = s0 + threadIdx.x;
+  const bool staged = T <= kScanStageT;
+  if (staged) {
+    const uint64_t rows = n - s0 < 256 ? n - s0 : 256;
+    const uint32_t nb = (uint32_t)(rows * T);
+    const uint8_t* src = present + s0 * T;
+#pragma unroll 8
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) fl[i] = src[i];
+    __syncthreads();
+  }
   uint32_t need = 0, ne = 0, nout = 0;
   unsigned long long err = ~0ull;
   if (s < n) {
-    const uint8_t* pr = present + s * (k + p);
+    const uint8_t* pr = staged ? fl + threadIdx.x * T : present + s * T;
     for (uint32_t j = 0; j < k; ++j) ne += pr[j] ? 0u : 1u;
     uint32_t np = k - ne, nr = 0, nmp = 0;
     for (uint32_t r = 0; r < p; ++r) {
@@ -1206,10 +1222,31 @@ __global__ __launch_bounds__(256) void batch_scan_kernel(const uint8_t* __restri
     const unsigned long long o = __shfl_xor(err, m);
     err = o < err ? o : err;
   }
+  // the workgroup's 4 waves through LDS, then one lane; an atomic only where
+  // it would raise the word (the words agree across most workgroups, and
+  // 4096 atomics on 4 addresses serialise: the scan took 40 us for 65536
+  // stripes with them, profiles/r04/s10/b4k_trace/)
+  __shared__ uint32_t wr[4][3];
+  __shared__ unsigned long long we[4];
+  const uint32_t wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63u) == 0) {
-    if (need) atomicMax(&res[0], need);
-    if (ne) atomicMax(&res[1], ne);
-    if (nout) atomicMax(&res[2], nout);
+    wr[wv][0] = need;
+    wr[wv][1] = ne;
+    wr[wv][2] = nout;
+    we[wv] = err;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64u; ++w) {
+      need = max(need, wr[w][0]);
+      ne = max(ne, wr[w][1]);
+      nout = max(nout, wr[w][2]);
+      err = we[w] < err ? we[w] : err;
+    }
+    const uint32_t v[3] = {need, ne, nout};
+    for (int q = 0; q < 3; ++q)
+      if (v[q] > __hip_atomic_load(&res[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&res[q], v[q]);
     if (err != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(res + 4), err);
   }
 }

@@ -1689,3 +1689,33 @@ def test_sub_chunk_shards(R, field, k, p, kib):
     finally:
         lib.rse_set_option(9, old9)
         lib.rse_set_option(33, old33)
+
+
+def test_wide_launch_follows_the_module_not_the_options(R):
+    """A wide module's workgroup shape is fixed when it is generated
+    (RSE_OPT_WIDE_SPLIT: outputs per wave); changing the option afterwards
+    must not change the launch (a 512-lane launch of a 256-lane module fails
+    to launch).  GF(2^8) 3+30: 4 waves by default, 8 at 4 outputs per wave."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    k, p, n = 3, 30, 3 * 4096 + 16
+    rng = np.random.default_rng(330)
+    oc = O.Codec(8, k, p)
+    full = rand_shards(rng, k, n) + [np.zeros(n, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    old9, old18 = lib.rse_get_option(9), lib.rse_get_option(18)
+    try:
+        lib.rse_set_option(9, 2)
+        r = R.core.ReedSolomon(k, p, 8)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        lib.rse_set_option(18, 4)
+        t = [dev(x) for x in full[:k]] + [torch.zeros(n, dtype=torch.uint8, device="cuda")
+                                          for _ in range(p)]
+        r.encode(t)
+        torch.cuda.synchronize()
+        assert last_kernel().startswith("bitslice-wide gf8 3+30 w4"), last_kernel()
+        for i in range(p):
+            assert (host(t[k + i]) == full[k + i]).all(), i
+    finally:
+        lib.rse_set_option(9, old9)
+        lib.rse_set_option(18, old18)
