@@ -63,7 +63,8 @@ struct Compiled {
   std::string code;  // gfx950 code object
   std::string log;
   double ms = 0;
-  int wide_w = 0;  // kJitWide: waves per workgroup the module was generated for
+  int wide_w = 0;         // kJitWide: waves per workgroup the module was generated for
+  bool wide_sub = false;  // ... and whether it has the 1 / 2 KiB kernels (LDS bodies)
 };
 
 // Two modules per codec, built in this order: the encode/verify kernel
@@ -205,7 +206,8 @@ void wide_share(uint32_t p, int W_, int w, uint32_t* o0, uint32_t* n) {
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage, JitKind kind, int* wide_w = nullptr) {
+                        int stage, JitKind kind, int* wide_w = nullptr,
+                        bool* wide_sub = nullptr) {
   std::string s;
   s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * (field == 16 ? 16 : 8));
   // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
@@ -221,6 +223,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     const int W = wide_waves(p);
     if (wide_w) *wide_w = W;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
+    if (wide_sub) *wide_sub = shared;
     // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS
     // kernels code a round's inputs two at a time, so W must be even
     const bool pairs = field == 8 && shared && W % 2 == 0 && get_option(29) != 0;
@@ -556,7 +559,8 @@ void build_in_process(const std::string& src, Compiled* out) {
 
 std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
   auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w);
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w,
+                                      &out->wide_sub);
   const auto t0 = std::chrono::steady_clock::now();
   const std::string key = hash_key(src);
   const bool disk = get_option(15) != 0 && !cache_dir().empty();
@@ -850,13 +854,12 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
       Entry::Loaded l{dev};
       l.fns.wide = fn;
       // the 1 / 2 KiB kernels exist in modules of the LDS bodies only
-      // (make_source); a missing one is not an error of this call
-      for (int q = 0; q < 2; ++q)
-        if (hipModuleGetFunction(&l.fns.wide_sub[q], m, q ? "rse_jit_wide_s2" : "rse_jit_wide_s1") !=
-            hipSuccess) {
-          l.fns.wide_sub[q] = nullptr;
-          (void)hipGetLastError();
-        }
+      for (int q = 0; q < 2 && c->wide_sub && he == hipSuccess; ++q)
+        he = hipModuleGetFunction(&l.fns.wide_sub[q], m, q ? "rse_jit_wide_s2" : "rse_jit_wide_s1");
+      if (he != hipSuccess) {
+        (void)hipModuleUnload(m);
+        return he;
+      }
       e->loaded.push_back(l);
       have = &e->loaded.back();
     }
