@@ -458,21 +458,32 @@ __device__ __forceinline__ void bitslice_body_deep(const CodeArgs& a, uint64_t c
 // HBM once and served to the other waves by L1/L2); every output is written
 // once.  Lane layout of the 4 KiB chunks: lane l loads vectors l, l+64,
 // l+128, l+192 (each load instruction 1 KiB contiguous per wave).
-template <class C, int O0, class A>
+// SUB: 1 or 2 KiB shards, a chunk = 4096 / SUB consecutive stripes' shards
+// (bitslice_body's SUB).
+template <class C, int O0, class A, uint32_t SUB = 0>
 __device__ __forceinline__ void wide_body(const A& a) {
   const WideHdr& h = a.h;
-  const uint64_t total = h.chunks_per_stripe * h.n_stripes;
-  const uint32_t lane_off = (threadIdx.x & 63u) * 16u;
+  constexpr uint32_t S = SUB ? SUB / 4u : 1024u;
+  constexpr uint32_t SPC = SUB ? 4096u / SUB : 1u, LPS = 64u / SPC;
+  const uint64_t total = SUB ? (h.n_stripes + SPC - 1) / SPC : h.chunks_per_stripe * h.n_stripes;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = (SUB ? lane % LPS : lane) * 16u;
   const uint32_t mode = h.mode;
   bool diff = false;
   for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
-    const uint64_t stripe = c / h.chunks_per_stripe, chunk = c - stripe * h.chunks_per_stripe;
-    const uint64_t off = stripe * h.stripe_stride + chunk * 4096u + lane_off;
+    uint64_t stripe, off;
+    if constexpr (SUB) {
+      stripe = c * SPC + lane / LPS;
+      off = (stripe < h.n_stripes ? stripe : h.n_stripes - 1) * h.stripe_stride + lane_off;
+    } else {
+      stripe = c / h.chunks_per_stripe;
+      off = stripe * h.stripe_stride + (c - stripe * h.chunks_per_stripe) * 4096u + lane_off;
+    }
+    const bool ok = SUB == 0 || stripe < h.n_stripes;  // lanes past the last stripe: no stores
     uint32_t acc[C::p * 16];
     u32x4 cur[4];
-    load4<false, 1024u>(cur, a.in[0] + off);
-    code_inputs<C, false, true, false, 0, 1024u, false, A>(acc, cur, a, off, ~0ull);
-    store_outputs<C, true, false, 1024u, O0, A>(acc, a, off, mode, diff);
+    load4<false, S>(cur, a.in[0] + off);
+    code_inputs<C, false, true, false, 0, S, false, A>(acc, cur, a, off, ~0ull);
+    store_outputs<C, true, false, S, O0, A>(acc, a, off, mode, diff, ok);
     if (h.per_stripe && diff) {
       flag_mismatch(h.mismatch + stripe);
       diff = false;

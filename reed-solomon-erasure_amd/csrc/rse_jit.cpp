@@ -63,8 +63,7 @@ struct Compiled {
   std::string code;  // gfx950 code object
   std::string log;
   double ms = 0;
-  int wide_w = 0;         // kJitWide: waves per workgroup the module was generated for
-  bool wide_sub = false;  // ... and whether it has the 1 / 2 KiB kernels (LDS bodies)
+  int wide_w = 0;  // kJitWide: waves per workgroup the module was generated for
 };
 
 // Two modules per codec, built in this order: the encode/verify kernel
@@ -206,8 +205,7 @@ void wide_share(uint32_t p, int W_, int w, uint32_t* o0, uint32_t* n) {
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage, JitKind kind, int* wide_w = nullptr,
-                        bool* wide_sub = nullptr) {
+                        int stage, JitKind kind, int* wide_w = nullptr) {
   std::string s;
   s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * (field == 16 ? 16 : 8));
   // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
@@ -223,7 +221,6 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     const int W = wide_waves(p);
     if (wide_w) *wide_w = W;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
-    if (wide_sub) *wide_sub = shared;
     // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS
     // kernels code a round's inputs two at a time, so W must be even
     const bool pairs = field == 8 && shared && W % 2 == 0 && get_option(29) != 0;
@@ -246,9 +243,9 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                   "  uint8_t* out[%u];\n  const uint8_t* cmp[%u];\n};\n",
                   k, p, p);
     s += buf;
-    // rse_jit_wide over 4 KiB chunks; with the LDS bodies also _s1 / _s2 over
-    // 1 / 2 KiB shards, 4 / 2 stripes per chunk (wide_body_lds_deep SUB)
-    for (int q = 0; q <= (shared ? 2 : 0); ++q) {
+    // rse_jit_wide over 4 KiB chunks, and _s1 / _s2 over 1 / 2 KiB shards,
+    // 4 / 2 stripes per chunk (the bodies' SUB)
+    for (int q = 0; q <= 2; ++q) {
       std::snprintf(buf, sizeof buf,
                     // at least 2 waves per SIMD (256 VGPRs): __launch_bounds__ of a
                     // 64-thread group would give 64 VGPRs and spill
@@ -268,7 +265,9 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                         w, w, o0, W, w, (int)get_option(26), 1024 * q);
         else
           std::snprintf(buf, sizeof buf,
-                        "    case %d: rse::wide_body<rse::JitWide%d, %u>(a); break;\n", w, w, o0);
+                        "    case %d: rse::wide_body<rse::JitWide%d, %u, WideArgs, %du>(a); "
+                        "break;\n",
+                        w, w, o0, 1024 * q);
         s += buf;
       }
       s += "    default: break;\n  }\n}\n";
@@ -559,8 +558,7 @@ void build_in_process(const std::string& src, Compiled* out) {
 
 std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
   auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w,
-                                      &out->wide_sub);
+  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w);
   const auto t0 = std::chrono::steady_clock::now();
   const std::string key = hash_key(src);
   const bool disk = get_option(15) != 0 && !cache_dir().empty();
@@ -853,8 +851,8 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
       }
       Entry::Loaded l{dev};
       l.fns.wide = fn;
-      // the 1 / 2 KiB kernels exist in modules of the LDS bodies only
-      for (int q = 0; q < 2 && c->wide_sub && he == hipSuccess; ++q)
+      // and the 1 / 2 KiB kernels
+      for (int q = 0; q < 2 && he == hipSuccess; ++q)
         he = hipModuleGetFunction(&l.fns.wide_sub[q], m, q ? "rse_jit_wide_s2" : "rse_jit_wide_s1");
       if (he != hipSuccess) {
         (void)hipModuleUnload(m);
@@ -865,7 +863,6 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
     }
     fn = subq ? have->fns.wide_sub[subq - 1] : have->fns.wide;
   }
-  if (!fn) return hipSuccess;  // no 1 / 2 KiB kernel: the table kernels
   // argument block: header, then the k input, p output and p compare pointers
   std::vector<uint8_t> buf(sizeof(WideHdr) + sizeof(void*) * (k + 2 * (size_t)p), 0);
   WideHdr h{};

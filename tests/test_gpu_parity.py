@@ -1622,7 +1622,8 @@ def test_jit_verify_completion_word(R, k, p):
 @pytest.mark.parametrize("field,k,p", [
     (8, 10, 4), (8, 10, 2), (16, 20, 8),   # compiled codecs
     (8, 4, 4), (8, 8, 8), (8, 5, 2), (16, 6, 3),  # run-time specialised
-    (8, 50, 20), (8, 16, 16), (16, 40, 12),  # wide codecs (one module)
+    (8, 50, 20), (8, 16, 16), (16, 40, 12),  # wide codecs (one module, LDS bodies)
+    (8, 40, 2),                              # wide, one wave (plain body)
 ])
 @pytest.mark.parametrize("kib", [1, 2])
 def test_sub_chunk_shards(R, field, k, p, kib):
