@@ -985,13 +985,14 @@ thread_local int64_t g_host_planned = 0;      // RSE_OPT_HOST_PLANNED_STRIPES
 // instead (jit_register_blocks; run_job launches them once all are ready),
 // when a call codes 1 MiB of every shard or more (each block is seconds of
 // hiprtc; `volume`: the bytes per shard over all stripes of the call).
-// Shards of 16 KiB or more qualify, and of exactly 1 or 2 KiB (bitslice_len:
-// the SUB kernels; at 4-16 KiB the syndrome kernels' 4 KiB chunks serve).
+// Shards of 4 KiB or more qualify, and of exactly 1 or 2 KiB (bitslice_len;
+// the SUB kernels).  Below 16 KiB the syndrome kernels code nothing (16 KiB
+// chunks), so without a pattern kernel such shards run on the table kernels.
 bool pattern_kernel(const rse_codec* c, const ReconPlan& plan, size_t len_bytes,
                     size_t volume = 0) {
   const int64_t mode = rse::get_option(RSE_OPT_JIT);
   if (mode == 0 || !rse::get_option(RSE_OPT_JIT_PATTERNS) || !rse::get_option(RSE_OPT_BITSLICE) ||
-      (len_bytes < rse::bitslice_chunk_bytes() && !(len_bytes < 4096 && bitslice_len(len_bytes))) ||
+      !bitslice_len(len_bytes) ||
       (mode < 2 && plan.pattern_uses < 2))
     return false;
   const uint32_t k = (uint32_t)c->k, n = (uint32_t)plan.rows.n_out;

@@ -1720,3 +1720,56 @@ def test_wide_launch_follows_the_module_not_the_options(R):
     finally:
         lib.rse_set_option(9, old9)
         lib.rse_set_option(18, old18)
+
+
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 20, 8), (8, 6, 3)])
+@pytest.mark.parametrize("nbytes", [4096, 8192 + 32, 12288])
+def test_pattern_kernels_below_16_kib(R, field, k, p, nbytes):
+    """Shards of 4 to 16 KiB: the syndrome kernels take 16 KiB chunks only, so
+    a repeated pattern gets its own kernel (4 KiB chunks, one per wave) here
+    too (RSE_OPT_JIT 2: built on first use); reconstruct, reconstruct_data
+    and the flat form against the oracle, each a pattern launch."""
+    lib = R._lib.load()
+    es = field // 8
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(nbytes + k + field)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    erased = [0, k - 1] + ([k] if p > 2 else [])
+    present = [i not in erased for i in range(k + p)]
+    old = lib.rse_get_option(9)
+    try:
+        lib.rse_set_option(9, 2)
+        r = R.core.ReedSolomon(k, p, field)
+        for data_only in (False, True):
+            tb = [dev(x).reshape(shape) for x in full]
+            for e in erased:
+                tb[e].fill_(0x6B)
+            n0 = lib.rse_get_option(12)
+            (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+            torch.cuda.synchronize()
+            assert lib.rse_get_option(12) - n0 == 1, data_only
+            for i in range(k + p):
+                got = host(tb[i]).reshape(-1)
+                if data_only and i >= k and i in erased:
+                    assert (got == 0x6B).all()
+                else:
+                    assert (got == full[i]).all(), (data_only, i)
+        stripes = 5
+        buf = np.concatenate([np.concatenate(full)] * stripes)
+        d = dev(buf)
+        v = d.view(stripes, k + p, nbytes)
+        for e in erased:
+            v[:, e].fill_(0)
+        n0 = lib.rse_get_option(12)
+        r.reconstruct_data_flat(d, n_elems, stripes, present)
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(12) - n0 == 1
+        got = host(d).reshape(stripes, k + p, nbytes)
+        for s_ in range(stripes):
+            for i in range(k):
+                assert (got[s_, i] == full[i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old)
