@@ -179,6 +179,12 @@ __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_desc_
   bitslice_recon_desc_body_w4<C, true, NS>(descs, cps4, n_stripes, base);
 }
 
+template <class C, int NS>
+__global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_w4_kernel(
+    const BsReconArgs a, uint64_t cps4, uint64_t base) {
+  bitslice_recon_body_w4<C, true, NS>(a, cps4, base);
+}
+
 // The same with D inputs in flight per lane (RSE_OPT_RECON_DEPTH; Horner mixing).
 template <class C, int NS, int D>
 __global__ __launch_bounds__(kBsBlock, NS > 4 ? 2 : 3) void bitslice_recon_deep_kernel(
@@ -381,6 +387,7 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
 using BsRecFn = void (*)(const BsReconArgs, uint64_t);
 using BsDescFn = void (*)(const BsReconArgs*, uint64_t, uint64_t);
 using BsDesc4Fn = void (*)(const BsReconArgs*, uint64_t, uint64_t, uint64_t);
+using BsRec4Fn = void (*)(const BsReconArgs, uint64_t, uint64_t);
 
 using BsFn = void (*)(const CodeArgs, uint64_t);
 struct BsShape {
@@ -400,6 +407,7 @@ struct BsShape {
                       // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
+  BsRec4Fn rec4[4];            // rec's Horner mode over 4 KiB chunks, one per wave
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
   BsRecFn rec_pair[7];         // NS = 8 on wave pairs (nullptr below 8 rows), by pair_slot:
@@ -423,6 +431,11 @@ constexpr BsDescFn rec_desc_fn() {
 template <class C, int NS>
 constexpr BsDesc4Fn rec_desc4_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_desc_w4_kernel<C, NS>;
+  else return nullptr;
+}
+template <class C, int NS>
+constexpr BsRec4Fn rec4_fn() {
+  if constexpr (NS <= C::p) return bitslice_recon_w4_kernel<C, NS>;
   else return nullptr;
 }
 template <class C, int NS, int D>
@@ -468,6 +481,7 @@ constexpr BsDescFn rec_desc_deep_fn() {
     {rec_fn<C, 1, 3>(), rec_fn<C, 2, 3>(), rec_fn<C, 4, 3>(), rec_fn<C, 8, 3>()}}, \
    {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()},   \
    {rec_desc4_fn<C, 1>(), rec_desc4_fn<C, 2>(), rec_desc4_fn<C, 4>(), rec_desc4_fn<C, 8>()}, \
+   {rec4_fn<C, 1>(), rec4_fn<C, 2>(), rec4_fn<C, 4>(), rec4_fn<C, 8>()},                 \
    {{rec_deep_fn<C, 1, 2>(), rec_deep_fn<C, 2, 2>(), rec_deep_fn<C, 4, 2>(),           \
      rec_deep_fn<C, 8, 2>()},                                                          \
     {rec_deep_fn<C, 1, 3>(), rec_deep_fn<C, 2, 3>(), rec_deep_fn<C, 4, 3>(),           \
@@ -693,12 +707,14 @@ int pair_slot(int field) {
 
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
-                                 bool* handled) {
-  *handled = false;
-  if (!get_option(5) || n_vec < kBsChunk / 16 || a.n_out == 0 || a.n_out > (uint32_t)kMaxOut ||
+                                 uint64_t* done) {
+  *done = 0;
+  if (!get_option(5) || n_vec < 4096u / 16 || a.n_out == 0 || a.n_out > (uint32_t)kMaxOut ||
       (a.present == 0 && a.synd == 0))
     return hipSuccess;
+  // whole 16 KiB chunks, then whole 4 KiB chunks of the rest (one per wave)
   const uint64_t cps = n_vec / (kBsChunk / 16);
+  const uint64_t cps4 = (n_vec * 16u - cps * kBsChunk) / 4096u, base4 = cps * kBsChunk;
   const uint64_t total = cps * a.n_stripes;
   const int64_t grid = get_option(2);
   // tools/tune.py --op reconstruct --patterns 0 sweeps: GF(2^8) 10+4 x 16 MiB at
@@ -707,6 +723,12 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
   uint64_t gx = grid > 0 ? (uint64_t)grid : (field == 8 ? 32768u : 8192u);
   if (gx > total) gx = total;
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
+  auto grid4 = [&]() {  // the 4 KiB chunks: four per workgroup step
+    uint64_t g4 = grid > 0 ? (uint64_t)grid : 8192u;
+    const uint64_t steps = (cps4 * a.n_stripes + 3) / 4;
+    if (g4 > steps) g4 = steps;
+    return g4 > 0x7fffffffu ? (uint64_t)0x7fffffffu : g4;
+  };
   // rows needed: sigma (R and missing parity); NS = smallest compiled cover
   const uint32_t need = 32u - (uint32_t)__builtin_clz(a.sigma | 1u);
   for (const BsShape& sh : kBsShapes) {
@@ -720,32 +742,41 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     const int mix = (int)get_option(17);
     const int depth = recon_depth(mix);
     static const char* const kMixName[4] = {"mix-tables", "mix-chain", "mix-horner", "mix-horner4"};
-    // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
-    const int np = pair_groups(field);
-    if (slot == 3 && np && sh.rec_pair[pair_slot(field)] && mix >= kReconMixHorner && depth == 1) {
-      note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d s%d", field, k, p, np, pair_slot(field));
-      // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
-      // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
-      uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);
-      const uint64_t units = total * (4 / np);
-      if (gp > units) gp = units;
-      if (gp > 0x7fffffffu) gp = 0x7fffffffu;
-      hipLaunchKernelGGL(sh.rec_pair[pair_slot(field)], dim3((uint32_t)gp), dim3(128 * np), 0, stream,
-                         a, cps);
-      hipError_t e = hipGetLastError();
+    if (cps) {
+      // 8 sigma rows: wave pairs (RSE_OPT_RECON_PAIRS; Horner mixing), 8 KiB units
+      const int np = pair_groups(field);
+      if (slot == 3 && np && sh.rec_pair[pair_slot(field)] && mix >= kReconMixHorner &&
+          depth == 1) {
+        note_kernel("bitslice-recon gf%d %u+%u ns8 pairs%d s%d", field, k, p, np,
+                    pair_slot(field));
+        // (tools/tune.py, two pairs per workgroup: 32768 workgroups 4.24 TB/s, 8192
+        // 4.16, 4096 4.10 at 8 lost; one pair: twice the workgroups)
+        uint64_t gp = grid > 0 ? (uint64_t)grid : 32768u * (2 / np);
+        const uint64_t units = total * (4 / np);
+        if (gp > units) gp = units;
+        if (gp > 0x7fffffffu) gp = 0x7fffffffu;
+        hipLaunchKernelGGL(sh.rec_pair[pair_slot(field)], dim3((uint32_t)gp), dim3(128 * np), 0,
+                           stream, a, cps);
+      } else {
+        note_kernel("bitslice-recon gf%d %u+%u ns%d %s d%d", field, k, p, 1 << slot,
+                    kMixName[mix], depth > 3 ? 3 : depth);
+        BsRecFn fn = depth > 1 ? sh.rec_deep[depth > 2 ? 1 : 0][slot] : sh.rec[mix][slot];
+        hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
+      }
+      const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       count_bitslice_launch();
-      *handled = true;
-      return hipSuccess;
+      *done = base4;
     }
-    note_kernel("bitslice-recon gf%d %u+%u ns%d %s d%d", field, k, p, 1 << slot, kMixName[mix],
-                depth > 3 ? 3 : depth);
-    BsRecFn fn = depth > 1 ? sh.rec_deep[depth > 2 ? 1 : 0][slot] : sh.rec[mix][slot];
-    hipLaunchKernelGGL(fn, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream, a, cps);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    count_bitslice_launch();
-    *handled = true;
+    if (cps4 && sh.rec4[slot]) {
+      if (!cps) note_kernel("bitslice-recon gf%d %u+%u ns%d w4", field, k, p, 1 << slot);
+      hipLaunchKernelGGL(sh.rec4[slot], dim3((uint32_t)grid4()), dim3(kBsBlock), 0, stream, a,
+                         cps4, base4);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      if (!cps) count_bitslice_launch();
+      *done = base4 + cps4 * 4096u;
+    }
     return hipSuccess;
   }
   JitFns jf;
@@ -755,14 +786,26 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
   for (int q = 0; q < jf.n_rec && slot < 0; ++q)
     if ((uint32_t)jf.rec_ns[q] >= need) slot = q;
   if (slot < 0) return hipSuccess;
-  uint64_t cps_arg = cps;
-  note_kernel("bitslice-jit-recon gf%d %u+%u ns%d", field, k, p, jf.rec_ns[slot]);
-  void* args[] = {const_cast<BsReconArgs*>(&a), &cps_arg};
-  e = hipModuleLaunchKernel(jf.rec[slot], (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args,
-                            nullptr);
-  if (e != hipSuccess) return e;
-  count_bitslice_launch();
-  *handled = true;
+  if (cps) {
+    uint64_t cps_arg = cps;
+    note_kernel("bitslice-jit-recon gf%d %u+%u ns%d", field, k, p, jf.rec_ns[slot]);
+    void* args[] = {const_cast<BsReconArgs*>(&a), &cps_arg};
+    e = hipModuleLaunchKernel(jf.rec[slot], (uint32_t)gx, 1, 1, kBsBlock, 1, 1, 0, stream, args,
+                              nullptr);
+    if (e != hipSuccess) return e;
+    count_bitslice_launch();
+    *done = base4;
+  }
+  if (cps4 && jf.rec4[slot]) {
+    if (!cps) note_kernel("bitslice-jit-recon gf%d %u+%u ns%d w4", field, k, p, jf.rec_ns[slot]);
+    uint64_t c4 = cps4, b4 = base4;
+    void* args[] = {const_cast<BsReconArgs*>(&a), &c4, &b4};
+    e = hipModuleLaunchKernel(jf.rec4[slot], (uint32_t)grid4(), 1, 1, kBsBlock, 1, 1, 0, stream,
+                              args, nullptr);
+    if (e != hipSuccess) return e;
+    if (!cps) count_bitslice_launch();
+    *done = base4 + cps4 * 4096u;
+  }
   return hipSuccess;
 }
 

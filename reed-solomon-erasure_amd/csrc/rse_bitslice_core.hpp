@@ -1307,6 +1307,23 @@ __device__ __forceinline__ void bitslice_recon_body(const BsReconArgs& a,
   }
 }
 
+// bitslice_recon_body (one erasure pattern for every stripe) over whole 4 KiB
+// chunks, one per wave, from byte `base` of every shard on: shards of 4 to 16
+// KiB, and the rest of longer ones past their 16 KiB chunks.  chunks_per_stripe
+// counts 4 KiB chunks.  Horner mixing.
+template <class C, bool NT, int NS>
+__device__ __forceinline__ void bitslice_recon_body_w4(const BsReconArgs& a,
+                                                       uint64_t chunks_per_stripe, uint64_t base) {
+  const uint64_t total = chunks_per_stripe * a.n_stripes;
+  const uint32_t sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const uint32_t lane_off = (threadIdx.x & 63u) * 16u;
+  for (uint64_t idx = (uint64_t)blockIdx.x * 4 + sub; idx < total; idx += (uint64_t)gridDim.x * 4) {
+    const uint64_t stripe = idx / chunks_per_stripe, chunk = idx - stripe * chunks_per_stripe;
+    recon_chunk<C, NT, NS, kReconMixHorner, 1024u>(
+        a, nullptr, nullptr, stripe * a.stripe_stride + base + chunk * 4096u + lane_off);
+  }
+}
+
 // bitslice_recon_desc_body over whole 4 KiB chunks, one per wave (lane l
 // codes vectors l, l + 64, l + 128, l + 192 of its wave's chunk), for shards
 // -- or the rest of shards past their 16 KiB chunks, from byte `base` on --

@@ -872,9 +872,8 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
                          size_t n_stripes, hipStream_t s, size_t* done) {
   *done = 0;
   const size_t k = c->k, p = c->p;
-  const uint64_t cb = rse::bitslice_chunk_bytes();
   want_bitslice(c, len_bytes);
-  if (k > (size_t)kMaxIn || p > (size_t)kMaxOut || len_bytes < cb || stripe_stride % 16u ||
+  if (k > (size_t)kMaxIn || p > (size_t)kMaxOut || len_bytes < 4096 || stripe_stride % 16u ||
       !rse::get_option(RSE_OPT_BITSLICE))
     return RSE_OK;
   rse::BsReconArgs a;
@@ -953,7 +952,7 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
   std::vector<uint16_t> rows(p * k);
   for (size_t r = 0; r < p; ++r)
     for (size_t j = 0; j < k; ++j) rows[r * k + j] = c->mat(k + r, j);
-  bool handled = false;
+  uint64_t coded = 0;  // bytes of every shard the kernels code (the same for every batch)
   for (size_t s0 = 0; s0 < n_stripes; s0 += 0x7fffffffu) {
     rse::BsReconArgs b = a;
     const size_t cnt = std::min<size_t>(n_stripes - s0, 0x7fffffffu);
@@ -965,10 +964,10 @@ int bitslice_reconstruct(const rse_codec* c, const uint8_t* const* shards, const
       if (b.par[r]) b.par[r] += adv;
     for (uint32_t q = 0; q < b.n_out; ++q) b.out[q] += adv;
     RSE_HIP(rse::launch_bitslice_recon(c->kfield, (uint32_t)k, (uint32_t)p, rows.data(), b,
-                                       len_bytes / 16u, s, &handled));
-    if (!handled) return RSE_OK;  // first batch decides; nothing launched
+                                       len_bytes / 16u, s, &coded));
+    if (!coded) return RSE_OK;  // first batch decides; nothing launched
   }
-  *done = (len_bytes / cb) * cb;
+  *done = coded;
   return RSE_OK;
 }
 

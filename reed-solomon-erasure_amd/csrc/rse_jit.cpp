@@ -364,8 +364,11 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     std::snprintf(buf, sizeof buf,
                   "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon_desc4_%d(\n"
                   "    const rse::BsReconArgs* d, uint64_t cps, uint64_t n, uint64_t base) {\n"
-                  "  rse::bitslice_recon_desc_body_w4<rse::JitCode, true, %d>(d, cps, n, base);\n}\n",
-                  wpe, ns[q], ns[q]);
+                  "  rse::bitslice_recon_desc_body_w4<rse::JitCode, true, %d>(d, cps, n, base);\n}\n"
+                  "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_recon4_%d(\n"
+                  "    const rse::BsReconArgs a, uint64_t cps, uint64_t base) {\n"
+                  "  rse::bitslice_recon_body_w4<rse::JitCode, true, %d>(a, cps, base);\n}\n",
+                  wpe, ns[q], ns[q], wpe, ns[q], ns[q]);
     s += buf;
   }
   return s;
@@ -974,6 +977,9 @@ bool jit_find(int field, uint32_t k, uint32_t p, const uint16_t* rows, size_t st
         if (he != hipSuccess) break;
         std::snprintf(name, sizeof name, "rse_jit_recon_desc4_%d", f.rec_ns[q]);
         he = hipModuleGetFunction(&f.rec_desc4[q], m, name);
+        if (he != hipSuccess) break;
+        std::snprintf(name, sizeof name, "rse_jit_recon4_%d", f.rec_ns[q]);
+        he = hipModuleGetFunction(&f.rec4[q], m, name);
       }
     }
     if (he != hipSuccess) {

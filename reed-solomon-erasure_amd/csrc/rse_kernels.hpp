@@ -236,11 +236,13 @@ uint64_t bitslice_chunk_bytes();
 int bitslice_compiled(int field, uint32_t k, uint32_t p);
 
 // parity_rows: the codec's p x k parity rows (row-major); must equal the
-// compiled (or run-time specialised) ones for *handled to be set.  n_vec:
-// 16-byte vectors per shard.
+// compiled (or run-time specialised) ones for anything to be launched.  n_vec:
+// 16-byte vectors per shard.  *done: the bytes of every shard coded, from 0
+// (whole 16 KiB chunks, then whole 4 KiB chunks of the rest; 0: nothing
+// launched, the caller codes the shards).
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
-                                 bool* handled);
+                                 uint64_t* done);
 
 // rse_reconstruct_batch on the bit-sliced kernels: a device planner writes one
 // BsReconArgs per stripe (its own erasure pattern: partition, e x e syndrome
@@ -341,6 +343,7 @@ struct JitFns {
   hipFunction_t rec[5] = {};    // bitslice reconstruct (BsReconArgs, chunks per stripe)
   hipFunction_t rec_desc[5] = {};  // ... over per-stripe BsReconArgs (descs, cps, n_stripes)
   hipFunction_t rec_desc4[5] = {}; // ... over 4 KiB chunks, one per wave (descs, cps4, n, base)
+  hipFunction_t rec4[5] = {};      // rec over 4 KiB chunks, one per wave (args, cps4, base)
   hipFunction_t wide = nullptr;    // kJitWide: rse_jit_wide (WideArgs)
   hipFunction_t wide_sub[2] = {};  // ... over 1 / 2 KiB shards (rse_jit_wide_s1 / _s2)
 };

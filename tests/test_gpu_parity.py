@@ -1773,3 +1773,67 @@ def test_pattern_kernels_below_16_kib(R, field, k, p, nbytes):
                 assert (got[s_, i] == full[i]).all(), (s_, i)
     finally:
         lib.rse_set_option(9, old)
+
+
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 20, 8), (8, 6, 3)])
+@pytest.mark.parametrize("nbytes", [4096, 8192 + 32, 16384 + 4096 + 48, 2 * 16384 + 3 * 4096])
+@SUBFIELD
+def test_syndrome_reconstruct_4k_chunks(R, subfield, field, k, p, nbytes):
+    """First use of a pattern (no decode-pattern kernels) on shards with whole
+    4 KiB chunks past their 16 KiB ones, or shorter than 16 KiB: the syndrome
+    reconstruct codes those chunks too (one wave each, Horner mixing), the
+    table kernels only the sub-4 KiB tail.  Every erasure count, data and
+    parity, reconstruct and reconstruct_data, one stripe and flat stripes,
+    against the oracle."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    es = field // 8
+    n_elems = nbytes // es
+    shape = (n_elems,) if field == 8 else (n_elems, 2)
+    rng = np.random.default_rng(nbytes * 3 + k + p + field)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    patterns = [sorted(rng.choice(k + p, ne, replace=False).tolist()) for ne in range(1, p + 1)]
+    patterns += [list(range(min(p, k)))]
+    old9, old11 = lib.rse_get_option(9), lib.rse_get_option(11)
+    try:
+        lib.rse_set_option(9, 2)   # run-time codecs built before the first call
+        lib.rse_set_option(11, 0)  # no decode-pattern kernels: the syndrome path
+        r = R.core.ReedSolomon(k, p, field)
+        r.kernel_kind(wait=True)
+        for erased in patterns:
+            present = [i not in erased for i in range(k + p)]
+            for data_only in (False, True):
+                if data_only and all(e >= k for e in erased):
+                    continue
+                tb = [dev(x).reshape(shape) for x in full]
+                for e in erased:
+                    tb[e].fill_(0x3C)
+                n0 = lib.rse_get_option(6)
+                (r.reconstruct_data if data_only else r.reconstruct)(list(zip(tb, present)))
+                torch.cuda.synchronize()
+                assert lib.rse_get_option(6) - n0 == 1, (erased, data_only)
+                if nbytes < 16384:
+                    assert "w4" in last_kernel(), last_kernel()
+                for i in range(k + p):
+                    got = host(tb[i]).reshape(-1)
+                    if data_only and i >= k and i in erased:
+                        assert (got == 0x3C).all()
+                    else:
+                        assert (got == full[i]).all(), (erased, data_only, i)
+        stripes = 3
+        erased = patterns[min(2, len(patterns) - 1)]
+        buf = np.concatenate([np.concatenate(full)] * stripes)
+        d = dev(buf)
+        v = d.view(stripes, k + p, nbytes)
+        for e in erased:
+            v[:, e].fill_(0)
+        r.reconstruct_data_flat(d, n_elems, stripes, [i not in erased for i in range(k + p)])
+        got = host(d).reshape(stripes, k + p, nbytes)
+        for s_ in range(stripes):
+            for i in range(k):
+                assert (got[s_, i] == full[i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old9)
+        lib.rse_set_option(11, old11)
