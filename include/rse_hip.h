@@ -367,6 +367,10 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
 #define RSE_OPT_JIT_MAX_PATTERNS 35  /* decode-pattern modules built per process (default 64);
                                         past it, patterns run on the syndrome / table kernels */
 #define RSE_OPT_JIT_MAX_PATTERN_BLOCKS 36 /* blocks of wide decode patterns per process (64) */
+#define RSE_OPT_RECON_W4_MIN 37      /* a pattern's first use on shards with 4 KiB chunks past their
+                                        16 KiB ones (or shorter than 16 KiB): the syndrome kernels
+                                        code those chunks when k x outputs >= this (default 64;
+                                        GF(2^16) proper always), else the table kernels do */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

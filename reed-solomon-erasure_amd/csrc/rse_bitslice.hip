@@ -705,6 +705,18 @@ int pair_slot(int field) {
   return o >= 3 && o <= 7 ? (int)o - 1 : pair_groups(field) - 1;
 }
 
+// The 4 KiB syndrome chunks against the table kernels over the same bytes
+// (tools/tune.py --op reconstruct --patterns 0 --bitslice 1,0, 16384 stripes,
+// profiles/r04/s14/): GF(2^8) 10+4 x 8 KiB, 2 lost, 5.24 against 5.57 TB/s;
+// 6+3 x 12 KiB, 3 lost, 5.96 both; GF(2^16) 20+8 (subfield) x 4 KiB, 4 lost,
+// 5.24 against 4.68.  The table kernels' work grows with the coefficients
+// (k x outputs); the syndrome kernels' much less: used from
+// RSE_OPT_RECON_W4_MIN coefficients (default 64), and always for GF(2^16)
+// proper, whose table kernels are 2 x 2 blocks of GF(2^8) ones.
+bool recon4_pays(int field, uint32_t k, uint32_t n_out) {
+  return field == 16 || (int64_t)k * n_out >= get_option(37);
+}
+
 hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16_t* parity_rows,
                                  const BsReconArgs& a, uint64_t n_vec, hipStream_t stream,
                                  uint64_t* done) {
@@ -768,7 +780,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
       count_bitslice_launch();
       *done = base4;
     }
-    if (cps4 && sh.rec4[slot]) {
+    if (cps4 && sh.rec4[slot] && recon4_pays(field, k, a.n_out)) {
       if (!cps) note_kernel("bitslice-recon gf%d %u+%u ns%d w4", field, k, p, 1 << slot);
       hipLaunchKernelGGL(sh.rec4[slot], dim3((uint32_t)grid4()), dim3(kBsBlock), 0, stream, a,
                          cps4, base4);
@@ -796,7 +808,7 @@ hipError_t launch_bitslice_recon(int field, uint32_t k, uint32_t p, const uint16
     count_bitslice_launch();
     *done = base4;
   }
-  if (cps4 && jf.rec4[slot]) {
+  if (cps4 && jf.rec4[slot] && recon4_pays(field, k, a.n_out)) {
     if (!cps) note_kernel("bitslice-jit-recon gf%d %u+%u ns%d w4", field, k, p, jf.rec_ns[slot]);
     uint64_t c4 = cps4, b4 = base4;
     void* args[] = {const_cast<BsReconArgs*>(&a), &c4, &b4};

@@ -796,6 +796,7 @@ struct Options {
   int64_t subfield = 1;           // GF(2^16) codecs of <= 256 shards code in GF(2^8) (A/B)
   int64_t jit_max_patterns = 64;  // decode-pattern modules per process
   int64_t jit_max_pattern_blocks = 64;  // blocks of wide decode patterns per process
+  int64_t recon_w4_min = 64;      // 4 KiB syndrome chunks from this many coefficients
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1327,6 +1328,7 @@ int set_option(int key, int64_t value) {
     case 34: g_opt.subfield = value ? 1 : 0; return 0;
     case 35: g_opt.jit_max_patterns = value < 0 ? 0 : value; return 0;
     case 36: g_opt.jit_max_pattern_blocks = value < 0 ? 0 : value; return 0;
+    case 37: g_opt.recon_w4_min = value < 0 ? 0 : value; return 0;
     default: return -1;
   }
 }
@@ -1375,6 +1377,7 @@ int64_t get_option(int key) {
     case 34: return g_opt.subfield;
     case 35: return g_opt.jit_max_patterns;
     case 36: return g_opt.jit_max_pattern_blocks;
+    case 37: return g_opt.recon_w4_min;
     default: return -1;
   }
 }
