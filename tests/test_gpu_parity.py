@@ -1841,10 +1841,11 @@ def test_syndrome_reconstruct_4k_chunks(R, subfield, field, k, p, nbytes):
         if nbytes == 4096 and (field == 8 or subfield):
             for erased, w4 in (([0], k * 1 >= 64), (list(range(p)), k * p >= 64)):
                 tb = [dev(x).reshape(shape) for x in full]
-                n0 = lib.rse_get_option(6)
                 r.reconstruct(list(zip(tb, [i not in erased for i in range(k + p)])))
                 torch.cuda.synchronize()
-                assert lib.rse_get_option(6) - n0 == (1 if w4 else 0), (erased, last_kernel())
+                # (not the launch count: another test's decode-pattern module for
+                # the same rows may serve the table-kernel route bit-sliced)
+                assert ("-recon " in last_kernel()) == w4, (erased, last_kernel())
     finally:
         lib.rse_set_option(9, old9)
         lib.rse_set_option(11, old11)

@@ -10,4 +10,4 @@ bash tools/gpu_session.sh \
  "pytest:900:python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
  "bench:600:python3 -u bench.py" \
  "trace:400:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace -o bench -- python3 bench.py --no-cpu --no-extras --steps 10" \
- "pmc_traffic:600:python3 tools/pmc_traffic.py --tag r04final --steps 5"
+ "pmc_traffic:600:python3 tools/pmc_traffic.py --tag r04final2 --steps 5"
