@@ -4,12 +4,25 @@ import tempfile
 
 import pytest
 
-# Run-time specialised modules go to a fresh on-disk cache per test session
-# (RSE_OPT_JIT_DISK_CACHE), so build counters mean builds and no run reuses
-# another's modules; tests of the cache itself set their own directories.
-os.environ.setdefault("RSE_JIT_CACHE_DIR", tempfile.mkdtemp(prefix="rse_jit_cache_"))
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# Run-time specialised modules go to a fresh on-disk cache per test session
+# (RSE_OPT_JIT_DISK_CACHE), so no run reuses another run's modules; tests of
+# the cache itself set their own directories.  It starts as a copy of the
+# tree's prebuilt cache (tools/prebuild_all.sh: code objects of this source,
+# keyed by a hash of the whole module source, so a stale one is never hit),
+# which spares the GPU box minutes of hiprtc; build counters in the tests
+# count built + cached modules where a codec may be among them.
+if "RSE_JIT_CACHE_DIR" not in os.environ:
+    import shutil
+    _cache = tempfile.mkdtemp(prefix="rse_jit_cache_")
+    _pre = os.path.join(ROOT, "jitcache")
+    if os.path.isdir(_pre):
+        for _f in os.listdir(_pre):
+            if _f.endswith(".co"):
+                shutil.copy(os.path.join(_pre, _f), _cache)
+    os.environ["RSE_JIT_CACHE_DIR"] = _cache
+
 PKG = os.path.join(ROOT, "reed-solomon-erasure_amd")
 for p in (ROOT, PKG):
     if p not in sys.path:

@@ -21,5 +21,5 @@ pat+=(--pattern "16:20:8:4194304:0,1,2,3")  # other_configs gf16_20_8 cached pat
 exec python3 tools/prebuild_jit.py \
   --codec 8:50:20 --codec 16:40:12 --codec 16:100:30 \
   --codec 8:4:4 --codec 8:8:8 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 --codec 8:5:2 \
-  --codec 8:12:4 --codec 16:6:3 --codec 8:6:3 \
+  --codec 8:12:4 --codec 16:6:3 --codec 8:6:3 --codec 8:32:8 --codec 8:17:5 --codec 16:1000:24 \
   "${pat[@]}"
