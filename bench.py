@@ -486,6 +486,7 @@ def main(argv=None):
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             extras["other_configs"] = other_configs(stream)
+            extras["reconstruct_batch_4k"] = batch_leg(stream)
             extras["reference_bench_matrix"] = reference_bench_matrix(stream)
 
     if rank == 0:
@@ -770,6 +771,56 @@ def other_configs(stream):
         torch.cuda.empty_cache()
     out["gf8_50_20"] = wide_config(stream, g, 8, 50, 20)
     out["gf16_40_12"] = wide_config(stream, g, 16, 40, 12)
+    return out
+
+
+def batch_leg(stream, stripes=65536, erasures=4, reps=10):
+    """rse_reconstruct_batch (core.rs:680-923 per stripe, every stripe its own
+    erasure pattern, planned on the device) of GF(2^16) 20+8 x 4 KiB stripes,
+    `erasures` random shards lost per stripe, flags in HBM (read in place).
+    The lost shards are poisoned before the timed calls; afterwards every
+    stripe must equal its encoded bytes again.  GB/s counts the k shards read
+    and the lost ones written per stripe."""
+    import numpy as np
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix, last_kernel
+    k, p, L, field = 20, 8, 4096, 16
+    T = k + p
+    buf = torch.empty(stripes * T * L, dtype=torch.uint8, device="cuda")
+    fill_splitmix(buf, SEED, 0xB4)
+    r = R.core.ReedSolomon(k, p, field)
+    elems = L // 2
+    r.encode_flat(buf, elems, stripes)
+    want = buf.clone()
+    rng = np.random.default_rng(0xB4)
+    lost = np.argsort(rng.random((stripes, T)), axis=1)[:, :erasures]
+    pres = np.ones((stripes, T), bool)
+    np.put_along_axis(pres, lost, False, axis=1)
+    dpres = torch.from_numpy(pres).cuda()
+    v = buf.view(stripes, T, L)
+
+    def poison_lost():
+        v[~dpres] = POISON
+
+    gbps = timed_gbps(lambda: r.reconstruct_batch(buf, elems, stripes, dpres), stripes *
+                      (k + erasures) * L, stream, reps=reps, prepare=poison_lost)
+    out = {"workload": f"gf16 {k}+{p} x 4 KiB, {stripes} stripes, {erasures} random shards lost "
+                       "per stripe, flags in HBM", "GB_per_s": gbps, "kernel": last_kernel(),
+           "rebuilt_ok_all_stripes": bool(torch.equal(buf, want))}
+    # reconstruct_data (core.rs:690): the lost data shards only; stripes that
+    # lost none are left alone, and lost parity keeps its poison
+    miss = (~pres[:, :k]).sum(axis=1)
+    nbytes = int(((miss > 0) * k + miss).sum()) * L
+    out["data_only_GB_per_s"] = timed_gbps(
+        lambda: r.reconstruct_batch(buf, elems, stripes, dpres, data_only=True), nbytes, stream,
+        reps=reps, prepare=poison_lost)
+    dmask = torch.from_numpy(pres).cuda()
+    dmask[:, k:] = True  # parity shards: not compared
+    out["data_only_rebuilt_ok_all_stripes"] = bool(torch.equal(v[~dmask], want.view(
+        stripes, T, L)[~dmask])) and bool(torch.equal(v[:, :k], want.view(stripes, T, L)[:, :k]))
+    del buf, want, v
+    torch.cuda.empty_cache()
     return out
 
 
