@@ -300,13 +300,17 @@ def load_traffic(workload, kernel_id):
     x2 gfx950 correction + WRITE_SIZE) -- only if it was measured on this
     workload AND on the kernel that ran here (rse_last_kernel); else None."""
     best = None
+    lib_sha = library_info().get("sha256")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         try:
             d = json.load(open(path))
         except Exception:
             continue
         if d.get("workload") == workload and d.get("kernel_id") == kernel_id:
-            best = dict(d, file=os.path.relpath(path, ROOT))
+            # a measurement of this very library wins over any other
+            if best is None or d.get("library_sha256") == lib_sha or \
+                    best.get("library_sha256") != lib_sha:
+                best = dict(d, file=os.path.relpath(path, ROOT))
     return best
 
 
