@@ -55,6 +55,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip reconstruct / e2e legs")
+    ap.add_argument("--full-out", default=None,
+                    help="where the full results (every leg) go; default "
+                         "gpurun_out/bench_full_n<N>.json")
     return ap.parse_args(argv)
 
 
@@ -329,6 +332,144 @@ def library_info():
     return out
 
 
+# ------------------------------------------------------ the printed line
+# The driver reads the LAST stdout line and keeps only the tail of stdout
+# (~8 KB), so that line is a compact summary (< LINE_LIMIT bytes): the
+# contract keys, the roofline, the CPU baseline and one number per extra leg.
+# Every leg in full goes to a JSON file named on the line (`full_results`).
+LINE_LIMIT = 4000
+# booleans in the full results that are descriptions, not correctness flags
+NOT_FLAGS = {"higher_is_better", "distinct_gpus", "rehearsal", "build_info_matches",
+             "pattern_kernel"}
+
+
+def _get(d, *path):
+    for key in path:
+        if not isinstance(d, dict) or key not in d:
+            return None
+        d = d[key]
+    return d
+
+
+def correctness_flags(d, prefix=""):
+    """(path, value) of every boolean correctness flag in the full results:
+    rebuilt-shard checks, parity-vs-digest checks, verify verdicts."""
+    out = []
+    if isinstance(d, dict):
+        for key, x in d.items():
+            path = f"{prefix}.{key}" if prefix else key
+            if isinstance(x, bool):
+                if key not in NOT_FLAGS:
+                    out.append((path, x))
+            else:
+                out += correctness_flags(x, path)
+    elif isinstance(d, list):
+        for i, x in enumerate(d):
+            out += correctness_flags(x, f"{prefix}[{i}]")
+    return out
+
+
+def leg_summary(full):
+    """One number per extra leg (algorithmic GB/s unless the key says
+    otherwise), read from the full results; legs that did not run are left out."""
+    oc = full.get("other_configs") or {}
+    s = {
+        "reconstruct_10_4_lost_0_1_GBps": _get(full, "reconstruct", "algorithmic_GB_per_s"),
+        "reconstruct_10_4_cached_pattern_GBps": _get(full, "reconstruct_cached_pattern",
+                                                     "algorithmic_GB_per_s"),
+        "verify_10_4_c_abi_us_per_call": _get(full, "verify", "c_abi", "us_per_call"),
+        "verify_flat_10_4_GBps": _get(full, "verify_flat", "algorithmic_GB_per_s"),
+        "e2e_pinned_host_flat_MBps": _get(full, "end_to_end_pinned_host_flat", "MB_per_s"),
+        "e2e_pinned_host_reconstruct_MBps": _get(full, "end_to_end_pinned_host_reconstruct",
+                                                 "MB_per_s"),
+        "e2e_host_all_ranks_MBps": _get(full, "end_to_end_host_all_ranks", "MB_per_s_all_ranks"),
+        "gf8_10_2_1MiB_encode_GBps": _get(oc, "gf8_10_2", "encode_GB_per_s"),
+        "gf16_20_8_4MiB_encode_GBps": _get(oc, "gf16_20_8", "encode_GB_per_s"),
+        "gf16_20_8_4MiB_lost8_GBps": _get(oc, "gf16_20_8", "reconstruct_8_erased_syndrome_GB_per_s"),
+        "gf8_50_20_1MiB_encode_GBps": _get(oc, "gf8_50_20", "encode_GB_per_s"),
+        "gf16_40_12_1MiB_encode_GBps": _get(oc, "gf16_40_12", "encode_GB_per_s"),
+        "gf16_proper_encode_GBps": _get(full, "gf16_proper", "encode_GB_per_s"),
+        "gf16_proper_reconstruct_GBps": _get(full, "gf16_proper", "reconstruct_GB_per_s"),
+        "batch_4k_gf16_20_8_lost4_GBps": _get(full, "reconstruct_batch_4k", "GB_per_s"),
+        "batch_4k_data_only_GBps": _get(full, "reconstruct_batch_4k", "data_only_GB_per_s"),
+        "cpu_all_cores_10_4_MBps": _get(full, "cpu_baseline_legs", "encode_10_4_16MiB",
+                                        "all_cores", "value"),
+        "crossover_10_4_device_call_beats_cpu_from_bytes": _get(
+            full, "reference_bench_matrix", "crossover_10_4",
+            "gpu_call_device_beats_cpu_from_shard_bytes"),
+    }
+    s = {key: x for key, x in s.items() if x is not None}
+    ents = _get(full, "reference_bench_matrix", "entries") or []
+    enc = {e["shape"].replace(" x ", "x").replace(" KiB", "K"): _get(e, "gpu_flat", "GB_per_s")
+           for e in ents if e.get("op") == "encode"}
+    if enc:
+        s["ref_bench_encode_GBps"] = enc
+    one = [e.get("gpu_call_device_us") for e in ents
+           if e.get("shape") == "10+4 x 1 KiB" and e.get("op") == "encode"]
+    if one:
+        s["call_10_4_1KiB_encode_device_us"] = one[0]
+    return s
+
+
+def compact_line(line, full, full_path):
+    """The printed line: `line`'s contract keys, roofline and cpu_baseline
+    (trimmed), the leg summary, every correctness flag folded into one, and
+    where the full results are; shortened until it fits LINE_LIMIT."""
+    c = {key: line[key] for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+                                    "ms_per_step", "higher_is_better", "scaling",
+                                    "vs_baseline", "dtype", "data")}
+    c["config"] = {key: x for key, x in line["config"].items()
+                   if key not in ("parity_check_per_rank", "parity_checked_stripes_rank0")}
+    coll = line.get("collective") or {}
+    c["collective"] = {key: coll.get(key) for key in ("backend", "world_size", "distinct_gpus",
+                                                      "rehearsal")}
+    roof = {key: x for key, x in line["roofline"].items()
+            if key not in ("kernel_ms_per_launch_per_rank", "traffic_source")}
+    src = line["roofline"].get("traffic_source")
+    roof["traffic_file"] = src.get("file") if src else None
+    c["roofline"] = roof
+    c["cpu_baseline"] = line.get("cpu_baseline")
+    lib = line.get("library") or {}
+    c["library"] = {"sha256_16": (lib.get("sha256") or "")[:16],
+                    "source_commit": lib.get("source_commit")}
+    flags = correctness_flags(full)
+    bad = [path for path, ok in flags if not ok]
+    c["checks"] = {"flags": len(flags), "all_true": not bad, "false": bad[:4]}
+    c["legs"] = leg_summary(full)
+    c["full_results"] = full_path
+    # shorten (least important first) until the line fits
+    for cut in ("ref_bench_encode_GBps", "legs", "sample", "false"):
+        if len(json.dumps(c)) < LINE_LIMIT:
+            break
+        if cut == "ref_bench_encode_GBps":
+            c["legs"].pop(cut, None)
+        elif cut == "legs":
+            c.pop("legs")
+        elif cut == "sample" and c.get("cpu_baseline"):
+            c["cpu_baseline"] = dict(c["cpu_baseline"], sample=c["cpu_baseline"]["sample"][:80])
+        elif cut == "false":
+            c["checks"]["false"] = bad[:1]
+    return c
+
+
+def emit_results(line, cpu, extras, path):
+    """Writes the full results (line + CPU legs + every extra leg) to `path`
+    and prints the compact line as the last stdout line."""
+    full = dict(line)
+    for key in ("cpu_baseline_legs", "cpu_host"):
+        if key in cpu:
+            full[key] = cpu[key]
+    full.update(extras)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(full, f, indent=1)
+    shown = os.path.relpath(os.path.abspath(path), ROOT)
+    print(f"full results (every leg): {shown}", file=sys.stderr, flush=True)
+    out = compact_line(line, full, shown)
+    print(json.dumps(out), flush=True)
+    return out
+
+
 # ----------------------------------------------------------------- main
 def golden_stripes():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["generated"]
@@ -482,16 +623,18 @@ def main(argv=None):
         extras["end_to_end_host_all_ranks"] = host_leg(r, v, k, p, L, stream, world, rank,
                                                        coll_dev)
     if rank == 0 and not args.no_extras and world == 1:  # single-GPU legs
-        extras.update(extra_legs(r, v, k, p, L, min(pool, 256), stream))
         if (k, p, L) == (10, 4, 16 * MiB):
-            # the other configurations get HBM of their own, not the memory
-            # left around the headline's 112 GiB
+            # every other leg gets HBM of its own, allocated after the
+            # headline's 112 GiB is freed (not the memory left around it)
             del v, buf, step
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+            extras.update(fresh_extra_legs(r, k, p, L, min(pool, 256), stream))
             extras["other_configs"] = other_configs(stream)
             extras["reconstruct_batch_4k"] = batch_leg(stream)
             extras["reference_bench_matrix"] = reference_bench_matrix(stream)
+        else:
+            extras.update(extra_legs(r, v, k, p, L, min(pool, 256), stream))
 
     if rank == 0:
         per_launch_bytes = n_local * stripe_bytes / launches
@@ -528,11 +671,8 @@ def main(argv=None):
             "roofline": roof, "cpu_baseline": cpu.get("cpu_baseline"),
         }
         line["library"] = library_info()
-        for key in ("cpu_baseline_legs", "cpu_host"):
-            if key in cpu:
-                line[key] = cpu[key]
-        line.update(extras)
-        print(json.dumps(line), flush=True)
+        emit_results(line, cpu, extras, args.full_out or os.path.join(
+            ROOT, "gpurun_out", f"bench_full_n{world}.json"))
     if world > 1:
         dist.destroy_process_group()
 
@@ -1112,6 +1252,26 @@ def per_call_crossover(stream, sizes=(1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 
 def R_lib():
     import reed_solomon_erasure as R
     return R._lib.load()
+
+
+def fresh_extra_legs(r, k, p, L, n_stripes, stream):
+    """extra_legs on `n_stripes` stripes in an allocation of their own, made
+    after the headline's buffer is freed: the reconstruct and verify legs do
+    not depend on where the headline's 112 GiB left free memory."""
+    import torch
+    from reed_solomon_erasure.core import fill_splitmix
+    buf = torch.empty(n_stripes * (k + p) * L, dtype=torch.uint8, device="cuda")
+    v = buf.view(n_stripes, k + p, L)
+    for s in range(n_stripes):
+        for i in range(k):
+            fill_splitmix(v[s, i], SEED, shard_id(s, i))
+    r.encode_flat(buf, L, n_stripes)
+    try:
+        return extra_legs(r, v, k, p, L, n_stripes, stream)
+    finally:
+        del v, buf
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
 
 def extra_legs(r, v, k, p, L, n_stripes, stream, stripe0=0):

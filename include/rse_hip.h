@@ -382,9 +382,11 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                         (compiled codecs; run-time ones use two); 0: one wave holds
                                         all 8 rows; A/B variants of the compiled codecs (one pair):
                                         3 next unit prefetched, 6 compact mixing, 7 one input in
-                                        flight per wave (round 3's kernel); 4 / 5 timing
-                                        splits that skip the Horner steps / data networks (WRONG
-                                        bytes: tools/tune.py only) */
+                                        flight per wave (round 3's kernel).  4 / 5 (timing
+                                        splits that skip the Horner steps / data networks, which
+                                        write wrong bytes) exist only in tools/tune.py's
+                                        -DRSE_TUNE_SPLITS build: this library refuses them with
+                                        RSE_ERR_INVALID_ARGUMENT and keeps its setting */
 #define RSE_OPT_HOST_PLANNED_STRIPES 25 /* read-only, per thread: stripes rse_reconstruct_batch
                                        planned on the host (a batch past the device planner's LDS
                                        budget: more than 8192 shards or very many erasures) */
@@ -392,7 +394,7 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                        stream, host-pipeline streams/events/ring) in existence, leased or
                                        idle.  Calls lease one from a process-wide pool that keeps at most 4
                                        idle per device, so threads that come and go leave nothing behind */
-/* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key. */
+/* Process-wide; returns RSE_ERR_INVALID_ARGUMENT for an unknown key or a refused value. */
 int rse_set_option(int key, int64_t value);
 /* Current value, or -1 for an unknown key. */
 int64_t rse_get_option(int key);

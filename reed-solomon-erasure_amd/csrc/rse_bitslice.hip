@@ -274,6 +274,15 @@ __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t i) {
 // (one lane per stripe, LDS) 86-93 us.  Only the fields the Horner syndrome
 // kernels read are written (data / par / out pointers, out_sigma, the masks,
 // n_out, hm); the GF(2^8) log / exp tables come from `tabs` (host-built).
+// Orders the group's LDS accesses explicitly between the Gauss-Jordan phases
+// (fill, swap, scale, each row's elimination): the lanes of a group read
+// columns other lanes write, so the order must not rest on the compiler
+// keeping runtime-indexed LDS accesses in program order.
+__device__ __forceinline__ void group_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
     int field, const uint16_t* __restrict__ rows, const uint8_t* __restrict__ tabs,
     const uint8_t* __restrict__ present, uint32_t k, uint32_t p, uint32_t data_only, uint8_t* base,
@@ -327,26 +336,33 @@ __global__ __launch_bounds__(kPlanBlock) void bs_recon_plan_kernel(
     const uint32_t t = i / (2 * ne), x = i % (2 * ne);
     G(t, x) = x < ne ? rows[nth_bit(rmask, t) * k + nth_bit(smask, x)] : (x - ne == t ? 1 : 0);
   }
+  group_lds_order();
   // Gauss-Jordan: lane gl owns columns x = gl, gl + kPlanLanes, ... of row
   // operations; the pivot row is found by every lane (same reads, same answer)
   for (uint32_t col = 0; col < ne; ++col) {
     uint32_t piv = col;
     while (piv < ne && G(piv, col) == 0) ++piv;
     if (piv == ne) return;  // singular: impossible for this code; stripe left at n_out = 0
-    if (piv != col)
+    if (piv != col) {
       for (uint32_t x = gl; x < 2 * ne; x += kPlanLanes) {
         const uint16_t t0 = G(col, x);
         G(col, x) = G(piv, x);
         G(piv, x) = t0;
       }
+      group_lds_order();
+    }
     const uint32_t sc = gf.inv(G(col, col));
+    group_lds_order();  // every lane has the pivot before its owner scales it
     for (uint32_t x = col + gl; x < 2 * ne; x += kPlanLanes) G(col, x) = (uint16_t)gf.mul(sc, G(col, x));
+    group_lds_order();
     for (uint32_t r = 0; r < ne; ++r) {
       const uint32_t f = G(r, col);  // read by every lane before any lane writes row r
+      group_lds_order();
       if (r == col || !f) continue;
       for (uint32_t x = col + gl; x < 2 * ne; x += kPlanLanes)
         G(r, x) ^= (uint16_t)gf.mul(f, G(col, x));
     }
+    group_lds_order();
   }
   // outputs, lane gl the outputs o = gl, gl + kPlanLanes, ...: missing data
   // S_u = sum_t Ainv[u][t] s_t; missing parity r = sigma_r ^ sum_t (P[r][S]
@@ -458,6 +474,15 @@ constexpr BsDescFn rec_desc_deep_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_desc_deep_kernel<C, NS, D>;
   else return nullptr;
 }
+// The timing splits (pair_slot 3 / 4: no Horner steps / no data networks) write
+// wrong bytes by design; they exist only in tools/tune.py's own build
+// (-DRSE_TUNE_SPLITS).  The release library has nullptr there, and
+// rse_set_option refuses RSE_OPT_RECON_PAIRS 4 / 5 (rse_kernels.hip).
+#ifdef RSE_TUNE_SPLITS
+#define RSE_SPLIT_FN(...) __VA_ARGS__
+#else
+#define RSE_SPLIT_FN(...) nullptr
+#endif
 #define BS(C, CP, FIELD)                                                          \
   {FIELD, C::k, C::p, &C::rows[0][0],                                             \
    {{bitslice_kernel<C, false, false, false>, bitslice_kernel<C, true, false, false>}, \
@@ -491,7 +516,7 @@ constexpr BsDescFn rec_desc_deep_fn() {
     {rec_desc_deep_fn<C, 1, 3>(), rec_desc_deep_fn<C, 2, 3>(), rec_desc_deep_fn<C, 4, 3>(), \
      rec_desc_deep_fn<C, 8, 3>()}},                                                    \
    {rec_pair_fn<C, 1, false, 4>(), rec_pair_fn<C, 2>(), rec_pair_fn<C, 1, true>(),  \
-    rec_pair_fn<C, 1, false, 1>(), rec_pair_fn<C, 1, false, 2>(),                   \
+    RSE_SPLIT_FN(rec_pair_fn<C, 1, false, 1>()), RSE_SPLIT_FN(rec_pair_fn<C, 1, false, 2>()), \
     rec_pair_fn<C, 1, false, 3>(), rec_pair_fn<C, 1>()},                            \
    {rec_desc_pair_fn<C, 1, false, 4>(), rec_desc_pair_fn<C, 2>(),                   \
     rec_desc_pair_fn<C, 1, true>(), nullptr, nullptr,                               \
@@ -503,6 +528,7 @@ static const BsShape kBsShapes[] = {
     BS(Bs16_20_8, Bs16_20_8Plain, 16),  // the same in GF(2^16) (RSE_OPT_SUBFIELD 0)
 };
 #undef BS
+#undef RSE_SPLIT_FN
 
 }  // namespace
 
@@ -829,9 +855,8 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
                                        BsReconArgs* d_descs, hipStream_t stream, uint64_t* done) {
   *done = 0;
   if (!get_option(5) || shard_bytes < 4096 || k == 0 || k > (uint32_t)kMaxIn ||
-      p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0 || e_cap == 0 ||
-      e_cap > (uint32_t)kMaxOut)
-    return hipSuccess;
+      p > (uint32_t)kMaxOut || need == 0 || n_stripes == 0 || e_cap > (uint32_t)kMaxOut)
+    return hipSuccess;  // (e_cap 0: only parity lost -- rebuilt from the sigma rows)
   BsDescFn sfn = nullptr;
   BsDesc4Fn sfn4 = nullptr;
   hipFunction_t jfn = nullptr, jfn4 = nullptr;

@@ -1874,6 +1874,12 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
   // skipped.  Paths that need them on the host copy them there.
   int fdev = -1;
   const bool dev_flags = device_memory(present, &fdev);
+  if (dev_flags) {
+    // device flags must sit on the stripes' device: the scan and the
+    // planners read them in place (peer memory would fault or crawl)
+    int sdev = -1;
+    if (!device_memory(base, &sdev) || sdev != fdev) return RSE_ERR_INVALID_ARGUMENT;
+  }
   std::vector<uint8_t> hflags;  // host copy of device flags, made on demand
   auto host_flags = [&](size_t n) -> const uint8_t* {
     if (!dev_flags) return present;
@@ -2024,7 +2030,10 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
       int dev = 0;
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = plan_consts(c, dev, &consts);
-      if (e != hipSuccess) return dev_fail(release(e));
+      if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the flags' copy into the lease may be in flight
+        return dev_fail(release(e));
+      }
       uint8_t* ws = dflags + desc_off;  // the descriptors
       uint64_t bs_done = 0;
       e = rse::launch_bitslice_recon_batch(
@@ -2085,7 +2094,10 @@ int rse_reconstruct_batch(const rse_codec* c, void* stripes, size_t shard_len, s
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = plan_consts(c, dev, &consts);
     if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&ws), grp * per_stripe, st);
-    if (e != hipSuccess) return dev_fail(release(e));
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(st);  // step 1's work and the flags' copy may be in flight
+      return dev_fail(release(e));
+    }
   }
   hipError_t e = hipSuccess;
   for (size_t g0 = 0; g0 < n_stripes && e == hipSuccess; g0 += grp) {

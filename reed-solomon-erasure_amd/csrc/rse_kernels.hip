@@ -1319,7 +1319,14 @@ int set_option(int key, int64_t value) {
     case 23: g_opt.jit_exact = value ? 1 : 0; return 0;
     case 26: g_opt.wide_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 27: g_opt.recon_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
-    case 28: g_opt.recon_pairs = value < 0 ? 0 : value > 8 ? 8 : value; return 0;
+    case 28:
+#ifndef RSE_TUNE_SPLITS
+      // 4 / 5 select the timing splits, which write wrong bytes: tools/tune.py's
+      // -DRSE_TUNE_SPLITS build only (rse_bitslice.hip RSE_SPLIT_FN)
+      if (value == 4 || value == 5) return -2;
+#endif
+      g_opt.recon_pairs = value < 0 ? 0 : value > 8 ? 8 : value;
+      return 0;
     case 29: g_opt.wide_pairs = value ? 1 : 0; return 0;
     case 30: g_opt.sync_event = value ? 1 : 0; return 0;
     case 31: g_opt.spin_wait = value ? 1 : 0; return 0;

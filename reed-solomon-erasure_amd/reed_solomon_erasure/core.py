@@ -317,7 +317,8 @@ class ReedSolomon:
         T = self.total_shard_count()
         if isinstance(present, torch.Tensor) and present.is_cuda:
             if (tuple(present.shape) != (n_stripes, T) or not present.is_contiguous()
-                    or present.dtype not in (torch.bool, torch.uint8)):
+                    or present.dtype not in (torch.bool, torch.uint8)
+                    or present.device != stripes.device):  # read in place, on that device
                 raise RSError(Error.InvalidShardFlags)
             _check_flat(stripes, shard_len, n_stripes, T, self.field)
             _raise(_lib.rse_reconstruct_batch(

@@ -215,3 +215,63 @@ def test_reference_bench_matrix_on_the_gpu():
         elif e["op"] != "reconstruct_none":
             assert e["rebuilt_ok_all_stripes"] is True
     assert len(out["crossover_10_4"]["rows"]) == 2
+
+
+# ------------------------------------------------------ the printed line
+_LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "collective", "roofline", "cpu_baseline", "library")
+
+
+def _split_full(full):
+    """A full results dict -> (line, cpu, extras) as bench.main holds them."""
+    line = {key: full[key] for key in _LINE_KEYS}
+    cpu = {key: full[key] for key in ("cpu_baseline_legs", "cpu_host") if key in full}
+    extras = {key: x for key, x in full.items() if key not in _LINE_KEYS and key not in cpu}
+    return line, cpu, extras
+
+
+def test_printed_line_is_last_compact_and_complete(tmp_path, capsys):
+    """Round 4's full bench results (28.7 KB, tests/golden/bench_full_r04s17.json,
+    the last line of profiles/r04/s17/bench.log) through bench.emit_results:
+    the LAST stdout line parses, is < 4096 bytes, and carries the contract keys,
+    roofline.frac and cpu_baseline.value; every leg is in the full file."""
+    import json
+    import os
+    full = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "bench_full_r04s17.json")))
+    assert len(json.dumps(full)) > 8192  # the line the driver could not read
+    line, cpu, extras = _split_full(full)
+    out_path = tmp_path / "full.json"
+    bench.emit_results(line, cpu, extras, str(out_path))
+    stdout = capsys.readouterr().out
+    last = stdout.rstrip("\n").split("\n")[-1]
+    assert len(last.encode()) < 4096
+    got = json.loads(last)
+    for key in _LINE_KEYS[:-1]:
+        assert key in got, key
+    assert got["value"] == full["value"] and got["ms_per_step"] == full["ms_per_step"]
+    assert 0 < got["roofline"]["frac"] < 1 and got["roofline"]["peak"] == 8000.0
+    assert got["roofline"]["algorithmic_bytes_per_launch"] > 0
+    assert got["cpu_baseline"]["value"] > 0 and got["cpu_baseline"]["kind"] == "reference"
+    assert got["config"]["workload"] == full["config"]["workload"]
+    assert got["checks"]["all_true"] is True and got["checks"]["flags"] > 50
+    legs = got["legs"]
+    assert legs["reconstruct_10_4_lost_0_1_GBps"] == full["reconstruct"]["algorithmic_GB_per_s"]
+    assert legs["ref_bench_encode_GBps"]["64+64x1K"] > 0
+    assert json.load(open(out_path)) == full  # nothing lost: every leg in the file
+
+
+def test_printed_line_reports_a_false_flag_and_still_fits(tmp_path, capsys):
+    import json
+    import os
+    full = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "bench_full_r04s17.json")))
+    full["reference_bench_matrix"]["entries"][3]["rebuilt_ok_all_stripes"] = False
+    full["reference_bench_matrix"]["entries"] *= 8  # a much longer matrix
+    line, cpu, extras = _split_full(full)
+    got = bench.emit_results(line, cpu, extras, str(tmp_path / "f.json"))
+    last = capsys.readouterr().out.rstrip("\n").split("\n")[-1]
+    assert len(last.encode()) < 4096 and json.loads(last) == got
+    assert got["checks"]["all_true"] is False
+    assert got["checks"]["false"][0].startswith("reference_bench_matrix.entries[3]")

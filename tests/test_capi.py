@@ -310,3 +310,24 @@ def test_every_header_option_is_readable():
         assert L.rse_get_option(keys["RSE_OPT_SPIN_WAIT"]) == 0
     finally:
         L.rse_set_option(keys["RSE_OPT_SPIN_WAIT"], old)
+
+
+def test_wrong_byte_timing_splits_are_refused():
+    """RSE_OPT_RECON_PAIRS 4 / 5 select timing splits that skip the Horner
+    steps or the data networks and so write wrong bytes; the release library
+    refuses them (reconstruct must always return core.rs:680-695's bytes) and
+    keeps its setting, while the real variants are still accepted.  Only
+    `make tune` (-DRSE_TUNE_SPLITS, build-tune/) carries the splits."""
+    RECON_PAIRS = 28
+    INVALID_ARGUMENT = L.rse_set_option(99, 1)
+    assert INVALID_ARGUMENT != 0
+    old = L.rse_get_option(RECON_PAIRS)
+    try:
+        for bad in (4, 5):
+            assert L.rse_set_option(RECON_PAIRS, bad) == INVALID_ARGUMENT, bad
+            assert L.rse_get_option(RECON_PAIRS) == old
+        for good in (0, 1, 2, 3, 6, 7, 8):
+            assert L.rse_set_option(RECON_PAIRS, good) == 0, good
+            assert L.rse_get_option(RECON_PAIRS) == good
+    finally:
+        L.rse_set_option(RECON_PAIRS, old)

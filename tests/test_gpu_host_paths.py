@@ -709,3 +709,34 @@ def test_host_direct_and_pipeline_agree(R, field, k, p, n, direct):
             assert all((as_np(shards[i]) == full[i]).all() for i in range(T)), erased
     finally:
         lib.rse_set_option(32, old)
+
+
+def test_device_flags_must_sit_with_the_stripes(R):
+    """rse_reconstruct_batch reads device-resident flags in place, so they
+    must be on the stripes' device: flags in HBM with host stripes (C ABI),
+    or on another GPU (Python mirror and C ABI), are refused with
+    RSE_ERR_INVALID_ARGUMENT (100) / InvalidShardFlags before anything is
+    written."""
+    import ctypes
+    lib = R._lib.load()
+    k, p, n, stripes = 4, 2, 4096, 3
+    T = k + p
+    r = R.galois_8.ReedSolomon(k, p)
+    present = torch.ones((stripes, T), dtype=torch.uint8, device="cuda")
+    present[:, 0] = 0
+    hostbuf = np.full(stripes * T * n, 0x33, np.uint8)
+    rc = lib.rse_reconstruct_batch(r._h, hostbuf.ctypes.data, n, stripes,
+                                   ctypes.cast(present.data_ptr(), ctypes.POINTER(ctypes.c_uint8)),
+                                   0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 100 and (hostbuf == 0x33).all()
+    if torch.cuda.device_count() < 2:
+        return
+    buf = torch.full((stripes * T * n,), 0x33, dtype=torch.uint8, device="cuda:0")
+    other = present.to("cuda:1")
+    with pytest.raises(R.RSError) as ei:
+        r.reconstruct_batch(buf, n, stripes, other)
+    assert ei.value.error == R.Error.InvalidShardFlags
+    rc = lib.rse_reconstruct_batch(r._h, buf.data_ptr(), n, stripes,
+                                   ctypes.cast(other.data_ptr(), ctypes.POINTER(ctypes.c_uint8)),
+                                   0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 100 and bool((buf == 0x33).all())

@@ -616,6 +616,45 @@ def test_reconstruct_batch_per_stripe_patterns(R, subfield, field, k, p, n, stri
     lib.rse_set_option(9, old_jit)
 
 
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 20, 8)])
+@pytest.mark.parametrize("dflags", [False, True])
+def test_reconstruct_batch_parity_only_losses(R, field, k, p, dflags):
+    """Stripes that lost only parity shards (a scrub that found a bad parity
+    disk): no data shard is missing, so no stripe needs the Gauss-Jordan
+    (e_cap = 0), and the lost parity is rebuilt from the sigma rows on the
+    bit-sliced syndrome kernels (one launch), not the table planner; with
+    data_only nothing is written.  Against the oracle's encode."""
+    rng = np.random.default_rng(4242 + field + int(dflags))
+    lib = R._lib.load()
+    r = R.core.ReedSolomon(k, p, field)
+    assert r.kernel_kind(wait=True).startswith("bitslice")
+    es, T, stripes, n = field // 8, k + p, 9, 16384 + 64
+    oc = O.Codec(field, k, p)
+    full = []
+    for s in range(stripes):
+        st = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+        oc.encode(st)
+        full.append(np.stack(st))
+    want = np.stack(full)
+    present = np.ones((stripes, T), bool)
+    for s in range(stripes):
+        lost = rng.choice(p, int(rng.integers(1, p + 1)), replace=False)
+        present[s, k + lost] = False
+    for data_only in (False, True):
+        v = want.copy()
+        v[~present] = 0x5A
+        d = dev(v.reshape(-1))
+        n0 = lib.rse_get_option(6)
+        flags = torch.from_numpy(present).cuda() if dflags else present
+        r.reconstruct_batch(d, n, stripes, flags, data_only=data_only)
+        got = host(d).reshape(stripes, T, n * es)
+        if data_only:
+            assert (got == v).all()  # nothing lost that data_only rebuilds
+        else:
+            assert lib.rse_get_option(6) - n0 == 1  # the bit-sliced syndrome launch
+            assert (got == want).all()
+
+
 def test_reconstruct_batch_many_stripes_and_errors(R):
     """> 65535 stripes (grid.y chunking), tiny unaligned shards, all patterns
     drawn at random; errors leave every stripe untouched."""

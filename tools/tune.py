@@ -5,6 +5,10 @@ Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
 every configuration is timed once per round, the median over rounds reported.
 
     python tools/tune.py [--stripes 128] [--rounds 5] [--k 10 --p 4]
+
+The timing-split kernels (RSE_OPT_RECON_PAIRS 4 / 5: phases skipped, wrong
+bytes) exist only in the tune build: `make -C reed-solomon-erasure_amd tune`,
+then run with RSE_LIB_PATH=reed-solomon-erasure_amd/build-tune/librse_hip.so.
 """
 import argparse
 import json
