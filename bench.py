@@ -631,6 +631,7 @@ def main(argv=None):
             torch.cuda.empty_cache()
             extras.update(fresh_extra_legs(r, k, p, L, min(pool, 256), stream))
             extras["other_configs"] = other_configs(stream)
+            extras["gf16_proper"] = gf16_proper_leg(stream)
             extras["reconstruct_batch_4k"] = batch_leg(stream)
             extras["reference_bench_matrix"] = reference_bench_matrix(stream)
         else:
@@ -916,6 +917,68 @@ def other_configs(stream):
     out["gf8_50_20"] = wide_config(stream, g, 8, 50, 20)
     out["gf16_40_12"] = wide_config(stream, g, 16, 40, 12)
     return out
+
+
+GF16_PROPER = (256, 16, 256 << 10, 64)  # k, p, shard bytes, stripes per launch
+
+
+def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROPER[2],
+                    stripes=GF16_PROPER[3], check=16384, lost=4):
+    """GF(2^16) proper: a codec past GF(2^8)'s 256 shards (galois_16.rs:20-21,
+    ORDER = 65536), whose Vandermonde points leave the subfield, so it codes
+    on the GF(2^16) kernels (16 x 16 bit matrices), not the GF(2^8) ones.
+    Encode of `stripes` stripes per launch (the one-module wide kernel, built
+    at run time and waited for), stripe 0's parity checked against the oracle
+    on its first and last `check` bytes (column j of the parity depends only
+    on column j of the data); then reconstruct_data_flat with data shards
+    0..lost-1 erased (first use: no decode-pattern kernel), every rebuilt
+    shard of every stripe checked against its synthetic bytes."""
+    import numpy as np
+    import torch
+    import reed_solomon_erasure as R
+    from reed_solomon_erasure.core import fill_splitmix, last_kernel
+    from oracle import oracle as O
+    T = k + p
+    buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
+    v = buf.view(stripes, T, nbytes)
+    for s_ in range(stripes):
+        for i in range(k):
+            fill_splitmix(v[s_, i], SEED, shard_id(s_, i))
+    r = R.core.ReedSolomon(k, p, 16)
+    t0 = time.perf_counter()
+    kind = r.kernel_kind(wait=True)
+    build_s = time.perf_counter() - t0
+    elems = nbytes // 2
+    enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream,
+                     reps=10, warm_s=0.25)
+    d = {"workload": f"gf16 {k}+{p} x {nbytes >> 10} KiB, {stripes} stripes/launch "
+                     f"({T} shards: past GF(2^8)'s 256, no subfield)",
+         "kernels": kind, "kernel": last_kernel(), "build_seconds": round(build_s, 1),
+         "timing": "0.25 s of untimed launches, then 10 back to back (HIP events)",
+         "encode_GB_per_s": enc, "encode_MB_per_s": round(enc * 1e9 / MiB, 1),
+         "encode_roofline_frac": round(enc / HBM_PEAK_GBPS, 4)}
+    oc = O.Codec(16, k, p)
+    ok = True
+    for sl in (slice(0, check), slice(nbytes - check, nbytes)):
+        sh = [v[0, i, sl].cpu().numpy().copy() for i in range(k)] + \
+             [np.zeros(check, np.uint8) for _ in range(p)]
+        oc.encode(sh)
+        ok = ok and all(np.array_equal(sh[k + j], v[0, k + j, sl].cpu().numpy())
+                        for j in range(p))
+    d["parity_check_vs_oracle_stripe0_head_tail"] = ok
+    lib = R_lib()
+    lib.rse_set_option(11, 0)  # a first use of the pattern
+    try:
+        leg = reconstruct_leg(r, v, k, list(range(lost)), elems, stripes, stream, fill_splitmix,
+                              list(range(stripes)), reps=10, warm_s=0.25)
+    finally:
+        lib.rse_set_option(11, 1)
+    d[f"reconstruct_{lost}_lost_kernel"] = last_kernel()
+    d["reconstruct_GB_per_s"] = leg["GB_per_s"]
+    d["reconstruct_rebuilt_ok_all_stripes"] = leg["rebuilt_ok_all_stripes"]
+    del buf, v
+    torch.cuda.empty_cache()
+    return d
 
 
 def batch_leg(stream, stripes=65536, erasures=4, reps=10):
