@@ -293,6 +293,33 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                size_t n_stripes, const uint8_t *present, int data_only,
                                rse_stream_t stream);
 
+/* ---- synchronous calls (the reference's own contract) ----------------- */
+/* encode / verify / reconstruct / reconstruct_data of ONE stripe of device
+ * shards that return when the result is in device memory, like the
+ * reference's ReedSolomon methods (core.rs:597-611, 637-651, 680-695): same
+ * validation, errors and bytes as rse_encode / rse_verify / rse_reconstruct /
+ * rse_reconstruct_data.  No stream: the call is not ordered after work the
+ * caller queued -- the caller has finished writing the shards it passes (for
+ * example by synchronising its stream).  Small stripes (GF(2^8) codecs and
+ * GF(2^16) codecs of at most 256 shards, 16-byte aligned shards, at most
+ * RSE_OPT_DISPATCH_MAX_BYTES per shard, k x outputs <= 1024) go to a resident
+ * workgroup that polls pinned host memory for requests (RSE_OPT_DISPATCH): no
+ * kernel launch, no stream synchronisation -- a round trip of a few
+ * microseconds.  It ends by itself after RSE_OPT_DISPATCH_IDLE_US without a
+ * call, so it never holds the device for longer (a hipDeviceSynchronize may
+ * wait that long).  Anything else runs the usual kernels on a library stream
+ * and waits for them.  Thread-safe; calls to one device are served one at a
+ * time. */
+int rse_encode_now(const rse_codec *codec, void *const *shards, const size_t *lens, size_t n);
+int rse_verify_now(const rse_codec *codec, const void *const *shards, const size_t *lens,
+                   size_t n, int *ok);
+int rse_reconstruct_now(const rse_codec *codec, void *const *shards, const size_t *lens,
+                        const uint8_t *present, size_t n);
+int rse_reconstruct_data_now(const rse_codec *codec, void *const *shards, const size_t *lens,
+                             const uint8_t *present, size_t n);
+/* Ends the resident dispatcher kernels now (they end by themselves when idle). */
+void rse_dispatcher_stop(void);
+
 /* ---- launch-shape options (performance only; results never change) ----- */
 #define RSE_OPT_NONTEMPORAL 1       /* 1: streaming (nt) loads/stores of shard bytes */
 #define RSE_OPT_GRID_X 2            /* table kernels: workgroups per stripe row; bit-sliced
@@ -371,6 +398,18 @@ int rse_reconstruct_host_batch(const rse_codec *codec, void *stripes, size_t sha
                                         16 KiB ones (or shorter than 16 KiB): the syndrome kernels
                                         code those chunks when k x outputs >= this (default 64;
                                         GF(2^16) proper always), else the table kernels do */
+#define RSE_OPT_WIDE_HALF 38         /* wide GF(2^8) modules with paired networks built after: 1
+                                        (default) each wave codes 2 KiB chunks, one 8-plane group
+                                        per lane (half the accumulators: 8 outputs per wave fit in
+                                        registers); 0: 4 KiB chunks, two groups per lane */
+#define RSE_OPT_DISPATCH 39           /* 1 (default): small *_now calls run on the resident dispatcher;
+                                        0: always the launch path (A/B) */
+#define RSE_OPT_DISPATCH_IDLE_US 40   /* the resident dispatcher ends after this many microseconds
+                                        without a call (default 2000) */
+#define RSE_OPT_DISPATCH_MAX_BYTES 41 /* shard bytes up to which a *_now call is dispatched
+                                        (default 32768) */
+#define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
+#define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

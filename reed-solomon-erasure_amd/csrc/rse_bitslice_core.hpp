@@ -743,6 +743,199 @@ __device__ __forceinline__ void wide_body_lds(const A& a, WidePlanes<W>& lds) {
   if (mode != kStore && diff) flag_mismatch(h.mismatch);
 }
 
+// ------------------------------------- GF(2^8) wide codecs on half chunks
+// wide_body_lds_deep gives each lane 16 dwords of every shard (a 4 KiB chunk
+// per wave): two 8-plane groups, so a wave's share of o outputs holds 16 o
+// accumulators.  At 8 outputs per wave (32+32, 64+64: the reference's widest
+// bench shapes, benches/bandwidth.rs:94-95, 154-155) that is 128 VGPRs before
+// the input pair's 16 planes and 32 temporaries, and the module spilled 172
+// (32+32) / 274 (64+64) VGPRs to scratch.  Here a wave's chunk is 2 KiB: lane
+// l loads vectors l and l + 64 (each load instruction still 1 KiB contiguous
+// per wave) -- 8 dwords, ONE plane group -- so the accumulators halve, and the
+// network code (written once per group in mac_pair) is half as long.  The
+// networks themselves are the paired GF(2^8) ones (C::kPairIn): the same
+// XORs per byte.  SUB: 1 or 2 KiB shards, a chunk = 2048 / SUB consecutive
+// stripes' shards (32 lanes per stripe for 1 KiB, vectors 512 B apart).
+template <int W>
+using WideHalfPlanes = uint4[2][W][2][64];  // [set][slot][quad of planes][lane]
+
+// 2 vectors (8 dwords) -> 8 planes, and back (clobbers pl).
+__device__ __forceinline__ void slice8(const u32x4 (&v)[2], uint32_t (&pl)[8]) {
+#pragma unroll
+  for (int d = 0; d < 8; ++d) pl[d] = v[d >> 2][d & 3];
+  transpose8(pl);
+}
+__device__ __forceinline__ void unslice8(uint32_t (&pl)[8], u32x4 (&v)[2]) {
+  transpose8(pl);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) v[d >> 2][d & 3] = pl[d];
+}
+template <uint32_t S>
+__device__ __forceinline__ void load2(u32x4 (&v)[2], const uint8_t* p) {
+  v[0] = ldv<false>(p);
+  v[1] = ldv<false>(p + S);
+}
+
+// mac_pair on one plane group: acc[o * 8 + q] (^)= plane q of output o's
+// terms of network input J (data inputs 2J, 2J + 1).
+template <class C, int J, int... OP>
+__device__ __forceinline__ void mac_pair_half(uint32_t (&acc)[C::p * 8], const uint32_t (&pa)[8],
+                                              const uint32_t (&pb)[8], int_seq<int, OP...>) {
+  uint32_t src[16 + C::kGTemps];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    src[q] = pa[q];
+    src[8 + q] = pb[q];
+  }
+#pragma unroll
+  for (int t = 0; t < C::kGTemps; ++t)
+    if (t < C::planes.ntmp[J]) src[16 + t] = temp_source<C, J>(src, t);
+  if constexpr (J == 0)
+    ((acc[OP] = xinit<C::planes.sel[OP / 8][J][OP % 8]>(src)), ...);
+  else
+    ((acc[OP] = xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[OP], src)), ...);
+}
+
+template <class C, int W, int R, int S>
+__device__ __forceinline__ void wide_code_round_half(uint32_t (&acc)[C::p * 8],
+                                                     const uint4 (&set)[W][2][64], uint32_t lane) {
+  static_assert(C::kPairIn && W % 2 == 0, "half chunks: paired GF(2^8) networks, W even");
+  if constexpr (S < W && R * W + S < C::k) {
+    uint32_t pa[8], pb[8];
+#pragma unroll
+    for (int q4 = 0; q4 < 2; ++q4) {
+      const uint4 v = set[S][q4][lane];
+      pa[q4 * 4 + 0] = v.x;
+      pa[q4 * 4 + 1] = v.y;
+      pa[q4 * 4 + 2] = v.z;
+      pa[q4 * 4 + 3] = v.w;
+    }
+    if constexpr (R * W + S + 1 < C::k) {
+#pragma unroll
+      for (int q4 = 0; q4 < 2; ++q4) {
+        const uint4 v = set[S + 1][q4][lane];
+        pb[q4 * 4 + 0] = v.x;
+        pb[q4 * 4 + 1] = v.y;
+        pb[q4 * 4 + 2] = v.z;
+        pb[q4 * 4 + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pb[q] = 0u;
+    }
+    mac_pair_half<C, (R * W + S) / 2>(acc, pa, pb, make_int_seq<C::p * 8>{});
+#pragma unroll
+    for (int q = 0; q < C::p * 8; ++q) asm volatile("" : "+v"(acc[q]));
+    wide_code_round_half<C, W, R, S + 2>(acc, set, lane);
+  }
+}
+
+// The rounds of one half chunk, D own inputs in flight per wave (as
+// wide_rounds_deep: ring of D + 1 slots; past the last round, the next
+// chunk's first rounds).
+template <class C, int W, int WI, int D, int R, class A, uint32_t S>
+__device__ __forceinline__ void wide_rounds_half(uint32_t (&acc)[C::p * 8], u32x4 (&buf)[D + 1][2],
+                                                 const A& a, uint64_t off, uint64_t next_off,
+                                                 WideHalfPlanes<W>& lds, uint32_t& g, uint32_t lane) {
+  constexpr int K = C::k, NR = (K + W - 1) / W;
+  if constexpr (R < NR) {
+    constexpr int mine = R * W + WI, ahead = R + D;
+    if constexpr (ahead < NR) {
+      if constexpr (ahead * W + WI < K) load2<S>(buf[ahead % (D + 1)], a.in[ahead * W + WI] + off);
+    } else if constexpr ((ahead - NR) * W + WI < K) {
+      if (next_off != ~0ull) load2<S>(buf[ahead % (D + 1)], a.in[(ahead - NR) * W + WI] + next_off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint4(&set)[W][2][64] = lds[g & 1u];
+    if constexpr (mine < K) {
+      uint32_t pl[8];
+      slice8(buf[R % (D + 1)], pl);
+      set[WI][0][lane] = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+      set[WI][1][lane] = make_uint4(pl[4], pl[5], pl[6], pl[7]);
+    }
+    __syncthreads();
+    wide_code_round_half<C, W, R, 0>(acc, set, lane);
+    ++g;
+    wide_rounds_half<C, W, WI, D, R + 1, A, S>(acc, buf, a, off, next_off, lds, g, lane);
+  }
+}
+
+// Wave WI of W; C its share of the outputs (O0 the first).  All W waves call
+// this with the same `lds`.  The launch's chunk count is in 2 KiB units
+// (rse_jit.cpp launch_wide: twice the 4 KiB chunks, or ceil(n_stripes /
+// (2048 / SUB))).
+template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0>
+__device__ __forceinline__ void wide_body_half(const A& a, WideHalfPlanes<W>& lds) {
+  static_assert(SUB == 0 || SUB == 1024u || SUB == 2048u, "1 or 2 KiB shards");
+  const WideHdr& h = a.h;
+  constexpr int K = C::k, NR = (K + W - 1) / W;
+  constexpr uint32_t S = SUB ? SUB / 2u : 1024u;  // a lane's two vectors, S bytes apart
+  constexpr uint32_t SPC = SUB ? 2048u / SUB : 1u, LPS = 64u / SPC;  // stripes / chunk, lanes / stripe
+  const uint64_t halves = 2 * h.chunks_per_stripe;  // 2 KiB chunks per stripe
+  const uint64_t total = SUB ? (h.n_stripes + SPC - 1) / SPC : halves * h.n_stripes;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = (SUB ? lane % LPS : lane) * 16u;
+  const uint32_t mode = h.mode;
+  bool diff = false;
+  uint32_t g = 0;
+  auto chunk_off = [&](uint64_t c) {
+    if constexpr (SUB) {
+      uint64_t stripe = c * SPC + lane / LPS;
+      if (stripe >= h.n_stripes) stripe = h.n_stripes - 1;  // loaded, never stored
+      return stripe * h.stripe_stride + lane_off;
+    }
+    const uint64_t stripe = c / halves, half = c - stripe * halves;
+    return stripe * h.stripe_stride + half * 2048u + lane_off;
+  };
+  u32x4 buf[D + 1][2];
+  if (blockIdx.x < total) {
+    const uint64_t off0 = chunk_off(blockIdx.x);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (j < NR && j * W + WI < K) load2<S>(buf[j], a.in[j * W + WI] + off0);
+  }
+  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const uint64_t off = chunk_off(c);
+    const uint64_t next = c + gridDim.x;
+    const uint64_t next_off = next < total ? chunk_off(next) : ~0ull;
+    uint32_t acc[C::p * 8];
+    wide_rounds_half<C, W, WI, D, 0, A, S>(acc, buf, a, off, next_off, lds, g, lane);
+    if constexpr (NR % (D + 1) != 0) {  // the next chunk's rounds j into slots j
+      u32x4 t[D][2];
+#pragma unroll
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) t[j][q] = buf[(NR + j) % (D + 1)][q];
+#pragma unroll
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) buf[j][q] = t[j][q];
+    }
+    const bool ok = SUB == 0 || c * SPC + lane / LPS < h.n_stripes;
+#pragma unroll
+    for (int o = 0; o < C::p; ++o) {
+      uint32_t pl[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pl[q] = acc[o * 8 + q];
+      u32x4 v[2];
+      unslice8(pl, v);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint64_t o16 = off + j * S;
+        if (mode != kCheck && ok) stv<true>(a.out[O0 + o] + o16, v[j]);
+        if (mode != kStore) {
+          const u32x4 w = ldv<true>(a.cmp[O0 + o] + o16);
+          diff |= ok & ((w.x != v[j].x) | (w.y != v[j].y) | (w.z != v[j].z) | (w.w != v[j].w));
+        }
+      }
+    }
+    if (h.per_stripe && diff) {
+      flag_mismatch(h.mismatch + (SUB ? c * SPC + lane / LPS : c / halves));
+      diff = false;
+    }
+  }
+  if (mode != kStore && diff) flag_mismatch(h.mismatch);
+}
+
 // ------------------------------------------------------------ reconstruct
 // Bit-sliced syndrome reconstruct (BsReconArgs in rse_kernels.hpp).  The input
 // sequence is the present data shards, then the syndrome parity shards; the

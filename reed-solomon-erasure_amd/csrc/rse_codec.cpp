@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/rse_hip.h"
+#include "rse_dispatch.hpp"
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
 
@@ -1770,6 +1771,104 @@ int rse_reconstruct_data(const rse_codec* c, void* const* shards, const size_t* 
   return reconstruct_impl(c, shards, lens, present, n, true, (hipStream_t)stream);
 }
 
+}  // extern "C"
+
+namespace {
+
+// One synchronous coding pass of the *_now entries: out = rows x in (check:
+// compared with cmp, *mismatch).  The resident dispatcher when it applies
+// (rse_dispatch.hip: no launch, no stream); otherwise run_job's launches on a
+// leased library stream, waited for.  Either way the call returns with the
+// result in device memory, and neither is ordered after the caller's streams:
+// the caller has finished writing the inputs (the reference's synchronous
+// contract, core.rs:597-695).
+int run_now(const rse_codec* c, const Rows& rows, const uint8_t* const* in, uint8_t* const* out,
+            const uint8_t* const* cmp, size_t len_bytes, bool* mismatch) {
+  const bool check = cmp != nullptr;
+  uint8_t* const* tgt = check ? const_cast<uint8_t* const*>(cmp) : out;
+  if (rse::dispatch_applies(c->kfield, (uint32_t)rows.n_in, (uint32_t)rows.n_out, len_bytes, in,
+                            tgt)) {
+    bool mm = false;
+    RSE_HIP(rse::dispatch_run(rows.c.data(), (uint32_t)rows.n_in, (uint32_t)rows.n_out, in, tgt,
+                              len_bytes, check, &mm));
+    if (mismatch) *mismatch = mm;
+    return RSE_OK;
+  }
+  Lease lease;
+  RSE_HIP(lease.acquire());
+  hipStream_t st = nullptr;
+  RSE_HIP(lease_own_stream(lease.get(), &st));
+  Job j{c->kfield, &rows, in, check ? nullptr : out, cmp, len_bytes,
+        check ? rse::kCheck : rse::kStore, false, nullptr, 0, 1};
+  if (check) {
+    int ok = 0;
+    const int rc = run_check(j, st, &ok);
+    if (rc) return rc;
+    if (mismatch) *mismatch = !ok;
+    return RSE_OK;
+  }
+  const int rc = run_job(j, st);
+  const hipError_t e = hipStreamSynchronize(st);
+  if (rc) return rc;
+  RSE_HIP(e);
+  return RSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rse_encode_now(const rse_codec* c, void* const* shards, const size_t* lens, size_t n) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  int rc;
+  if ((rc = check_count(n, c->total, RSE_TOO_FEW_SHARDS, RSE_TOO_MANY_SHARDS))) return rc;
+  if (!lens || !shards) return RSE_ERR_INVALID_ARGUMENT;
+  if ((rc = check_multi(lens, n))) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
+  const Rows rows = parity_rows(c);
+  return run_now(c, rows, reinterpret_cast<const uint8_t* const*>(shards),
+                 reinterpret_cast<uint8_t* const*>(shards) + c->k, nullptr, lens[0] * c->esize(),
+                 nullptr);
+}
+
+int rse_verify_now(const rse_codec* c, const void* const* shards, const size_t* lens, size_t n,
+                   int* ok) {
+  int rc = verify_checks(c, shards, lens, n, nullptr, nullptr, 0, false, ok);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!shards[i]) return RSE_ERR_INVALID_ARGUMENT;
+  const Rows rows = parity_rows(c);
+  bool mm = false;
+  rc = run_now(c, rows, reinterpret_cast<const uint8_t* const*>(shards), nullptr,
+               reinterpret_cast<const uint8_t* const*>(shards) + c->k, lens[0] * c->esize(), &mm);
+  if (rc) return rc;
+  *ok = mm ? 0 : 1;
+  return RSE_OK;
+}
+
+static int reconstruct_now(const rse_codec* c, void* const* shards, const size_t* lens,
+                           const uint8_t* present, size_t n, bool data_only) {
+  if (!c) return RSE_ERR_INVALID_ARGUMENT;
+  ReconPlan plan;
+  int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
+  if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  return run_now(c, plan.rows, plan.in.data(), plan.out.data(), nullptr, plan.len * c->esize(),
+                 nullptr);
+}
+
+int rse_reconstruct_now(const rse_codec* c, void* const* shards, const size_t* lens,
+                        const uint8_t* present, size_t n) {
+  return reconstruct_now(c, shards, lens, present, n, false);
+}
+
+int rse_reconstruct_data_now(const rse_codec* c, void* const* shards, const size_t* lens,
+                             const uint8_t* present, size_t n) {
+  return reconstruct_now(c, shards, lens, present, n, true);
+}
+
+void rse_dispatcher_stop(void) { rse::dispatch_stop_all(); }
+
 int rse_encode_flat(const rse_codec* c, void* stripes, size_t shard_len, size_t n_stripes,
                     rse_stream_t stream) {
   RSE_ON_STREAM(stream);
@@ -2371,6 +2470,8 @@ int64_t rse_get_option(int key) {
   if (key == RSE_OPT_PATTERN_LAUNCHES) return g_pattern_launches;
   if (key == RSE_OPT_SCRATCH_LIVE) return scratch_pool().live.load();
   if (key == RSE_OPT_HOST_PLANNED_STRIPES) return g_host_planned;
+  if (key == RSE_OPT_DISPATCHED) return rse::dispatch_count();
+  if (key == RSE_OPT_DISPATCH_LAUNCHES) return rse::dispatch_launch_count();
   return rse::get_option(key);
 }
 

@@ -1,0 +1,406 @@
+// rse_dispatch.hip -- the resident dispatcher of the synchronous small-stripe
+// calls (rse_encode_now / rse_verify_now / rse_reconstruct_now, include/rse_hip.h).
+//
+// Why.  The reference's ReedSolomon::encode (core.rs:597-611) is a synchronous
+// CPU call that returns in 0.06-14 us on its own bench's 1-16 KiB blocks
+// (benches/bandwidth.rs:88-190).  A kernel launch plus the wait for it costs
+// 12 us on MI355X before any work (tools/latency_probe.hip: empty kernel +
+// hipStreamSynchronize 12.3 us, + a spin on a pinned word 6.1 us; rse_encode
+// of 10+4 x 1 KiB + hipStreamSynchronize 18.5 us), while a round trip to a
+// kernel that is already resident and polls pinned host memory is 2.7 us.
+// So small calls go to one resident workgroup instead of a launch.
+//
+// Protocol (one request in flight per device; callers serialise on a mutex):
+//  * the request is a run of 16-byte granules in pinned host memory, each
+//    {tag, a, b}; the host writes the body, then granule 0, every granule
+//    tagged with the request's sequence number;
+//  * wave 0 of the resident workgroup reads the first 64 granules with one
+//    wave-wide system-coherent load per poll (a PCIe read of 1 KiB: the whole
+//    request for codecs up to ~24 coefficient rows x inputs); a request is
+//    taken when granule 0 carries a new sequence number and every granule of
+//    the request carries it too (a line the host had not written yet when it
+//    was read shows the old tag: poll again);
+//  * the workgroup builds the coefficients' v_perm tables in LDS, codes (or
+//    checks) the shards, drains its stores, and stores {seq, verdict} into a
+//    pinned ack word, which the host spins on;
+//  * after RSE_OPT_DISPATCH_IDLE_US without a request the kernel stores
+//    {last seq, EXIT} and ends, so it never holds the device (a
+//    hipDeviceSynchronize waits at most that long for it) and always drains.
+//    A host that finds EXIT without its sequence number relaunches; the new
+//    kernel takes the pending request (it starts from the last sequence
+//    number served).
+//
+// Memory ordering.  Inputs are read with non-temporal loads (they bypass the
+// CU's L1, which would otherwise keep lines of an earlier request), outputs are
+// written with write-through (sc1) stores and drained (s_waitcnt vmcnt(0))
+// before the ack, so later kernels on any XCD read them from memory
+// (MI355X_MICROARCH.md, inter-workgroup visibility).  Only vector stores are
+// used.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "rse_device.hpp"
+#include "rse_dispatch.hpp"
+
+namespace rse {
+namespace {
+
+constexpr int kDispThreads = 512;       // one workgroup, 8 waves (256 VGPRs: no spills)
+constexpr int kMaxGranules = 256;       // 4 KiB of request
+constexpr uint32_t kDispMaxIn = 64, kDispMaxOut = 64, kDispMaxCoef = 1024;
+constexpr uint64_t kAckExit = 1ull << 32, kAckMismatch = 1ull << 33;
+constexpr uint32_t kOpCode = 0, kOpCheck = 1, kOpStop = 2;  // granule 0's a & 0xF
+
+struct alignas(16) Granule {
+  uint32_t tag, a;
+  uint64_t b;
+};
+
+// 16-byte system-coherent loads of pinned host memory (PCIe reads that bypass
+// L1 and L2), as vector loads: one request per granule, so a granule is read
+// whole (a line the host is writing is seen before or after, never torn).
+// The wait is tied to the loaded registers, so no use moves above it.
+typedef unsigned dw4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ dw4 load_sys16_nowait(const Granule* g) {
+  dw4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(g) : "memory");
+  return v;
+}
+__device__ __forceinline__ void wait_loads(dw4& a) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a)::"memory");
+}
+__device__ __forceinline__ void wait_loads(dw4& a, dw4& b, dw4& c) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c)::"memory");
+}
+
+__device__ __forceinline__ uint64_t now_ticks() {  // 100 MHz constant clock
+  return __builtin_amdgcn_s_memrealtime();
+}
+
+// Codes one request: items (vector v, output block ob) over the workgroup;
+// OB outputs per item.  Pointers and tables are read from LDS (broadcast: the
+// lanes of a wave share an output block).  Returns this thread's mismatch
+// (check mode).
+template <int OB>
+__device__ bool code_items(const Granule* req, uint32_t n_in, uint32_t n_out, uint64_t n_vec,
+                           bool check, const uint4* tq, const uint32_t* tt) {
+  bool diff = false;
+  const uint32_t n_ob = (n_out + OB - 1) / OB;
+  const uint64_t items = n_vec * n_ob;
+  for (uint64_t it = threadIdx.x; it < items; it += kDispThreads) {
+    const uint32_t ob = (uint32_t)(it / n_vec);
+    const uint64_t off = (it - (uint64_t)ob * n_vec) * 16u;
+    const uint32_t o0 = ob * OB;
+    uint4 acc[OB];
+#pragma unroll
+    for (int o = 0; o < OB; ++o) acc[o] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i0 = 0; i0 < n_in; i0 += 8) {
+      uint4 x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)  // every load of the group in flight at once
+        if (i0 + j < n_in)
+          x[j] = ld16<true>(reinterpret_cast<const uint8_t*>(req[1 + i0 + j].b) + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (i0 + j >= n_in) break;
+        const Sel s0 = make_sel(x[j].x), s1 = make_sel(x[j].y), s2 = make_sel(x[j].z),
+                  s3 = make_sel(x[j].w);
+#pragma unroll
+        for (int o = 0; o < OB; ++o) {
+          if (o0 + o >= n_out) break;
+          const Gf8Tab t = read_tab(tq, tt, (int)((o0 + o) * n_in + i0 + j));
+          acc[o].x = gf8_mac4(acc[o].x, t, s0);
+          acc[o].y = gf8_mac4(acc[o].y, t, s1);
+          acc[o].z = gf8_mac4(acc[o].z, t, s2);
+          acc[o].w = gf8_mac4(acc[o].w, t, s3);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < OB; ++o) {
+      if (o0 + o >= n_out) break;
+      uint8_t* p = reinterpret_cast<uint8_t*>(req[1 + n_in + o0 + o].b) + off;
+      if (check) {
+        const uint4 w = ld16<true>(p);
+        diff |= (w.x != acc[o].x) | (w.y != acc[o].y) | (w.z != acc[o].z) | (w.w != acc[o].w);
+      } else {
+        const dw4 v = {acc[o].x, acc[o].y, acc[o].z, acc[o].w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+      }
+    }
+  }
+  return diff;
+}
+
+// The resident workgroup.  ring: the request granules (device view of pinned
+// host memory); ack: the pinned ack word.  seen: the last sequence number
+// served before this launch.
+__global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granule* ring,
+                                                                    uint64_t* ack, uint32_t seen,
+                                                                    uint64_t idle_ticks) {
+  __shared__ Granule req[kMaxGranules];
+  __shared__ uint4 tq[kDispMaxCoef];
+  __shared__ uint32_t tt[kDispMaxCoef];
+  __shared__ uint32_t s_state;  // 0 idle, 1 request in req[], 2 exit
+  __shared__ uint32_t s_diff;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t last = now_ticks();
+  for (;;) {
+    if (wave == 0) {
+      // one poll: granules lane, lane + 64, ... of the request as far as needed
+      uint32_t state = 0;
+      dw4 g0 = load_sys16_nowait(ring + lane);
+      wait_loads(g0);
+      const uint32_t tag0 = __shfl(g0.x, 0);
+      const uint32_t n_gran = (__shfl(g0.y, 0) >> 20) & 0xFFFu;
+      if (tag0 != seen && n_gran >= 1 && n_gran <= (uint32_t)kMaxGranules) {
+        dw4 m[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+        if (n_gran > 64u) {
+          for (int q = 0; q < 3; ++q)
+            if (lane + 64u * (q + 1) < n_gran) m[q] = load_sys16_nowait(ring + lane + 64u * (q + 1));
+          wait_loads(m[0], m[1], m[2]);
+        }
+        bool ok = lane >= n_gran || g0.x == tag0;
+        for (int q = 0; q < 3; ++q)
+          if (lane + 64u * (q + 1) < n_gran) ok = ok && m[q].x == tag0;
+        if (__all(ok)) {  // every granule of the request is this request's
+          reinterpret_cast<dw4*>(req)[lane] = g0;
+          for (int q = 0; q < 3; ++q)
+            if (lane + 64u * (q + 1) < n_gran) reinterpret_cast<dw4*>(req)[lane + 64u * (q + 1)] = m[q];
+          state = (__shfl(g0.y, 0) & 0xFu) == kOpStop ? 2u : 1u;  // a stop request ends it now
+          seen = tag0;
+        }
+      }
+      if (state == 0 && now_ticks() - last > idle_ticks) state = 2;
+      if (lane == 0) {
+        s_state = state;
+        s_diff = 0;
+      }
+    }
+    __syncthreads();
+    const uint32_t state = s_state;
+    if (state == 2) break;
+    if (state == 0) {
+      __syncthreads();  // s_state is rewritten by wave 0 only after everyone read it
+      continue;
+    }
+    // the request: granule 0 {tag, op | n_in << 4 | n_out << 12 | n_gran << 20,
+    // len | outputs per work item << 56},
+    // then n_in input and n_out output pointers, then the coefficients (12 per
+    // granule, row-major by output, in a then b)
+    const uint32_t hdr = req[0].a;
+    const bool check = (hdr & 0xFu) == kOpCheck;
+    const uint32_t n_in = (hdr >> 4) & 0xFFu, n_out = (hdr >> 12) & 0xFFu;
+    const uint64_t len = req[0].b & ((1ull << 48) - 1);
+    const uint32_t n_coef = n_in * n_out;
+    for (uint32_t c = tid; c < n_coef; c += kDispThreads) {
+      const Granule& g = req[1 + n_in + n_out + c / 12u];
+      const uint32_t byte = c % 12u;
+      const uint32_t coef = byte < 4 ? (g.a >> (8 * byte)) & 0xFFu
+                                     : (uint32_t)(g.b >> (8 * (byte - 4))) & 0xFFu;
+      const Gf8Tab t = make_gf8_tab(coef);
+      write_tab(tq, tt, (int)c, t);
+    }
+    __syncthreads();
+    const uint64_t n_vec = len / 16u;
+    // outputs per item: enough items for the workgroup's threads, at most 8
+    const uint32_t ob = (uint32_t)(req[0].b >> 56);
+    bool diff;
+    if (ob <= 1) diff = code_items<1>(req, n_in, n_out, n_vec, check, tq, tt);
+    else if (ob == 2) diff = code_items<2>(req, n_in, n_out, n_vec, check, tq, tt);
+    else if (ob <= 4) diff = code_items<4>(req, n_in, n_out, n_vec, check, tq, tt);
+    else diff = code_items<8>(req, n_in, n_out, n_vec, check, tq, tt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this thread landed
+    if (diff) atomicOr(&s_diff, 1u);
+    __syncthreads();
+    if (tid == 0) {
+      const uint64_t a = (uint64_t)seen | (s_diff ? kAckMismatch : 0ull);
+      __hip_atomic_store(ack, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    last = now_ticks();
+    __syncthreads();
+  }
+  if (tid == 0) __hip_atomic_store(ack, (uint64_t)seen | kAckExit, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------- host
+struct Dispatcher {
+  std::mutex mu;
+  bool init = false, running = false;
+  hipStream_t st = nullptr;
+  Granule* req = nullptr;  // pinned, mapped: host view
+  Granule* dreq = nullptr;
+  uint64_t* ack = nullptr;
+  uint64_t* dack = nullptr;
+  uint32_t seq = 0;     // the last request posted
+  uint32_t served = 0;  // the last request acknowledged
+};
+constexpr int kDispDevs = 64;
+Dispatcher& dispatcher(int dev) {
+  static Dispatcher* d = new Dispatcher[kDispDevs];  // never destroyed (see rse_codec.cpp pool)
+  return d[dev];
+}
+std::atomic<int64_t> g_dispatched{0}, g_dispatch_launches{0};
+
+hipError_t disp_init(Dispatcher& d) {
+  if (d.init) return hipSuccess;
+  hipError_t e = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&d.req), sizeof(Granule) * kMaxGranules + 64,
+                      hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&d.ack), 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dreq), d.req, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dack), d.ack, 0);
+  if (e != hipSuccess) return e;
+  std::memset(d.req, 0, sizeof(Granule) * kMaxGranules);
+  *reinterpret_cast<volatile uint64_t*>(d.ack) = 0;
+  d.init = true;
+  return hipSuccess;
+}
+
+// A kernel that starts from the last request served (a posted one is new to
+// it); the ack starts there too, never at a stale EXIT.
+hipError_t disp_launch(Dispatcher& d) {
+  *reinterpret_cast<volatile uint64_t*>(d.ack) = (uint64_t)d.served;
+  const int64_t idle_us = get_option(40);
+  hipLaunchKernelGGL(rse_dispatch_kernel, dim3(1), dim3(kDispThreads), 0, d.st, d.dreq, d.dack,
+                     d.served, (uint64_t)(idle_us < 1 ? 1 : idle_us) * 100u);
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    d.running = true;
+    ++g_dispatch_launches;
+  }
+  return e;
+}
+
+}  // namespace
+
+bool dispatch_applies(int field, uint32_t n_in, uint32_t n_out, uint64_t len_bytes,
+                      const uint8_t* const* in, uint8_t* const* out) {
+  if (!get_option(39) || field != 8 || n_in == 0 || n_out == 0 || n_in > kDispMaxIn ||
+      n_out > kDispMaxOut || n_in * n_out > kDispMaxCoef || len_bytes == 0 ||
+      len_bytes % 16u != 0 || (int64_t)len_bytes > get_option(41))
+    return false;
+  const uint32_t n_gran = 1 + n_in + n_out + (n_in * n_out + 11) / 12;
+  if (n_gran > (uint32_t)kMaxGranules) return false;
+  for (uint32_t i = 0; i < n_in; ++i)
+    if (!in[i] || (reinterpret_cast<uintptr_t>(in[i]) & 15u)) return false;
+  for (uint32_t o = 0; o < n_out; ++o)
+    if (!out[o] || (reinterpret_cast<uintptr_t>(out[o]) & 15u)) return false;
+  return true;
+}
+
+// outputs = rows x inputs (check: compare with outputs, *mismatch set) on the
+// resident workgroup of the current device; synchronous.  dispatch_applies
+// must hold.  Returns a hipError_t.
+hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
+                        const uint8_t* const* in, uint8_t* const* out, uint64_t len_bytes,
+                        bool check, bool* mismatch) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kDispDevs) return hipErrorInvalidDevice;
+  Dispatcher& d = dispatcher(dev);
+  std::lock_guard<std::mutex> g(d.mu);
+  if ((e = disp_init(d)) != hipSuccess) return e;
+  const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;  // 0: the zeroed ring
+  const uint32_t n_gran = 1 + n_in + n_out + (n_in * n_out + 11) / 12;
+  // outputs per work item: items (vectors x output blocks) for the threads
+  const uint64_t n_vec = len_bytes / 16u;
+  uint32_t ob = 1;
+  while (ob < 8 && n_vec * ((n_out + 2 * ob - 1) / (2 * ob)) >= (uint64_t)kDispThreads) ob *= 2;
+  volatile Granule* r = d.req;
+  for (uint32_t i = 0; i < n_in; ++i) {
+    r[1 + i].a = 0;
+    r[1 + i].b = reinterpret_cast<uint64_t>(in[i]);
+  }
+  for (uint32_t o = 0; o < n_out; ++o) {
+    r[1 + n_in + o].a = 0;
+    r[1 + n_in + o].b = reinterpret_cast<uint64_t>(out[o]);
+  }
+  const uint32_t nc = n_in * n_out, cg0 = 1 + n_in + n_out;
+  for (uint32_t q = 0; q * 12 < nc; ++q) {
+    uint8_t b[12] = {};
+    for (uint32_t j = 0; j < 12 && q * 12 + j < nc; ++j) b[j] = (uint8_t)rows[q * 12 + j];
+    uint32_t a;
+    uint64_t w;
+    std::memcpy(&a, b, 4);
+    std::memcpy(&w, b + 4, 8);
+    r[cg0 + q].a = a;
+    r[cg0 + q].b = w;
+  }
+  for (uint32_t q = 1; q < n_gran; ++q) r[q].tag = seq;
+  r[0].a = (check ? kOpCheck : kOpCode) | (n_in << 4) | (n_out << 12) | (n_gran << 20);
+  r[0].b = len_bytes | ((uint64_t)ob << 56);
+  std::atomic_thread_fence(std::memory_order_release);
+  r[0].tag = seq;  // the request is posted
+  d.seq = seq;
+  if (!d.running) {
+    if ((e = disp_launch(d)) != hipSuccess) return e;
+  }
+  volatile uint64_t* ack = d.ack;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t n = 1;; ++n) {
+    const uint64_t a = *ack;
+    if ((uint32_t)a == seq && !(a & kAckExit)) {
+      d.served = seq;
+      if (mismatch) *mismatch = (a & kAckMismatch) != 0;
+      ++g_dispatched;
+      return hipSuccess;
+    }
+    if (a & kAckExit) {  // the kernel idled out before it saw this request
+      if ((e = hipStreamSynchronize(d.st)) != hipSuccess) return e;
+      d.running = false;
+      if ((e = disp_launch(d)) != hipSuccess) return e;
+      continue;
+    }
+    __builtin_ia32_pause();
+    if ((n & 4095u) == 0) {
+      // a launch that failed, or a kernel that died, ends the wait
+      const hipError_t q = hipStreamQuery(d.st);
+      if (q != hipErrorNotReady && q != hipSuccess) return q;
+      if (q == hipSuccess && *ack == a) {  // ended without an ack for us: run again
+        d.running = false;
+        if ((e = disp_launch(d)) != hipSuccess) return e;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+        return hipErrorLaunchTimeOut;
+    }
+  }
+}
+
+// Ends the resident kernel of every device this process started one on: a
+// stop request (it would also end by itself after RSE_OPT_DISPATCH_IDLE_US).
+void dispatch_stop_all() {
+  for (int dev = 0; dev < kDispDevs; ++dev) {
+    Dispatcher& d = dispatcher(dev);
+    std::lock_guard<std::mutex> g(d.mu);
+    if (!d.init || !d.running) continue;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) continue;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) continue;
+    const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;
+    volatile Granule* r = d.req;
+    r[0].a = kOpStop | (1u << 20);  // one granule
+    r[0].b = 0;
+    std::atomic_thread_fence(std::memory_order_release);
+    r[0].tag = seq;
+    d.seq = seq;
+    (void)hipStreamSynchronize(d.st);  // it takes the stop (or has idled out)
+    d.served = seq;
+    d.running = false;
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
+}
+
+int64_t dispatch_count() { return g_dispatched.load(); }
+int64_t dispatch_launch_count() { return g_dispatch_launches.load(); }
+
+}  // namespace rse

@@ -64,6 +64,7 @@ struct Compiled {
   std::string log;
   double ms = 0;
   int wide_w = 0;  // kJitWide: waves per workgroup the module was generated for
+  bool wide_half = false;  // kJitWide: 2 KiB chunks per wave (wide_body_half)
 };
 
 // Two modules per codec, built in this order: the encode/verify kernel
@@ -205,7 +206,8 @@ void wide_share(uint32_t p, int W_, int w, uint32_t* o0, uint32_t* n) {
 // The device source of one codec: the shared kernel code, the codec's
 // plane-selection table, and extern "C" entry points.
 std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uint16_t>& rows,
-                        int stage, JitKind kind, int* wide_w = nullptr) {
+                        int stage, JitKind kind, int* wide_w = nullptr,
+                        bool* wide_half = nullptr) {
   std::string s;
   s.reserve(sizeof(kJitSource) + 1024 + (size_t)8 * k * p * (field == 16 ? 16 : 8));
   // hiprtc has no <stdint.h>: its runtime header declares the fixed-width
@@ -224,6 +226,11 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS
     // kernels code a round's inputs two at a time, so W must be even
     const bool pairs = field == 8 && shared && W % 2 == 0 && get_option(29) != 0;
+    // RSE_OPT_WIDE_HALF: the paired GF(2^8) networks on 2 KiB chunks, one plane
+    // group per lane (rse_bitslice_core.hpp wide_body_half: half the
+    // accumulators; 8 outputs per wave no longer spill)
+    const bool half = pairs && get_option(38) != 0;
+    if (wide_half) *wide_half = half;
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, W, w, &o0, &n);
@@ -251,14 +258,20 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
                     // 64-thread group would give 64 VGPRs and spill
                     "extern \"C\" __global__ __attribute__((amdgpu_flat_work_group_size(%d, %d),\n"
                     "    amdgpu_waves_per_eu(%d))) void rse_jit_wide%s(const WideArgs a) {\n"
-                    "  __shared__ rse::WidePlanes<%d> lds;\n"
+                    "  __shared__ rse::%s<%d> lds;\n"
                     "  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {\n",
-                    64 * W, 64 * W, wide_waves_per_eu(p), q == 0 ? "" : q == 1 ? "_s1" : "_s2", W);
+                    64 * W, 64 * W, wide_waves_per_eu(p), q == 0 ? "" : q == 1 ? "_s1" : "_s2",
+                    half ? "WideHalfPlanes" : "WidePlanes", W);
       s += buf;
       for (int w = 0; w < W; ++w) {
         uint32_t o0, n;
         wide_share(p, W, w, &o0, &n);
-        if (shared)
+        if (half)
+          std::snprintf(buf, sizeof buf,
+                        "    case %d: rse::wide_body_half<rse::JitWide%d, %u, %d, %d, %d, "
+                        "WideArgs, %du>(a, lds); break;\n",
+                        w, w, o0, W, w, (int)get_option(26), 1024 * q);
+        else if (shared)
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d, "
                         "WideArgs, %du>(a, lds); break;\n",
@@ -561,7 +574,8 @@ void build_in_process(const std::string& src, Compiled* out) {
 
 std::shared_ptr<const Compiled> compile(const Entry& e, int stage, int slot) {
   auto out = std::make_shared<Compiled>();
-  const std::string src = make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w);
+  const std::string src =
+      make_source(e.field, e.k, e.p, e.rows, stage, e.kind, &out->wide_w, &out->wide_half);
   const auto t0 = std::chrono::steady_clock::now();
   const std::string key = hash_key(src);
   const bool disk = get_option(15) != 0 && !cache_dir().empty();
@@ -885,7 +899,10 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   size_t size = buf.size();
   void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                    HIP_LAUNCH_PARAM_END};
-  const uint64_t total = subq ? (n_stripes + 4u / subq - 1) / (4u / subq) : cps * n_stripes;
+  // chunks of the module's own size: 4 KiB, or 2 KiB (wide_body_half); with
+  // 1 / 2 KiB shards, 4096 (2048) / len stripes per chunk
+  const uint64_t cb = c->wide_half ? 2048u : 4096u, spc = cb / (subq ? len : cb);
+  const uint64_t total = subq ? (n_stripes + spc - 1) / spc : cps * (4096u / cb) * n_stripes;
   const int64_t grid = get_option(2);
   // tools/tune.py grid sweeps, 128 stripes x 1 MiB (profiles/r04/s2/): GF(2^16)
   // 40+12 16384 workgroups 5.29 TB/s against 5.05 at 4096; GF(2^8) 50+20 flat
@@ -895,9 +912,10 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
   const int W = c->wide_w;  // the module's own workgroup shape
   if (subq)
-    note_kernel("bitslice-wide gf%d %u+%u w%d sub%d", field, k, p, W, subq);
+    note_kernel("bitslice-wide gf%d %u+%u w%d%s sub%d", field, k, p, W, c->wide_half ? " half" : "",
+                subq);
   else
-    note_kernel("bitslice-wide gf%d %u+%u w%d", field, k, p, W);
+    note_kernel("bitslice-wide gf%d %u+%u w%d%s", field, k, p, W, c->wide_half ? " half" : "");
   he = hipModuleLaunchKernel(fn, (uint32_t)gx, 1, 1, 64u * (uint32_t)W, 1, 1, 0, stream, nullptr,
                              extra);
   if (he != hipSuccess) return he;

@@ -797,6 +797,10 @@ struct Options {
   int64_t jit_max_patterns = 64;  // decode-pattern modules per process
   int64_t jit_max_pattern_blocks = 64;  // blocks of wide decode patterns per process
   int64_t recon_w4_min = 64;      // 4 KiB syndrome chunks from this many coefficients
+  int64_t wide_half = 1;          // GF(2^8) paired wide modules on 2 KiB chunks (one plane group)
+  int64_t dispatch = 1;           // *_now calls on the resident dispatcher (rse_dispatch.hip)
+  int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
+  int64_t dispatch_max_bytes = 32768;  // shard bytes up to which a *_now call is dispatched
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1336,6 +1340,10 @@ int set_option(int key, int64_t value) {
     case 35: g_opt.jit_max_patterns = value < 0 ? 0 : value; return 0;
     case 36: g_opt.jit_max_pattern_blocks = value < 0 ? 0 : value; return 0;
     case 37: g_opt.recon_w4_min = value < 0 ? 0 : value; return 0;
+    case 38: g_opt.wide_half = value ? 1 : 0; return 0;
+    case 39: g_opt.dispatch = value ? 1 : 0; return 0;
+    case 40: g_opt.dispatch_idle_us = value < 10 ? 10 : value > 1000000 ? 1000000 : value; return 0;
+    case 41: g_opt.dispatch_max_bytes = value < 0 ? 0 : value; return 0;
     default: return -1;
   }
 }
@@ -1385,6 +1393,10 @@ int64_t get_option(int key) {
     case 35: return g_opt.jit_max_patterns;
     case 36: return g_opt.jit_max_pattern_blocks;
     case 37: return g_opt.recon_w4_min;
+    case 38: return g_opt.wide_half;
+    case 39: return g_opt.dispatch;
+    case 40: return g_opt.dispatch_idle_us;
+    case 41: return g_opt.dispatch_max_bytes;
     default: return -1;
   }
 }

@@ -29,6 +29,8 @@ EXPORTS = (
     "rse_encode_single_sep_host", "rse_verify_host", "rse_verify_with_buffer_host",
     "rse_verify_host_flat", "rse_reconstruct_host", "rse_reconstruct_data_host",
     "rse_reconstruct_host_batch", "rse_fill_splitmix",
+    "rse_encode_now", "rse_verify_now", "rse_reconstruct_now", "rse_reconstruct_data_now",
+    "rse_dispatcher_stop",
     "rse_set_option", "rse_get_option", "rse_last_kernel",
 )
 
@@ -84,6 +86,11 @@ _SIGS = {
     "rse_gf16_mul_slice": (_c.c_int, [_u8p, _vp, _vp, _sz, _c.c_int, _vp]),
     "rse_last_kernel": (_c.c_char_p, []),
     "rse_fill_splitmix": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64, _vp]),
+    "rse_encode_now": (_c.c_int, [_vp, _vp, _szp, _sz]),
+    "rse_verify_now": (_c.c_int, [_vp, _vp, _szp, _sz, _ip]),
+    "rse_reconstruct_now": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz]),
+    "rse_reconstruct_data_now": (_c.c_int, [_vp, _vp, _szp, _u8p, _sz]),
+    "rse_dispatcher_stop": (None, []),
     "rse_set_option": (_c.c_int, [_c.c_int, _c.c_int64]),
     "rse_get_option": (_c.c_int64, [_c.c_int]),
 }

@@ -65,6 +65,15 @@ def _dev(t: torch.Tensor) -> int:
     return t.data_ptr()
 
 
+def _settle(t: Optional[torch.Tensor]) -> None:
+    """Waits for torch's current stream on t's device (the *_now entries are
+    not stream-ordered: the shards' writers must have finished)."""
+    idx = t.get_device() if t is not None else -1
+    st = torch.cuda.current_stream(idx if idx >= 0 else None)
+    if not st.query():
+        st.synchronize()
+
+
 def _check_flat(stripes: torch.Tensor, shard_len: int, n_stripes: int, total: int,
                 field: int) -> None:
     """The flat calls take a base pointer: refuse a buffer the stripes overrun."""
@@ -233,7 +242,7 @@ class ReedSolomon:
         """core.rs:693-695: only the data shards are rebuilt."""
         self._reconstruct(shards, data_only=True)
 
-    def _reconstruct(self, shards: list, data_only: bool) -> None:
+    def _reconstruct(self, shards: list, data_only: bool, now: bool = False) -> None:
         if len(shards) < self.total_shard_count():
             raise RSError(Error.TooFewShards)
         if len(shards) > self.total_shard_count():
@@ -274,11 +283,43 @@ class ReedSolomon:
             *[(_elems(b, self.field) if b is not None else 0) for b in bufs])
         pres = (ctypes.c_uint8 * max(1, n))(*[1 if p else 0 for p in present])
         like = next((b for b in bufs if b is not None), None)
-        fn = _lib.rse_reconstruct_data if data_only else _lib.rse_reconstruct
-        _raise(fn(self._h, ptrs, lens, pres, n, _stream(like)))
+        if now:
+            _settle(like)
+            fn = _lib.rse_reconstruct_data_now if data_only else _lib.rse_reconstruct_now
+            _raise(fn(self._h, ptrs, lens, pres, n))
+        else:
+            fn = _lib.rse_reconstruct_data if data_only else _lib.rse_reconstruct
+            _raise(fn(self._h, ptrs, lens, pres, n, _stream(like)))
         if not flagged:
             for i in range(n):
                 shards[i] = bufs[i]
+
+    # ------------------------------------------------- synchronous forms
+    # The reference's methods return when done (core.rs:597-695); these do
+    # too: torch's current stream is waited for (the shards' writers), then
+    # the *_now entry codes the stripe -- small stripes on the resident
+    # dispatcher, no kernel launch -- and returns with the result in place.
+    def encode_now(self, shards: ShardList) -> None:
+        """encode() (core.rs:597-611), returning when the parity is written."""
+        ptrs, lens = _arrays(shards, self.field)
+        _settle(_first(shards))
+        _raise(_lib.rse_encode_now(self._h, ptrs, lens, len(shards)))
+
+    def verify_now(self, shards: ShardList) -> bool:
+        """verify() (core.rs:637-651) through rse_verify_now."""
+        ptrs, lens = _arrays(shards, self.field)
+        ok = ctypes.c_int(0)
+        _settle(_first(shards))
+        _raise(_lib.rse_verify_now(self._h, ptrs, lens, len(shards), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def reconstruct_now(self, shards: list) -> None:
+        """reconstruct() (core.rs:680-682), returning when the shards are rebuilt."""
+        self._reconstruct(shards, data_only=False, now=True)
+
+    def reconstruct_data_now(self, shards: list) -> None:
+        """reconstruct_data() (core.rs:693-695), returning when the data is rebuilt."""
+        self._reconstruct(shards, data_only=True, now=True)
 
     # ------------------------------------------------ beyond the reference
     def encode_flat(self, stripes: torch.Tensor, shard_len: int, n_stripes: int = 1) -> None:

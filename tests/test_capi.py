@@ -331,3 +331,33 @@ def test_wrong_byte_timing_splits_are_refused():
             assert L.rse_get_option(RECON_PAIRS) == good
     finally:
         L.rse_set_option(RECON_PAIRS, old)
+
+
+def test_now_entries_validate_like_the_stream_entries():
+    """rse_encode_now / rse_verify_now / rse_reconstruct(_data)_now (the
+    synchronous forms, core.rs:597-695's contract) return the same errors as
+    rse_encode / rse_verify / rse_reconstruct, in the same precedence, before
+    any device work (tests/mod.rs:1058-1163)."""
+    r = R.galois_8.ReedSolomon(3, 2)
+    ok = ctypes.c_int()
+    pres = (ctypes.c_uint8 * 6)(*([1] * 6))
+    for n, err in [(4, Error.TooFewShards), (6, Error.TooManyShards)]:
+        assert L.rse_encode_now(r._h, ptrs(n), lens([10] * n), n) == err
+        assert L.rse_verify_now(r._h, ptrs(n), lens([10] * n), n, ctypes.byref(ok)) == err
+        assert L.rse_reconstruct_now(r._h, ptrs(n), lens([10] * n), pres, n) == err
+        assert L.rse_reconstruct_data_now(r._h, ptrs(n), lens([10] * n), pres, n) == err
+    r2 = R.galois_8.ReedSolomon(2, 2)
+    pres4 = (ctypes.c_uint8 * 4)(1, 1, 1, 1)
+    for ls, err in [([3, 2, 3, 3], Error.IncorrectShardSize), ([2, 2, 3, 3], Error.IncorrectShardSize),
+                    ([2, 3, 3, 3], Error.IncorrectShardSize), ([0, 3, 3, 3], Error.EmptyShard)]:
+        assert L.rse_encode_now(r2._h, ptrs(4), lens(ls), 4) == err
+        assert L.rse_encode(r2._h, ptrs(4), lens(ls), 4, None) == err
+        assert L.rse_verify_now(r2._h, ptrs(4), lens(ls), 4, ctypes.byref(ok)) == err
+        assert L.rse_reconstruct_now(r2._h, ptrs(4), lens(ls), pres4, 4) == err
+    none = (ctypes.c_uint8 * 4)(0, 0, 0, 0)
+    assert L.rse_reconstruct_now(r2._h, ptrs(4), lens([3] * 4), none, 4) == \
+        Error.TooFewShardsPresent
+    assert L.rse_reconstruct_now(r2._h, ptrs(4), lens([3] * 4), pres4, 4) == 0  # nothing to do
+    assert L.rse_encode_now(None, ptrs(4), lens([3] * 4), 4) == 100
+    assert L.rse_verify_now(r2._h, ptrs(4), lens([3] * 4), 4, None) == 100
+    L.rse_dispatcher_stop()  # nothing started: a no-op

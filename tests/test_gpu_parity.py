@@ -1497,7 +1497,26 @@ def test_bench_ranks_rehearsal(ranks, extras):
 # (rse_jit.cpp wide_waves): 1 for p < 4, else 4 (p <= 32) or 8 (10+40: shares
 # of 5; 4+17: 5/4/4/4).
 WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
-               (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9)]
+               (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9),
+               (8, 32, 32, 1), (8, 64, 64, 1)]  # benches/bandwidth.rs:94-95's widest (half chunks)
+
+
+def test_wide_full_chunks_option(R):
+    """RSE_OPT_WIDE_HALF 0: a GF(2^8) paired wide module on 4 KiB chunks per
+    wave (two plane groups per lane, wide_body_lds_deep) instead of the
+    default 2 KiB ones (wide_body_half); the same bytes.  A codec no other
+    test builds (modules are keyed by rows, not options)."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    old = lib.rse_get_option(38)
+    try:
+        assert lib.rse_set_option(38, 0) == 0
+        test_wide_codec_kernels(R, 1, 8, 34, 10, 1)
+        assert "half" not in last_kernel(), last_kernel()
+    finally:
+        lib.rse_set_option(38, old)
+    test_wide_codec_kernels(R, 1, 8, 35, 10, 1)  # the default: half chunks
+    assert last_kernel().startswith("bitslice-wide gf8 35+10 w4 half"), last_kernel()
 
 
 def test_wide_codec_unbalanced_waves(R):
@@ -1662,6 +1681,7 @@ def test_jit_verify_completion_word(R, k, p):
     (8, 10, 4), (8, 10, 2), (16, 20, 8),   # compiled codecs
     (8, 4, 4), (8, 8, 8), (8, 5, 2), (16, 6, 3),  # run-time specialised
     (8, 50, 20), (8, 16, 16), (16, 40, 12),  # wide codecs (one module, LDS bodies)
+    (8, 32, 32), (8, 64, 64),                # wide, half chunks, 8 outputs per wave
     (8, 40, 2),                              # wide, one wave (plain body)
 ])
 @pytest.mark.parametrize("kib", [1, 2])

@@ -18,7 +18,10 @@ for kp in 4:4 8:8 16:16 32:32 64:64 5:2 10:4 50:20; do
 done
 pat+=(--pattern "8:4:4:2048:0" --pattern "8:4:4:2048:0,1,2,3")
 pat+=(--pattern "16:20:8:4194304:0,1,2,3")  # other_configs gf16_20_8 cached pattern
-exec python3 tools/prebuild_jit.py \
+# tests/test_gpu_parity.py test_wide_full_chunks_option: one codec on full
+# (4 KiB) chunks, RSE_OPT_WIDE_HALF 0, in a process of its own
+python3 tools/prebuild_jit.py --set 38=0 --codec 8:34:10 || exit 1
+exec python3 tools/prebuild_jit.py --codec 8:35:10 \
   --codec 8:50:20 --codec 16:40:12 --codec 16:100:30 \
   --codec 8:4:4 --codec 8:8:8 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 --codec 8:5:2 \
   --codec 8:12:4 --codec 16:6:3 --codec 8:6:3 --codec 8:32:8 --codec 8:17:5 --codec 16:1000:24 \
