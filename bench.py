@@ -405,10 +405,17 @@ def leg_summary(full):
            for e in ents if e.get("op") == "encode"}
     if enc:
         s["ref_bench_encode_GBps"] = enc
-    one = [e.get("gpu_call_device_us") for e in ents
-           if e.get("shape") == "10+4 x 1 KiB" and e.get("op") == "encode"]
-    if one:
-        s["call_10_4_1KiB_encode_device_us"] = one[0]
+    for key, col in (("call_10_4_1KiB_encode_device_us", "gpu_call_device_us"),
+                     ("call_10_4_1KiB_encode_now_us", "gpu_call_now_us"),
+                     ("cpu_10_4_1KiB_encode_call_us", "cpu_reference_call_us")):
+        one = [e.get(col) for e in ents
+               if e.get("shape") == "10+4 x 1 KiB" and e.get("op") == "encode"]
+        if one and one[0] is not None:
+            s[key] = one[0]
+    now_win = _get(full, "reference_bench_matrix", "crossover_10_4",
+                   "gpu_call_now_beats_cpu_from_shard_bytes")
+    if now_win is not None:
+        s["crossover_10_4_now_call_beats_cpu_from_bytes"] = now_win
     return s
 
 
@@ -1171,7 +1178,10 @@ def reference_bench_matrix(stream, shapes=None, crossover_sizes=None):
     sh = st.cuda_stream
     out = {"what": "benches/bandwidth.rs:88-190 shapes; data_MB_per_s counts k x block per "
                    "call as criterion does; *_call_us are per synchronous call (python ctypes "
-                   "loop, ~1 us of call overhead included); cpu_reference = simd_c -O3 "
+                   "loop, ~1 us of call overhead included): gpu_call_device = the stream entry + "
+                   "stream synchronisation, gpu_call_now = the synchronous entry (rse_*_now: "
+                   "small stripes on the resident dispatcher), gpu_call_host = the *_host entry "
+                   "on pageable host shards; cpu_reference = simd_c -O3 "
                    "-march=haswell in core.rs loop order, 1 thread, decode rows cached; "
                    "run-time kernel builds waited for (RSE_OPT_JIT 2): steady state, as the "
                    "reference's repeated calls with their decode rows cached",
@@ -1243,6 +1253,9 @@ def _matrix_rows(lib, stream, st, sh, out, one_stripe, shapes):
 
                 def host():
                     _ck(lib.rse_encode_host(r._h, hptrs, lens, T, sh))
+
+                def now():
+                    _ck(lib.rse_encode_now(r._h, ptrs, lens, T))
                 erased = None
             else:
                 d = p if delete == -1 else delete
@@ -1263,6 +1276,9 @@ def _matrix_rows(lib, stream, st, sh, out, one_stripe, shapes):
 
                 def host():
                     _ck(lib.rse_reconstruct_host(r._h, hptrs, lens, pres, T, sh))
+
+                def now():
+                    _ck(lib.rse_reconstruct_now(r._h, ptrs, lens, pres, T))
             if "gpu_flat" in e:
                 f = e["gpu_flat"]
                 alg = T if op == "encode" else k + len(erased)
@@ -1272,10 +1288,13 @@ def _matrix_rows(lib, stream, st, sh, out, one_stripe, shapes):
             st.synchronize()
             e["gpu_call_device_async_us"] = round(t_async, 2)
             e["gpu_call_host_us"] = round(per_call_us(host), 2)
+            st.synchronize()
+            e["gpu_call_now_us"] = round(per_call_us(now), 2)
             if erased is None or erased:
                 c = cpu_reference_call_us(k, p, block, erased)
                 e["cpu_reference_call_us"] = round(c, 3) if c is not None else None
-            for key in ("gpu_call_device_us", "gpu_call_host_us", "cpu_reference_call_us"):
+            for key in ("gpu_call_device_us", "gpu_call_host_us", "gpu_call_now_us",
+                        "cpu_reference_call_us"):
                 if e.get(key):
                     e[key.replace("_us", "_data_MB_per_s")] = round(data_bytes / e[key] / MiB * 1e6, 1)
             out["entries"].append(e)
@@ -1319,15 +1338,21 @@ def per_call_crossover(stream, sizes=(1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 
 
         def host_call():
             _ck(lib.rse_encode_host(r._h, hptrs, lens, T, sh))
+
+        def now():
+            _ck(lib.rse_encode_now(r._h, ptrs, lens, T))
         row = {"shard_bytes": L, "gpu_call_device_us": round(per_call_us(dev), 2),
                "gpu_call_host_us": round(per_call_us(host_call), 2)}
+        st.synchronize()
+        row["gpu_call_now_us"] = round(per_call_us(now), 2)
         c = cpu_reference_call_us(k, p, L, None)
         row["cpu_reference_call_us"] = round(c, 2) if c is not None else None
         rows.append(row)
         del dv
-    out = {"what": "10+4 encode, one stripe per synchronous call (device shards; pageable host "
-                   "shards; reference CPU kernel, 1 thread)", "rows": rows}
-    for key in ("gpu_call_device_us", "gpu_call_host_us"):
+    out = {"what": "10+4 encode, one stripe per synchronous call (device shards: rse_encode + "
+                   "stream synchronisation, and rse_encode_now; pageable host shards; reference "
+                   "CPU kernel, 1 thread)", "rows": rows}
+    for key in ("gpu_call_device_us", "gpu_call_now_us", "gpu_call_host_us"):
         win = [x["shard_bytes"] for x in rows
                if x["cpu_reference_call_us"] is not None and x[key] < x["cpu_reference_call_us"]]
         out[f"{key.replace('_us', '')}_beats_cpu_from_shard_bytes"] = min(win) if win else None

@@ -159,20 +159,33 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
       const uint32_t tag0 = __shfl(g0.x, 0);
       const uint32_t n_gran = (__shfl(g0.y, 0) >> 20) & 0xFFFu;
       if (tag0 != seen && n_gran >= 1 && n_gran <= (uint32_t)kMaxGranules) {
-        dw4 m[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-        if (n_gran > 64u) {
-          for (int q = 0; q < 3; ++q)
-            if (lane + 64u * (q + 1) < n_gran) m[q] = load_sys16_nowait(ring + lane + 64u * (q + 1));
-          wait_loads(m[0], m[1], m[2]);
-        }
         bool ok = lane >= n_gran || g0.x == tag0;
-        for (int q = 0; q < 3; ++q)
-          if (lane + 64u * (q + 1) < n_gran) ok = ok && m[q].x == tag0;
-        if (__all(ok)) {  // every granule of the request is this request's
+        if (n_gran > 64u) {
+          // granules 64..255: three more loads, all lanes (the ring holds 256,
+          // so no lane's address is out of bounds), waited for together.  The
+          // loaded registers are used only inside this block (no phi of an
+          // asm output that might be copied before the wait).
+          dw4 m0 = load_sys16_nowait(ring + lane + 64u);
+          dw4 m1 = load_sys16_nowait(ring + lane + 128u);
+          dw4 m2 = load_sys16_nowait(ring + lane + 192u);
+          wait_loads(m0, m1, m2);
+          ok = ok && (lane + 64u >= n_gran || m0.x == tag0) &&
+               (lane + 128u >= n_gran || m1.x == tag0) && (lane + 192u >= n_gran || m2.x == tag0);
+          if (__all(ok)) {  // every granule of the request is this request's
+            dw4* q = reinterpret_cast<dw4*>(req);
+            q[lane] = g0;
+            if (lane + 64u < n_gran) q[lane + 64u] = m0;
+            if (lane + 128u < n_gran) q[lane + 128u] = m1;
+            if (lane + 192u < n_gran) q[lane + 192u] = m2;
+            state = 1;
+          }
+        } else if (__all(ok)) {
           reinterpret_cast<dw4*>(req)[lane] = g0;
-          for (int q = 0; q < 3; ++q)
-            if (lane + 64u * (q + 1) < n_gran) reinterpret_cast<dw4*>(req)[lane + 64u * (q + 1)] = m[q];
-          state = (__shfl(g0.y, 0) & 0xFu) == kOpStop ? 2u : 1u;  // a stop request ends it now
+          state = 1;
+        }
+        if (state == 1) {
+          // a stop request ends the kernel now
+          if ((__shfl(g0.y, 0) & 0xFu) == kOpStop) state = 2;
           seen = tag0;
         }
       }

@@ -18,6 +18,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-erasure_amd"))
+# the tree's prebuilt run-time modules (tools/prebuild_all.sh), as bench.py
+os.environ.setdefault("RSE_JIT_CACHE_DIR", os.path.join(ROOT, "jitcache"))
 
 import torch  # noqa: E402
 
