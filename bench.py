@@ -426,13 +426,11 @@ def compact_line(line, full, full_path):
     c = {key: line[key] for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
                                     "ms_per_step", "higher_is_better", "scaling",
                                     "vs_baseline", "dtype", "data")}
-    c["config"] = {key: x for key, x in line["config"].items()
-                   if key not in ("parity_check_per_rank", "parity_checked_stripes_rank0")}
+    c["config"] = dict(line["config"])  # incl. every rank's verdict (N ints)
     coll = line.get("collective") or {}
     c["collective"] = {key: coll.get(key) for key in ("backend", "world_size", "distinct_gpus",
                                                       "rehearsal")}
-    roof = {key: x for key, x in line["roofline"].items()
-            if key not in ("kernel_ms_per_launch_per_rank", "traffic_source")}
+    roof = {key: x for key, x in line["roofline"].items() if key != "traffic_source"}
     src = line["roofline"].get("traffic_source")
     roof["traffic_file"] = src.get("file") if src else None
     c["roofline"] = roof
@@ -935,7 +933,7 @@ def other_configs(stream):
 # parity rows (rse_jit.cpp jit_register_blocks), prebuilt into jitcache/ by
 # tools/prebuild_all.sh.  (A one-module GF(2^16) 256+16 did not finish
 # compiling in 25 minutes of hiprtc on the build host.)
-GF16_PROPER = (1000, 24, 64 << 10, 32)
+GF16_PROPER = (1000, 24, 64 << 10, 128)
 
 
 def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROPER[2],
@@ -957,9 +955,7 @@ def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROP
     assert T > 256, "GF(2^16) proper: past the subfield's 256 shards"
     buf = torch.empty(stripes * T * nbytes, dtype=torch.uint8, device="cuda")
     v = buf.view(stripes, T, nbytes)
-    for s_ in range(stripes):
-        for i in range(k):  # (shard_id's 8-bit shard field is too small for k = 1000)
-            fill_splitmix(v[s_, i], SEED, (0x16 << 40) | (s_ << 16) | i)
+    fill_splitmix(buf, SEED, 0x16 << 40)  # one stream over everything; encode overwrites parity
     r = R.core.ReedSolomon(k, p, 16)
     t0 = time.perf_counter()
     kind = r.kernel_kind(wait=True)

@@ -410,6 +410,9 @@ void rse_dispatcher_stop(void);
                                         (default 32768) */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
+#define RSE_OPT_WIDE_GRID 44          /* wide-module launches: 0 fixed workgroup counts (8192
+                                        GF(2^8), 16384 GF(2^16)); m > 0: m x the workgroups the
+                                        device holds at once (occupancy of the module) */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

@@ -85,6 +85,7 @@ struct Entry {
     int dev;
     bool have_rec = false;
     JitFns fns;
+    uint32_t wide_cap[3] = {};  // kJitWide: resident workgroups on the device (4 KiB, 1, 2 KiB kernels)
   };
   std::vector<Loaded> loaded;
 };
@@ -853,6 +854,7 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   hipError_t he = hipGetDevice(&dev);
   if (he != hipSuccess) return he;
   hipFunction_t fn = nullptr;
+  uint32_t cap = 0;
   {
     std::lock_guard<std::mutex> g(e->mu);
     const Entry::Loaded* have = nullptr;
@@ -875,10 +877,22 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
         (void)hipModuleUnload(m);
         return he;
       }
+      // how many workgroups of each kernel the device holds at once
+      // (RSE_OPT_WIDE_GRID sizes launches in multiples of it)
+      int n_cu = 0;
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+        for (int q = 0; q < 3; ++q) {
+          int per = 0;
+          const hipFunction_t f = q == 0 ? l.fns.wide : l.fns.wide_sub[q - 1];
+          if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 64 * c->wide_w, 0) ==
+              hipSuccess)
+            l.wide_cap[q] = (uint32_t)(per > 0 ? per : 0) * (uint32_t)n_cu;
+        }
       e->loaded.push_back(l);
       have = &e->loaded.back();
     }
     fn = subq ? have->fns.wide_sub[subq - 1] : have->fns.wide;
+    cap = have->wide_cap[subq];
   }
   // argument block: header, then the k input, p output and p compare pointers
   std::vector<uint8_t> buf(sizeof(WideHdr) + sizeof(void*) * (k + 2 * (size_t)p), 0);
@@ -907,7 +921,12 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   // tools/tune.py grid sweeps, 128 stripes x 1 MiB (profiles/r04/s2/): GF(2^16)
   // 40+12 16384 workgroups 5.29 TB/s against 5.05 at 4096; GF(2^8) 50+20 flat
   // from 2048 to 8192 (4.72), 4.68 at 16384
-  uint64_t gx = grid > 0 ? (uint64_t)grid : field == 16 ? 16384u : 8192u;
+  // RSE_OPT_WIDE_GRID m > 0: m x the workgroups the device holds at once
+  const int64_t mult = get_option(44);
+  uint64_t gx = grid > 0                ? (uint64_t)grid
+                : (mult > 0 && cap > 0) ? (uint64_t)mult * cap
+                : field == 16           ? 16384u
+                                        : 8192u;
   if (gx > total) gx = total;
   if (gx > 0x7fffffffu) gx = 0x7fffffffu;
   const int W = c->wide_w;  // the module's own workgroup shape

@@ -801,6 +801,7 @@ struct Options {
   int64_t dispatch = 1;           // *_now calls on the resident dispatcher (rse_dispatch.hip)
   int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
   int64_t dispatch_max_bytes = 32768;  // shard bytes up to which a *_now call is dispatched
+  int64_t wide_grid = 0;          // wide launches: 0 fixed workgroup counts, m > 0 m x resident
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1344,6 +1345,7 @@ int set_option(int key, int64_t value) {
     case 39: g_opt.dispatch = value ? 1 : 0; return 0;
     case 40: g_opt.dispatch_idle_us = value < 10 ? 10 : value > 1000000 ? 1000000 : value; return 0;
     case 41: g_opt.dispatch_max_bytes = value < 0 ? 0 : value; return 0;
+    case 44: g_opt.wide_grid = value < 0 ? 0 : value > 64 ? 64 : value; return 0;
     default: return -1;
   }
 }
@@ -1397,6 +1399,7 @@ int64_t get_option(int key) {
     case 39: return g_opt.dispatch;
     case 40: return g_opt.dispatch_idle_us;
     case 41: return g_opt.dispatch_max_bytes;
+    case 44: return g_opt.wide_grid;
     default: return -1;
   }
 }

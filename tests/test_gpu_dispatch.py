@@ -169,13 +169,15 @@ def test_dispatcher_idles_out_and_comes_back(R):
         for i in range(p):
             assert (t[k + i].cpu().numpy() == full[k + i]).all()
         lib.rse_set_option(IDLE_US, 1000000)
-        r.encode_now(t)
+        lib.rse_dispatcher_stop()
+        r.encode_now(t)  # a kernel that would stay for 1 s
         t0 = time.perf_counter()
-        lib.rse_dispatcher_stop()  # ends the 1 s-idle kernel now
+        lib.rse_dispatcher_stop()  # ends it now
         torch.cuda.synchronize()
         assert time.perf_counter() - t0 < 0.5
+        l1 = lib.rse_get_option(LAUNCHES)
         r.encode_now(t)
-        assert lib.rse_get_option(LAUNCHES) - l0 == 4
+        assert lib.rse_get_option(LAUNCHES) - l1 == 1
     finally:
         lib.rse_set_option(IDLE_US, old)
         lib.rse_dispatcher_stop()

@@ -1452,7 +1452,7 @@ def test_all_kernel_variants_and_launch_shapes(R, field, k, p):
 
 # ------------------------------------------------------------ bench, N > 1
 @pytest.mark.parametrize("ranks,extras", [(2, False), (4, True)])
-def test_bench_ranks_rehearsal(ranks, extras):
+def test_bench_ranks_rehearsal(ranks, extras, tmp_path):
     """bench.py's multi-rank path (torch.distributed.run, barrier, max-over-
     ranks timing, whole-job value) with `ranks` ranks sharing the one GPU over
     gloo.  Every rank checks its own first and last stripe against the
@@ -1466,7 +1466,8 @@ def test_bench_ranks_rehearsal(ranks, extras):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={ranks}", "--master-addr", "127.0.0.1", "--master-port",
            str(29533 + ranks), os.path.join(root, "bench.py"), "--gpus", str(ranks), "--steps",
-           "2", "--warmup", "1", "--stripes", "4", "--no-cpu"] + ([] if extras else ["--no-extras"])
+           "2", "--warmup", "1", "--stripes", "4", "--no-cpu",
+           "--full-out", str(tmp_path / "full.json")] + ([] if extras else ["--no-extras"])
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -1487,8 +1488,11 @@ def test_bench_ranks_rehearsal(ranks, extras):
     assert all(x["device"] == "cuda:0" and x["pci"] for x in coll["rank_devices"])
     assert coll["distinct_gpus"] is False
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
+    assert len(json.dumps(d)) < 4096  # the printed line stays compact at N ranks
+    full = json.load(open(tmp_path / "full.json"))  # every leg
+    assert full["config"] == d["config"] and full["value"] == d["value"]
     if extras:
-        h = d["end_to_end_host_all_ranks"]
+        h = full["end_to_end_host_all_ranks"]
         assert h["ranks"] == ranks and h["parity_matches_device_all_ranks"] is True
 
 
