@@ -811,9 +811,14 @@ uint32_t wide_per_wave() {
   return v >= 2 && v <= (int64_t)kJitMaxOut ? (uint32_t)v : kJitMaxOut;
 }
 
+// One module for k > 32 or p > per outputs per wave (RSE_OPT_WIDE_SPLIT), up to
+// 8 waves -- or, with fewer outputs per wave than the default 8, up to 16
+// waves (1024 lanes) for the same p <= 64 (e.g. 64+64 at 4 outputs per wave).
 bool wide_eligible(uint32_t k, uint32_t p) {
   const uint32_t per = wide_per_wave();
-  return k >= 1 && p >= 1 && (k > (uint32_t)kMaxIn || p > per) && p <= per * 8u &&
+  const bool fits = p <= per * 8u || (per < kJitMaxOut && p <= kJitMaxOut * 8u &&
+                                      (p + per - 1) / per <= 16u);
+  return k >= 1 && p >= 1 && (k > (uint32_t)kMaxIn || p > per) && fits &&
          k + 2u * p <= kWideMaxPtrs;
 }
 
