@@ -408,6 +408,9 @@ void rse_dispatcher_stop(void);
                                         without a call (default 2000) */
 #define RSE_OPT_DISPATCH_MAX_BYTES 41 /* shard bytes up to which a *_now call is dispatched
                                         (default 32768) */
+#define RSE_OPT_DISPATCH_WORKGROUPS 45 /* workgroups of the resident dispatcher (1..64, default 8):
+                                        a request is coded by as many as its size needs; only
+                                        the first polls more than 16 bytes per poll. Read at launch */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: 0 fixed workgroup counts (8192

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -54,6 +55,7 @@ constexpr int kDispThreads = 512;       // one workgroup, 8 waves (256 VGPRs: no
 constexpr int kMaxGranules = 256;       // 4 KiB of request
 constexpr uint32_t kDispMaxIn = 64, kDispMaxOut = 64, kDispMaxCoef = 1024;
 constexpr uint64_t kAckExit = 1ull << 32, kAckMismatch = 1ull << 33;
+constexpr uint32_t kMaxDispWgs = 64, kAckStride = 8;  // one 64-byte line per workgroup's ack
 constexpr uint32_t kOpCode = 0, kOpCheck = 1, kOpStop = 2;  // granule 0's a & 0xF
 
 struct alignas(16) Granule {
@@ -71,8 +73,13 @@ __device__ __forceinline__ dw4 load_sys16_nowait(const Granule* g) {
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(g) : "memory");
   return v;
 }
-__device__ __forceinline__ void wait_loads(dw4& a) {
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a)::"memory");
+__device__ __forceinline__ dw4 load_sys16_wait(const Granule* g) {  // one asm: load + wait
+  dw4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v)
+               : "v"(g)
+               : "memory");
+  return v;
 }
 __device__ __forceinline__ void wait_loads(dw4& a, dw4& b, dw4& c) {
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c)::"memory");
@@ -88,11 +95,12 @@ __device__ __forceinline__ uint64_t now_ticks() {  // 100 MHz constant clock
 // (check mode).
 template <int OB>
 __device__ bool code_items(const Granule* req, uint32_t n_in, uint32_t n_out, uint64_t n_vec,
-                           bool check, const uint4* tq, const uint32_t* tt) {
+                           bool check, const uint4* tq, const uint32_t* tt, uint32_t n_wg) {
   bool diff = false;
   const uint32_t n_ob = (n_out + OB - 1) / OB;
   const uint64_t items = n_vec * n_ob;
-  for (uint64_t it = threadIdx.x; it < items; it += kDispThreads) {
+  for (uint64_t it = (uint64_t)blockIdx.x * kDispThreads + threadIdx.x; it < items;
+       it += (uint64_t)n_wg * kDispThreads) {
     const uint32_t ob = (uint32_t)(it / n_vec);
     const uint64_t off = (it - (uint64_t)ob * n_vec) * 16u;
     const uint32_t o0 = ob * OB;
@@ -137,56 +145,67 @@ __device__ bool code_items(const Granule* req, uint32_t n_in, uint32_t n_out, ui
   return diff;
 }
 
-// The resident workgroup.  ring: the request granules (device view of pinned
-// host memory); ack: the pinned ack word.  seen: the last sequence number
-// served before this launch.
+// The resident workgroups.  ring: the request granules (device view of pinned
+// host memory); acks: one pinned ack word per workgroup, kAckStride words
+// apart.  seen: the last sequence number served before this launch.
+// Workgroup 0 polls the first 64 granules every time (the whole of a small
+// request in one PCIe read); the others poll granule 0 alone and read the
+// request once its tag is new (a second round trip, but 16 bytes per poll).
+// A request names how many workgroups code it (n_wg, the first n_wg); the
+// others only take note of it.
 __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granule* ring,
-                                                                    uint64_t* ack, uint32_t seen,
+                                                                    uint64_t* acks, uint32_t seen,
                                                                     uint64_t idle_ticks) {
   __shared__ Granule req[kMaxGranules];
   __shared__ uint4 tq[kDispMaxCoef];
   __shared__ uint32_t tt[kDispMaxCoef];
-  __shared__ uint32_t s_state;  // 0 idle, 1 request in req[], 2 exit
+  __shared__ uint32_t s_state;  // 0 idle, 1 request in req[], 2 exit, 3 seen, not ours
   __shared__ uint32_t s_diff;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const bool lead = blockIdx.x == 0;
+  uint64_t* ack = acks + (size_t)blockIdx.x * kAckStride;
   uint64_t last = now_ticks();
   for (;;) {
     if (wave == 0) {
-      // one poll: granules lane, lane + 64, ... of the request as far as needed
       uint32_t state = 0;
-      dw4 g0 = load_sys16_nowait(ring + lane);
-      wait_loads(g0);
-      const uint32_t tag0 = __shfl(g0.x, 0);
-      const uint32_t n_gran = (__shfl(g0.y, 0) >> 20) & 0xFFFu;
-      if (tag0 != seen && n_gran >= 1 && n_gran <= (uint32_t)kMaxGranules) {
-        bool ok = lane >= n_gran || g0.x == tag0;
-        if (n_gran > 64u) {
-          // granules 64..255: three more loads, all lanes (the ring holds 256,
-          // so no lane's address is out of bounds), waited for together.  The
-          // loaded registers are used only inside this block (no phi of an
-          // asm output that might be copied before the wait).
-          dw4 m0 = load_sys16_nowait(ring + lane + 64u);
-          dw4 m1 = load_sys16_nowait(ring + lane + 128u);
-          dw4 m2 = load_sys16_nowait(ring + lane + 192u);
-          wait_loads(m0, m1, m2);
-          ok = ok && (lane + 64u >= n_gran || m0.x == tag0) &&
-               (lane + 128u >= n_gran || m1.x == tag0) && (lane + 192u >= n_gran || m2.x == tag0);
-          if (__all(ok)) {  // every granule of the request is this request's
-            dw4* q = reinterpret_cast<dw4*>(req);
-            q[lane] = g0;
-            if (lane + 64u < n_gran) q[lane + 64u] = m0;
-            if (lane + 128u < n_gran) q[lane + 128u] = m1;
-            if (lane + 192u < n_gran) q[lane + 192u] = m2;
+      const dw4 p0 = load_sys16_wait(ring + (lead ? lane : 0u));
+      const uint32_t tag0 = __shfl(p0.x, 0);
+      if (tag0 != seen) {
+        // the request's granules lane, lane + 64, ...
+        const dw4 g0 = lead ? p0 : load_sys16_wait(ring + lane);
+        const uint32_t tag = __shfl(g0.x, 0);
+        const uint32_t n_gran = (__shfl(g0.y, 0) >> 20) & 0xFFFu;
+        if (tag == tag0 && n_gran >= 1 && n_gran <= (uint32_t)kMaxGranules) {
+          bool ok = lane >= n_gran || g0.x == tag0;
+          if (n_gran > 64u) {
+            // granules 64..255: three more loads, all lanes (the ring holds
+            // 256, so no lane's address is out of bounds), waited for
+            // together; the loaded registers are used only inside this block
+            // (no phi of an asm output that might be copied before the wait)
+            dw4 m0 = load_sys16_nowait(ring + lane + 64u);
+            dw4 m1 = load_sys16_nowait(ring + lane + 128u);
+            dw4 m2 = load_sys16_nowait(ring + lane + 192u);
+            wait_loads(m0, m1, m2);
+            ok = ok && (lane + 64u >= n_gran || m0.x == tag0) &&
+                 (lane + 128u >= n_gran || m1.x == tag0) && (lane + 192u >= n_gran || m2.x == tag0);
+            if (__all(ok)) {  // every granule of the request is this request's
+              dw4* q = reinterpret_cast<dw4*>(req);
+              q[lane] = g0;
+              if (lane + 64u < n_gran) q[lane + 64u] = m0;
+              if (lane + 128u < n_gran) q[lane + 128u] = m1;
+              if (lane + 192u < n_gran) q[lane + 192u] = m2;
+              state = 1;
+            }
+          } else if (__all(ok)) {
+            reinterpret_cast<dw4*>(req)[lane] = g0;
             state = 1;
           }
-        } else if (__all(ok)) {
-          reinterpret_cast<dw4*>(req)[lane] = g0;
-          state = 1;
-        }
-        if (state == 1) {
-          // a stop request ends the kernel now
-          if ((__shfl(g0.y, 0) & 0xFu) == kOpStop) state = 2;
-          seen = tag0;
+          if (state == 1) {
+            seen = tag0;
+            const uint32_t n_wg = (uint32_t)(__shfl(g0.w, 0) >> 16) & 0xFFu;  // b bits 48..55
+            if ((__shfl(g0.y, 0) & 0xFu) == kOpStop) state = 2;  // a stop request: end now
+            else if (blockIdx.x >= n_wg) state = 3;              // not one of its workgroups
+          }
         }
       }
       if (state == 0 && now_ticks() - last > idle_ticks) state = 2;
@@ -198,18 +217,20 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
     __syncthreads();
     const uint32_t state = s_state;
     if (state == 2) break;
-    if (state == 0) {
+    if (state != 1) {
+      if (state == 3) last = now_ticks();  // the others are busy: not idle
       __syncthreads();  // s_state is rewritten by wave 0 only after everyone read it
       continue;
     }
     // the request: granule 0 {tag, op | n_in << 4 | n_out << 12 | n_gran << 20,
-    // len | outputs per work item << 56},
+    // len | n_wg << 48 | outputs per work item << 56},
     // then n_in input and n_out output pointers, then the coefficients (12 per
     // granule, row-major by output, in a then b)
     const uint32_t hdr = req[0].a;
     const bool check = (hdr & 0xFu) == kOpCheck;
     const uint32_t n_in = (hdr >> 4) & 0xFFu, n_out = (hdr >> 12) & 0xFFu;
     const uint64_t len = req[0].b & ((1ull << 48) - 1);
+    const uint32_t n_wg = (uint32_t)(req[0].b >> 48) & 0xFFu;
     const uint32_t n_coef = n_in * n_out;
     for (uint32_t c = tid; c < n_coef; c += kDispThreads) {
       const Granule& g = req[1 + n_in + n_out + c / 12u];
@@ -221,13 +242,13 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
     }
     __syncthreads();
     const uint64_t n_vec = len / 16u;
-    // outputs per item: enough items for the workgroup's threads, at most 8
-    const uint32_t ob = (uint32_t)(req[0].b >> 56);
+    // outputs per item: enough items for the threads, at most 8
+    const uint32_t ob = (uint32_t)(req[0].b >> 56) & 0xFu;
     bool diff;
-    if (ob <= 1) diff = code_items<1>(req, n_in, n_out, n_vec, check, tq, tt);
-    else if (ob == 2) diff = code_items<2>(req, n_in, n_out, n_vec, check, tq, tt);
-    else if (ob <= 4) diff = code_items<4>(req, n_in, n_out, n_vec, check, tq, tt);
-    else diff = code_items<8>(req, n_in, n_out, n_vec, check, tq, tt);
+    if (ob <= 1) diff = code_items<1>(req, n_in, n_out, n_vec, check, tq, tt, n_wg);
+    else if (ob == 2) diff = code_items<2>(req, n_in, n_out, n_vec, check, tq, tt, n_wg);
+    else if (ob <= 4) diff = code_items<4>(req, n_in, n_out, n_vec, check, tq, tt, n_wg);
+    else diff = code_items<8>(req, n_in, n_out, n_vec, check, tq, tt, n_wg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this thread landed
     if (diff) atomicOr(&s_diff, 1u);
     __syncthreads();
@@ -249,10 +270,11 @@ struct Dispatcher {
   hipStream_t st = nullptr;
   Granule* req = nullptr;  // pinned, mapped: host view
   Granule* dreq = nullptr;
-  uint64_t* ack = nullptr;
+  uint64_t* ack = nullptr;  // kMaxDispWgs ack words, kAckStride apart
   uint64_t* dack = nullptr;
   uint32_t seq = 0;     // the last request posted
   uint32_t served = 0;  // the last request acknowledged
+  uint32_t n_wgs = 1;   // workgroups of the running kernel
 };
 constexpr int kDispDevs = 64;
 Dispatcher& dispatcher(int dev) {
@@ -268,23 +290,30 @@ hipError_t disp_init(Dispatcher& d) {
     e = hipHostMalloc(reinterpret_cast<void**>(&d.req), sizeof(Granule) * kMaxGranules + 64,
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess)
-    e = hipHostMalloc(reinterpret_cast<void**>(&d.ack), 64, hipHostMallocMapped | hipHostMallocCoherent);
+    e = hipHostMalloc(reinterpret_cast<void**>(&d.ack), sizeof(uint64_t) * kAckStride * kMaxDispWgs,
+                      hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dreq), d.req, 0);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dack), d.ack, 0);
   if (e != hipSuccess) return e;
   std::memset(d.req, 0, sizeof(Granule) * kMaxGranules);
-  *reinterpret_cast<volatile uint64_t*>(d.ack) = 0;
+  std::memset(d.ack, 0, sizeof(uint64_t) * kAckStride * kMaxDispWgs);
   d.init = true;
   return hipSuccess;
 }
 
 // A kernel that starts from the last request served (a posted one is new to
 // it); the ack starts there too, never at a stale EXIT.
-hipError_t disp_launch(Dispatcher& d) {
-  *reinterpret_cast<volatile uint64_t*>(d.ack) = (uint64_t)d.served;
+// at_least: the workgroups a pending request names (the option may have
+// changed since it was posted).
+hipError_t disp_launch(Dispatcher& d, uint32_t at_least = 1) {
+  const int64_t g = get_option(45);  // RSE_OPT_DISPATCH_WORKGROUPS
+  d.n_wgs = std::max<uint32_t>(at_least,
+                               (uint32_t)(g < 1 ? 1 : g > (int64_t)kMaxDispWgs ? kMaxDispWgs : g));
+  for (uint32_t w = 0; w < kMaxDispWgs; ++w)
+    reinterpret_cast<volatile uint64_t*>(d.ack)[w * kAckStride] = (uint64_t)d.served;
   const int64_t idle_us = get_option(40);
-  hipLaunchKernelGGL(rse_dispatch_kernel, dim3(1), dim3(kDispThreads), 0, d.st, d.dreq, d.dack,
-                     d.served, (uint64_t)(idle_us < 1 ? 1 : idle_us) * 100u);
+  hipLaunchKernelGGL(rse_dispatch_kernel, dim3(d.n_wgs), dim3(kDispThreads), 0, d.st, d.dreq,
+                     d.dack, d.served, (uint64_t)(idle_us < 1 ? 1 : idle_us) * 100u);
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess) {
     d.running = true;
@@ -325,10 +354,18 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
   if ((e = disp_init(d)) != hipSuccess) return e;
   const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;  // 0: the zeroed ring
   const uint32_t n_gran = 1 + n_in + n_out + (n_in * n_out + 11) / 12;
-  // outputs per work item: items (vectors x output blocks) for the threads
+  // workgroups that code it: ~2 (16-byte vector, output) units per lane, as
+  // many as the running kernel has; outputs per work item: items (vectors x
+  // output blocks) for their lanes
   const uint64_t n_vec = len_bytes / 16u;
+  if (!d.running) d.n_wgs = (uint32_t)std::min<int64_t>(std::max<int64_t>(get_option(45), 1),
+                                                          kMaxDispWgs);
+  const uint64_t units = n_vec * n_out;
+  const uint32_t n_wg = (uint32_t)std::min<uint64_t>(
+      d.n_wgs, std::max<uint64_t>(1, (units + 2 * kDispThreads - 1) / (2 * kDispThreads)));
+  const uint64_t lanes = (uint64_t)n_wg * kDispThreads;
   uint32_t ob = 1;
-  while (ob < 8 && n_vec * ((n_out + 2 * ob - 1) / (2 * ob)) >= (uint64_t)kDispThreads) ob *= 2;
+  while (ob < 8 && n_vec * ((n_out + 2 * ob - 1) / (2 * ob)) >= lanes) ob *= 2;
   volatile Granule* r = d.req;
   for (uint32_t i = 0; i < n_in; ++i) {
     r[1 + i].a = 0;
@@ -351,42 +388,52 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
   }
   for (uint32_t q = 1; q < n_gran; ++q) r[q].tag = seq;
   r[0].a = (check ? kOpCheck : kOpCode) | (n_in << 4) | (n_out << 12) | (n_gran << 20);
-  r[0].b = len_bytes | ((uint64_t)ob << 56);
+  r[0].b = len_bytes | ((uint64_t)n_wg << 48) | ((uint64_t)ob << 56);
   std::atomic_thread_fence(std::memory_order_release);
   r[0].tag = seq;  // the request is posted
   d.seq = seq;
   if (!d.running) {
-    if ((e = disp_launch(d)) != hipSuccess) return e;
+    if ((e = disp_launch(d, n_wg)) != hipSuccess) return e;
   }
-  volatile uint64_t* ack = d.ack;
+  // every coding workgroup's ack.  A workgroup that idled out before it saw
+  // the request (EXIT without this seq): wait for the whole kernel to end and
+  // launch again -- the new one serves the request in full (coding it twice
+  // writes the same bytes: no request's inputs are its outputs).
+  const volatile uint64_t* ack = d.ack;
   const auto t0 = std::chrono::steady_clock::now();
-  for (uint64_t n = 1;; ++n) {
-    const uint64_t a = *ack;
-    if ((uint32_t)a == seq && !(a & kAckExit)) {
-      d.served = seq;
-      if (mismatch) *mismatch = (a & kAckMismatch) != 0;
-      ++g_dispatched;
-      return hipSuccess;
-    }
-    if (a & kAckExit) {  // the kernel idled out before it saw this request
+  bool mm = false;
+  for (uint32_t w = 0; w < n_wg;) {
+    for (uint64_t n = 1;; ++n) {
+      const uint64_t a = ack[w * kAckStride];
+      if ((uint32_t)a == seq && !(a & kAckExit)) {
+        mm = mm || (a & kAckMismatch) != 0;
+        ++w;
+        break;
+      }
+      bool again = (a & kAckExit) != 0;
+      if (!again) {
+        __builtin_ia32_pause();
+        if ((n & 4095u) != 0) continue;
+        // a launch that failed, or a kernel that died, ends the wait
+        const hipError_t q = hipStreamQuery(d.st);
+        if (q != hipErrorNotReady && q != hipSuccess) return q;
+        again = q == hipSuccess && ack[w * kAckStride] == a;  // ended without our ack
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+          return hipErrorLaunchTimeOut;
+        if (!again) continue;
+      }
       if ((e = hipStreamSynchronize(d.st)) != hipSuccess) return e;
       d.running = false;
-      if ((e = disp_launch(d)) != hipSuccess) return e;
-      continue;
-    }
-    __builtin_ia32_pause();
-    if ((n & 4095u) == 0) {
-      // a launch that failed, or a kernel that died, ends the wait
-      const hipError_t q = hipStreamQuery(d.st);
-      if (q != hipErrorNotReady && q != hipSuccess) return q;
-      if (q == hipSuccess && *ack == a) {  // ended without an ack for us: run again
-        d.running = false;
-        if ((e = disp_launch(d)) != hipSuccess) return e;
-      }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-        return hipErrorLaunchTimeOut;
+      if ((e = disp_launch(d, n_wg)) != hipSuccess) return e;
+      w = 0;  // every workgroup again
+      mm = false;
+      break;
     }
   }
+  d.served = seq;
+  if (mismatch) *mismatch = mm;
+  ++g_dispatched;
+  return hipSuccess;
 }
 
 // Ends the resident kernel of every device this process started one on: a

@@ -802,6 +802,7 @@ struct Options {
   int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
   int64_t dispatch_max_bytes = 32768;  // shard bytes up to which a *_now call is dispatched
   int64_t wide_grid = 0;          // wide launches: 0 fixed workgroup counts, m > 0 m x resident
+  int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1346,6 +1347,7 @@ int set_option(int key, int64_t value) {
     case 40: g_opt.dispatch_idle_us = value < 10 ? 10 : value > 1000000 ? 1000000 : value; return 0;
     case 41: g_opt.dispatch_max_bytes = value < 0 ? 0 : value; return 0;
     case 44: g_opt.wide_grid = value < 0 ? 0 : value > 64 ? 64 : value; return 0;
+    case 45: g_opt.dispatch_wgs = value < 1 ? 1 : value > 64 ? 64 : value; return 0;
     default: return -1;
   }
 }
@@ -1400,6 +1402,7 @@ int64_t get_option(int key) {
     case 40: return g_opt.dispatch_idle_us;
     case 41: return g_opt.dispatch_max_bytes;
     case 44: return g_opt.wide_grid;
+    case 45: return g_opt.dispatch_wgs;
     default: return -1;
   }
 }

@@ -233,3 +233,26 @@ def test_now_c_abi_latency(R):
         lib.rse_encode_now(r._h, ptrs, lens, k + p)
     us = (time.perf_counter() - t0) / 200 * 1e6
     assert us < 15, us
+
+
+@pytest.mark.parametrize("wgs", [1, 3, 8, 32])
+def test_now_dispatcher_workgroup_counts(R, wgs):
+    """RSE_OPT_DISPATCH_WORKGROUPS: the resident kernel's workgroups split a
+    request's (vector, output block) items; every count gives the oracle's
+    bytes for encode, verify and reconstruct, at sizes that use one and all
+    of them (up to 256 KiB shards with the size limit raised)."""
+    lib = R._lib.load()
+    WGS = 45
+    old = [lib.rse_get_option(x) for x in (WGS, MAX_BYTES)]
+    try:
+        lib.rse_set_option(WGS, wgs)
+        lib.rse_set_option(MAX_BYTES, 1 << 18)
+        lib.rse_dispatcher_stop()  # the next call launches with `wgs` workgroups
+        for nbytes in (1024, 16384, 65536, 1 << 18):
+            d0 = lib.rse_get_option(DISPATCHED)
+            test_now_matches_oracle(R, 8, 10, 4, nbytes)
+            assert lib.rse_get_option(DISPATCHED) - d0 >= 1 + 3  # the encode and the verifies
+    finally:
+        lib.rse_set_option(WGS, old[0])
+        lib.rse_set_option(MAX_BYTES, old[1])
+        lib.rse_dispatcher_stop()

@@ -10,6 +10,7 @@
 //   G  rse_encode 10+4 x 1 KiB + hipStreamWriteValue32 of a pinned word, host spins
 //   H  empty kernel + hipStreamWriteValue32, host spins
 //   I  rse_encode_now 10+4 x 1 KiB (the resident dispatcher)
+//   J  rse_encode_now by shard size: 1, 8, 32 dispatcher workgroups, and the launch path
 // The resident kernel of E exits on a stop value or after a bounded number of
 // polls, so it always drains.
 //   hipcc --offload-arch=gfx950 -O2 -I include tools/latency_probe.hip \
@@ -181,6 +182,46 @@ int main() {
     CK(hipStreamSynchronize(st));
     d.report("D rse_encode 10+4 x 1 KiB, enqueue only");
     std::printf("   kernel: %s\n", rse_last_kernel());
+    rse_codec_free(c);
+    CK(hipFree(buf));
+  }
+  {  // J: rse_encode_now by shard size and dispatcher workgroups, against the launch path
+    rse_codec* c = nullptr;
+    if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
+    const size_t T = 14, Lmax = 1u << 20;
+    uint8_t* buf = nullptr;
+    CK(hipMalloc(reinterpret_cast<void**>(&buf), T * Lmax));
+    CK(hipMemset(buf, 7, T * Lmax));
+    rse_set_option(RSE_OPT_DISPATCH_MAX_BYTES, (int64_t)Lmax);
+    for (size_t L : {1024u, 4096u, 16384u, 65536u, 262144u, 1048576u}) {
+      std::vector<void*> sh(T);
+      std::vector<size_t> lens(T, L);
+      for (size_t i = 0; i < T; ++i) sh[i] = buf + i * L;
+      char name[96];
+      for (int wgs : {1, 8, 32, 0}) {
+        Stat g;
+        if (wgs) {
+          rse_set_option(RSE_OPT_DISPATCH, 1);
+          rse_set_option(RSE_OPT_DISPATCH_WORKGROUPS, wgs);
+          rse_dispatcher_stop();  // the next call launches with this many
+        } else {
+          rse_set_option(RSE_OPT_DISPATCH, 0);  // the launch path, waited for
+        }
+        const int n = L >= 262144 ? 300 : 1000;
+        for (int i = 0; i < n + 20; ++i) {
+          const auto t0 = clk::now();
+          if (rse_encode_now(c, sh.data(), lens.data(), T)) return 4;
+          if (i >= 20) g.v.push_back(us_since(t0));
+        }
+        if (wgs) std::snprintf(name, sizeof name, "J encode_now 10+4 x %zu KiB, %d workgroups", L >> 10, wgs);
+        else std::snprintf(name, sizeof name, "J encode_now 10+4 x %zu KiB, launch path", L >> 10);
+        g.report(name);
+      }
+    }
+    rse_set_option(RSE_OPT_DISPATCH, 1);
+    rse_set_option(RSE_OPT_DISPATCH_WORKGROUPS, 8);
+    rse_set_option(RSE_OPT_DISPATCH_MAX_BYTES, 32768);
+    rse_dispatcher_stop();
     rse_codec_free(c);
     CK(hipFree(buf));
   }
