@@ -1303,8 +1303,8 @@ def _ck(rc):
         raise RuntimeError(f"rse call failed with status {rc}")
 
 
-def per_call_crossover(stream, sizes=(1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10,
-                                      1 << 20, 4 << 20)):
+def per_call_crossover(stream, sizes=(1 << 10, 4 << 10, 8 << 10, 16 << 10, 32 << 10,
+                                      64 << 10, 256 << 10, 1 << 20, 4 << 20)):
     """One 10+4 stripe per synchronous encode call at growing shard sizes:
     device shards, pageable host shards and the reference CPU kernel, and the
     smallest size at which each GPU form beats the CPU."""

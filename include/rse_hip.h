@@ -407,7 +407,7 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_DISPATCH_IDLE_US 40   /* the resident dispatcher ends after this many microseconds
                                         without a call (default 2000) */
 #define RSE_OPT_DISPATCH_MAX_BYTES 41 /* shard bytes up to which a *_now call is dispatched
-                                        (default 32768) */
+                                        (default 65536) */
 #define RSE_OPT_DISPATCH_WORKGROUPS 45 /* workgroups of the resident dispatcher (1..64, default 8):
                                         a request is coded by as many as its size needs; only
                                         the first polls more than 16 bytes per poll. Read at launch */

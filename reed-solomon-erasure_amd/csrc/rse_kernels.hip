@@ -800,7 +800,7 @@ struct Options {
   int64_t wide_half = 1;          // GF(2^8) paired wide modules on 2 KiB chunks (one plane group)
   int64_t dispatch = 1;           // *_now calls on the resident dispatcher (rse_dispatch.hip)
   int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
-  int64_t dispatch_max_bytes = 32768;  // shard bytes up to which a *_now call is dispatched
+  int64_t dispatch_max_bytes = 65536;  // shard bytes up to which a *_now call is dispatched
   int64_t wide_grid = 0;          // wide launches: 0 fixed workgroup counts, m > 0 m x resident
   int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
 };

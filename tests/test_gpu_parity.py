@@ -1484,6 +1484,7 @@ def test_bench_ranks_rehearsal(ranks, extras, tmp_path):
     # rank's device gathered (all on the one GPU here, so not distinct)
     coll = d["collective"]
     assert coll["backend"] == "gloo" and coll["world_size"] == ranks and coll["rehearsal"]
+    coll = json.load(open(tmp_path / "full.json"))["collective"]  # with every rank's device
     assert len(coll["rank_devices"]) == ranks
     assert all(x["device"] == "cuda:0" and x["pci"] for x in coll["rank_devices"])
     assert coll["distinct_gpus"] is False
@@ -1503,6 +1504,22 @@ def test_bench_ranks_rehearsal(ranks, extras, tmp_path):
 WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
                (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9),
                (8, 32, 32, 1), (8, 64, 64, 1)]  # benches/bandwidth.rs:94-95's widest (half chunks)
+
+
+def test_wide_sixteen_waves(R):
+    """RSE_OPT_WIDE_SPLIT 4: 4 outputs per wave, so a 60+60 codec's module is
+    16 waves (1024 lanes, half chunks, paired networks, ~115 VGPRs); the same
+    bytes as the oracle for encode, verify and flat stripes.  A codec no other
+    test builds (modules are keyed by rows, not options)."""
+    from reed_solomon_erasure.core import last_kernel
+    lib = R._lib.load()
+    old = lib.rse_get_option(18)
+    try:
+        assert lib.rse_set_option(18, 4) == 0
+        test_wide_codec_kernels(R, 1, 8, 60, 60, 1)
+        assert last_kernel().startswith("bitslice-wide gf8 60+60 w16 half"), last_kernel()
+    finally:
+        lib.rse_set_option(18, old)
 
 
 def test_wide_full_chunks_option(R):

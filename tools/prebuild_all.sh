@@ -21,6 +21,8 @@ pat+=(--pattern "16:20:8:4194304:0,1,2,3")  # other_configs gf16_20_8 cached pat
 # tests/test_gpu_parity.py test_wide_full_chunks_option: one codec on full
 # (4 KiB) chunks, RSE_OPT_WIDE_HALF 0, in a process of its own
 python3 tools/prebuild_jit.py --set 38=0 --codec 8:34:10 || exit 1
+# test_wide_sixteen_waves: 4 outputs per wave (a 16-wave module)
+python3 tools/prebuild_jit.py --set 18=4 --codec 8:60:60 || exit 1
 exec python3 tools/prebuild_jit.py --codec 8:35:10 \
   --codec 8:50:20 --codec 16:40:12 --codec 16:100:30 \
   --codec 8:4:4 --codec 8:8:8 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 --codec 8:5:2 \
