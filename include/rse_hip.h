@@ -411,6 +411,10 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_DISPATCH_WORKGROUPS 45 /* workgroups of the resident dispatcher (1..64, default 8):
                                         a request is coded by as many as its size needs; only
                                         the first polls more than 16 bytes per poll. Read at launch */
+#define RSE_OPT_WIDE_BLOCK_INPUTS 46  /* codecs past one wide module (k + 2p > 480: GF(2^16) past
+                                        256 shards): a chain of wide modules over blocks of at
+                                        most this many data inputs, each coding every output
+                                        (default 128); 0: modules of 8 outputs x 32 inputs */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: 0 fixed workgroup counts (8192

@@ -229,6 +229,9 @@ def _check(rc):
         raise OracleError(rc)
 
 
+_SHARED = {}
+
+
 class Codec:
     """Checker-side ReedSolomon<F> (core.rs:343-923), numpy shards in, in place."""
 
@@ -238,6 +241,16 @@ class Codec:
         h = ctypes.c_void_p()
         _check(lib().oracle_codec_new(field, data_shards, parity_shards, ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def shared(cls, field, data_shards, parity_shards):
+        """One checker codec per shape per process: GF(2^16) past 256 shards
+        inverts a ~1000 x 1000 matrix in scalar C (about a minute)."""
+        key = (field, data_shards, parity_shards)
+        c = _SHARED.get(key)
+        if c is None:
+            c = _SHARED[key] = cls(field, data_shards, parity_shards)
+        return c
 
     def __del__(self):
         h = getattr(self, "_h", None)

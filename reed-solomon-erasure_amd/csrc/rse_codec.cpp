@@ -27,6 +27,7 @@
 
 #include "../../include/rse_hip.h"
 #include "rse_dispatch.hpp"
+#include "rse_wideblk.hpp"
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
 
@@ -227,6 +228,31 @@ bool bitslice_len(size_t len) {
   return len >= 4096 || ((len == 1024 || len == 2048) && rse::get_option(RSE_OPT_SUB_CHUNKS));
 }
 
+int run_job(const Job& j, hipStream_t s);
+
+// The bytes of every shard past `done` (a wide launch coded whole chunks up
+// to there); the wide launch stays the kernel rse_last_kernel reports.
+int run_rest(const Job& j, uint64_t done, hipStream_t s) {
+  const size_t n_out = j.rows->n_out, n_in = j.rows->n_in;
+  std::vector<const uint8_t*> in(j.in, j.in + n_in);
+  std::vector<uint8_t*> out(n_out, nullptr);
+  std::vector<const uint8_t*> cmp(n_out, nullptr);
+  for (auto& q : in) q += done;
+  for (size_t r = 0; r < n_out; ++r) {
+    if (j.out && j.out[r]) out[r] = j.out[r] + done;
+    if (j.cmp && j.cmp[r]) cmp[r] = j.cmp[r] + done;
+  }
+  Job rest = j;
+  rest.in = in.data();
+  rest.out = j.out ? out.data() : nullptr;
+  rest.cmp = j.cmp ? cmp.data() : nullptr;
+  rest.len_bytes = j.len_bytes - done;
+  const std::string wide_kernel = rse::last_kernel();  // the launch to report
+  const int rc = run_job(rest, s);
+  rse::note_kernel("%s", wide_kernel.c_str());
+  return rc;
+}
+
 // Executes a Job; `scratch` provides per-output buffers when a CHECK job must
 // be split over several input chunks (full sums are needed before comparing).
 int run_job(const Job& j, hipStream_t s) {
@@ -261,26 +287,22 @@ int run_job(const Job& j, hipStream_t s) {
       RSE_HIP(rse::launch_wide(j.field, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data(), j.in,
                                j.out, j.cmp, j.len_bytes, j.stripe_stride, (uint32_t)j.n_stripes,
                                j.mode, j.mismatch, j.per_stripe, s, &done));
-    if (done) {
-      if (done == j.len_bytes) return RSE_OK;
-      std::vector<const uint8_t*> in(j.in, j.in + n_in);
-      std::vector<uint8_t*> out(n_out, nullptr);
-      std::vector<const uint8_t*> cmp(n_out, nullptr);
-      for (auto& q : in) q += done;
-      for (size_t r = 0; r < n_out; ++r) {
-        if (j.out && j.out[r]) out[r] = j.out[r] + done;
-        if (j.cmp && j.cmp[r]) cmp[r] = j.cmp[r] + done;
-      }
-      Job rest = j;
-      rest.in = in.data();
-      rest.out = j.out ? out.data() : nullptr;
-      rest.cmp = j.cmp ? cmp.data() : nullptr;
-      rest.len_bytes = j.len_bytes - done;
-      const std::string wide_kernel = rse::last_kernel();  // the launch to report
-      const int rc = run_job(rest, s);
-      rse::note_kernel("%s", wide_kernel.c_str());
-      return rc;
-    }
+    if (done) return done == j.len_bytes ? RSE_OK : run_rest(j, done, s);
+  }
+  // too wide for one module (GF(2^16) past 256 shards): the chain of wide
+  // modules over input blocks, once all of them are built (want_bitslice)
+  if (j.mode == rse::kStore && !j.accumulate && bitslice_len(j.len_bytes) &&
+      j.stripe_stride % 16u == 0 && rse::get_option(RSE_OPT_BITSLICE) &&
+      j.n_stripes <= 0xffffffffu && rse::wide_blocks_plan((uint32_t)n_in, (uint32_t)n_out, nullptr)) {
+    bool al = true;
+    for (size_t i = 0; i < n_in; ++i) al = al && aligned16(j.in[i]);
+    for (size_t r = 0; r < n_out; ++r) al = al && aligned16(j.out[r]);
+    uint64_t done = 0;
+    if (al)
+      RSE_HIP(rse::launch_wide_blocks(j.field, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data(),
+                                      j.in, j.out, j.len_bytes, j.stripe_stride,
+                                      (uint32_t)j.n_stripes, s, &done));
+    if (done) return done == j.len_bytes ? RSE_OK : run_rest(j, done, s);
   }
   const bool single_in = n_in <= (size_t)kMaxIn;
   if (j.mode == rse::kStore || single_in) {

@@ -46,6 +46,7 @@
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
 #include "rse_netgen.hpp"
+#include "rse_wideblk.hpp"
 
 extern char** environ;
 
@@ -217,6 +218,11 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
        "using __hip_internal::uint8_t;\nusing __hip_internal::uint16_t;\n"
        "using __hip_internal::uint32_t;\nusing __hip_internal::uint64_t;\n"
        "using __hip_internal::int32_t;\n";
+#ifdef RSE_TUNE_SPLITS
+  // timing split (tools/tune.py's build only, WRONG bytes): wide modules
+  // without their workgroup barriers, what the per-round synchronisation costs
+  if (kind == kJitWide && get_option(47) == 1) s += "#define __syncthreads() ((void)0)\n";
+#endif
   s += kJitSource;
   if (kind == kJitWide) {
     // one code struct per wave's share of the outputs, and the kernel (the
@@ -760,6 +766,56 @@ int status_of(Entry* e, bool wait) {
   return 2;
 }
 
+// ------------------------------------------ wide modules over input blocks
+// A codec too wide for one wide module's argument block (k + 2p >
+// kWideMaxPtrs: GF(2^16) past 256 shards, e.g. 1000+24) runs as a chain of
+// wide modules over blocks of its inputs, each coding ALL p outputs: block 0
+// is rows[:, 0..b0) and stores the outputs; block i > 0 is rows[:, block i]
+// followed by the p x p identity over the outputs themselves, so it reads the
+// sums so far as p more inputs and stores the new ones (a workgroup reads a
+// chunk of an output before it writes the same chunk; no two workgroups share
+// one).  Each input is read once and each output read and written once per
+// later block, against once per 8-output block and once per 32-input block
+// for the kJitBlock modules (~4.5x the algorithmic bytes at 1000+24).
+// RSE_OPT_WIDE_BLOCK_INPUTS caps the data inputs per block (hiprtc time grows
+// with the module); blocks are balanced.
+struct WideBlock {
+  uint32_t i0, ni, kk;          // data inputs i0..i0+ni, module inputs kk (ni, or ni + p)
+  std::vector<uint16_t> rows;   // p x kk
+};
+
+bool wide_blocks_plan_impl(uint32_t k, uint32_t p, uint32_t* nb) {
+  const int64_t lim = get_option(46);
+  if (lim <= 0 || k == 0 || p == 0 || wide_eligible(k, p) || 3u * p >= kWideMaxPtrs) return false;
+  const uint32_t kmax = (uint32_t)std::min<int64_t>(lim, (int64_t)(kWideMaxPtrs - 3u * p));
+  const uint32_t n = (k + kmax - 1) / kmax;
+  if (n < 2) return false;
+  const uint32_t base = k / n;  // blocks of base or base + 1 inputs
+  if (!wide_eligible(base, p) || !wide_eligible(base + p, p) || !wide_eligible(base + 1 + p, p))
+    return false;
+  *nb = n;
+  return true;
+}
+
+std::vector<WideBlock> wide_blocks_of(uint32_t k, uint32_t p, const uint16_t* rows, uint32_t n) {
+  std::vector<WideBlock> v(n);
+  const uint32_t base = k / n, extra = k % n;
+  uint32_t i0 = 0;
+  for (uint32_t b = 0; b < n; ++b) {
+    WideBlock& w = v[b];
+    w.i0 = i0;
+    w.ni = base + (b < extra ? 1u : 0u);
+    w.kk = w.ni + (b ? p : 0u);
+    w.rows.assign((size_t)p * w.kk, 0);
+    for (uint32_t o = 0; o < p; ++o) {
+      for (uint32_t i = 0; i < w.ni; ++i) w.rows[(size_t)o * w.kk + i] = rows[(size_t)o * k + i0 + i];
+      if (b) w.rows[(size_t)o * w.kk + w.ni + o] = 1;  // the output's sum so far
+    }
+    i0 += w.ni;
+  }
+  return v;
+}
+
 }  // namespace
 
 int jit_register(int field, uint32_t k, uint32_t p, const uint16_t* rows, JitKind kind) {
@@ -787,6 +843,28 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || p == 0) return 0;
   registry();
   Worker& w = worker();
+  uint32_t nb = 0;
+  if (wide_blocks_plan_impl(k, p, &nb)) {
+    const std::vector<WideBlock> bl = wide_blocks_of(k, p, rows, nb);
+    std::lock_guard<std::mutex> g(g_mu);
+    int need = 0, pending = 0;
+    for (const WideBlock& b : bl)
+      if (!find_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide)) {
+        need += (int)(((b.kk + kMaxIn - 1) / kMaxIn) * ((p + kJitMaxOut - 1) / kJitMaxOut));
+        ++pending;
+      }
+    if (need == 0) return 1;
+    if (pattern ? (g_pattern_blocks + need > max_pattern_blocks() ||
+                   g_pending_pattern_blocks + pending > kMaxPendingPatternBlocks)
+                : g_blocks + need > kMaxBlocks)
+      return 0;
+    for (const WideBlock& b : bl)
+      if (!find_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide))
+        add_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide, pattern);
+    w.start();
+    g_cv.notify_all();
+    return 1;
+  }
   std::lock_guard<std::mutex> g(g_mu);
   int need = 0;
   for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
@@ -950,12 +1028,61 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
 
 int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
   int worst = 2;
+  uint32_t nb = 0;
+  if (wide_blocks_plan_impl(k, p, &nb)) {
+    for (const WideBlock& b : wide_blocks_of(k, p, rows, nb)) {
+      const int s = status_of(find_entry(field, b.kk, p, b.rows.data(), b.kk, kJitWide), wait);
+      if (s < worst) worst = s;
+      if (worst <= 0) break;
+    }
+    return worst;
+  }
   for_each_block(k, p, [&](uint32_t o0, uint32_t i0, uint32_t no, uint32_t ni, JitKind kind) {
     if (worst <= 0) return;  // one block not registered: the rows are not a wide codec's
     const int s = status_of(find_entry(field, ni, no, rows + (size_t)o0 * k + i0, k, kind), wait);
     if (s < worst) worst = s;
   });
   return worst;
+}
+
+bool wide_blocks_plan(uint32_t k, uint32_t p, uint32_t* n_blocks) {
+  uint32_t nb = 0;
+  const bool ok = wide_blocks_plan_impl(k, p, &nb);
+  if (n_blocks) *n_blocks = ok ? nb : 0;
+  return ok;
+}
+
+hipError_t launch_wide_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
+                              const uint8_t* const* in, uint8_t* const* out, uint64_t len,
+                              uint64_t stripe_stride, uint32_t n_stripes, hipStream_t stream,
+                              uint64_t* done) {
+  *done = 0;
+  uint32_t nb = 0;
+  if (!wide_blocks_plan_impl(k, p, &nb) || n_stripes == 0) return hipSuccess;
+  const std::vector<WideBlock> bl = wide_blocks_of(k, p, rows, nb);
+  const bool wait = get_option(9) >= 2;
+  for (const WideBlock& b : bl)  // every module built, or none is launched
+    if (status_of(find_entry(field, b.kk, p, b.rows.data(), b.kk, kJitWide), wait) != 2)
+      return hipSuccess;
+  std::vector<const uint8_t*> ins;
+  uint64_t d0 = 0;
+  for (size_t bi = 0; bi < bl.size(); ++bi) {
+    const WideBlock& b = bl[bi];
+    ins.assign(in + b.i0, in + b.i0 + b.ni);
+    if (bi) ins.insert(ins.end(), out, out + p);
+    uint64_t d = 0;
+    const hipError_t he = launch_wide(field, b.kk, p, b.rows.data(), ins.data(), out, nullptr, len,
+                                      stripe_stride, n_stripes, kStore, nullptr, false, stream, &d);
+    if (he != hipSuccess) return he;
+    // every block codes the same whole chunks (same length, every module built)
+    if (bi == 0) d0 = d;
+    else if (d != d0) return hipErrorInvalidValue;
+    if (d0 == 0) return hipSuccess;
+  }
+  note_kernel("bitslice-wide-blocks gf%d %u+%u x%u (%u+%u w%d)", field, k, p, nb, bl[0].ni, p,
+              wide_waves(p));
+  *done = d0;
+  return hipSuccess;
 }
 
 int jit_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {

@@ -484,7 +484,7 @@ def test_encode_single_steps_match_oracle(R, field, k, p):
 @pytest.mark.parametrize("k,p,lens", [(300, 60, [1, 7, 1000, 4099]), (1000, 24, [5, 2051])])
 def test_gf16_beyond_256_shards(R, k, p, lens):
     rng = np.random.default_rng(k + p)
-    oc = O.Codec(16, k, p)
+    oc = O.Codec.shared(16, k, p)
     r = R.galois_16.ReedSolomon(k, p)
     assert (np.array(r.matrix(), np.int64) ==
             (oc.matrix()[..., 0].astype(np.int64) << 8 | oc.matrix()[..., 1])).all()

@@ -1618,6 +1618,62 @@ def test_wide_codec_kernels(R, subfield, field, k, p, modules):
         lib.rse_set_option(9, old)
 
 
+def test_wide_block_chain_gf16_past_256(R):
+    """GF(2^16) 1000+24 (k + 2p > 480: too wide for one wide module's pointer
+    block) on a chain of wide modules over input blocks (rse_jit.cpp;
+    RSE_OPT_WIDE_BLOCK_INPUTS 128: 8 blocks of 125 data shards), each coding
+    all 24 outputs, the blocks after the first reading the sums so far as 24
+    more inputs.  Encode (whole 4 KiB chunks on the chain, a table-coded tail),
+    verify (sums materialised through the chain, then compared) and a
+    2-stripe encode_flat against the oracle.  The modules come from the
+    tree's jitcache (tools/prebuild_all.sh)."""
+    lib = R._lib.load()
+    k, p = 1000, 24
+    nbytes = 2 * 4096 + 96
+    n_elems = nbytes // 2
+    rng = np.random.default_rng(1024)
+    oc = O.Codec.shared(16, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    old = lib.rse_get_option(9)
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        r = R.core.ReedSolomon(k, p, 16)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        t = [dev(x).reshape(n_elems, 2) for x in full[:k]] + \
+            [torch.full((n_elems, 2), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        n0 = lib.rse_get_option(6)
+        r.encode(t)
+        torch.cuda.synchronize()
+        assert lib.rse_get_option(6) - n0 == 8
+        from reed_solomon_erasure.core import last_kernel
+        assert last_kernel().startswith("bitslice-wide-blocks gf16 1000+24 x8 (125+24"), last_kernel()
+        for i in range(p):
+            assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
+        assert r.verify(t)
+        t[k + p - 1].view(-1)[5000] ^= 1  # in a chain-coded chunk
+        assert not r.verify(t)
+        t[k + p - 1].view(-1)[5000] ^= 1
+        t[k - 1].view(-1)[nbytes - 1] ^= 0x80  # in the table-coded tail
+        assert not r.verify(t)
+        t[k - 1].view(-1)[nbytes - 1] ^= 0x80
+        stripes = 2
+        flat = torch.full((stripes, k + p, nbytes), 0xA5, dtype=torch.uint8, device="cuda")
+        for s_ in range(stripes):
+            flat[s_, :k] = dev(np.stack([np.roll(full[i], 7 * s_) for i in range(k)]))
+        r.encode_flat(flat, n_elems, stripes)
+        torch.cuda.synchronize()
+        got = host(flat)
+        for s_ in range(stripes):
+            sh = [np.roll(full[i], 7 * s_) for i in range(k)] + \
+                 [np.zeros(nbytes, np.uint8) for _ in range(p)]
+            oc.encode(sh)
+            for i in range(p):
+                assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
+    finally:
+        lib.rse_set_option(9, old)
+
+
 @pytest.mark.parametrize("field,k,p,erased", [(8, 40, 2, [3, 39]), (8, 6, 10, [0, 1, 2, 5, 6, 8, 9, 12, 15]),
                                               (16, 36, 3, [0, 35, 37])])
 def test_wide_reconstruct_pattern_blocks(R, field, k, p, erased):
