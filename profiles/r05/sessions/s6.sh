@@ -14,12 +14,27 @@ W32="--k 32 --p 32 --shard-kib 1 --stripes 4096"
 C1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 P="rocprofv3 --kernel-include-regex rse_jit --output-format csv"
 PT="python3 tools/tune.py --rounds 2 --shapes 0:0 --nt-only"
-bash tools/gpu_session.sh \
+[ "$1" = occ ] || bash tools/gpu_session.sh \
  "chain:600:$PY tests/test_gpu_parity.py -k 'wide_block_chain or wide_codec_kernels' && $PY tests/test_gpu_host_paths.py -k beyond_256" \
  "g1000:400:for i in 1 2; do $TU $G16 && $TU $G16 --set 46=0 || exit 1; done" \
  "pmcc_1:120:timeout -s KILL 110 $P --pmc $C1 -d gpurun_out/pmcc_1 -o p -- $PT $G16" \
  "pmcc_f:120:timeout -s KILL 110 $P --pmc FETCH_SIZE -d gpurun_out/pmcc_f -o p -- $PT $G16" \
  "pmcc_w:120:timeout -s KILL 110 $P --pmc WRITE_SIZE -d gpurun_out/pmcc_w -o p -- $PT $G16" \
- "tracec:120:timeout -s KILL 110 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tracec -o t -- $PT $G16" \
- "o64:400:for i in 1 2; do $TU $W64 && $TU $W64 --set 20=4 && $TU $W64 --set 20=4 --set 13=16 && $TU $W64 --set 20=4 --set 13=8 || exit 1; done" \
- "o32:400:for i in 1 2; do $TU $W32 && $TU $W32 --set 20=4 && $TU $W32 --set 20=4 --set 13=16 && $TU $W32 --set 20=4 --set 13=8 || exit 1; done"
+ "tracec:120:timeout -s KILL 110 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tracec -o t -- $PT $G16"
+
+
+# (second call) 64+64 / 32+32 x 1 KiB: RSE_OPT_WIDE_OCCUPANCY 4 (<= 128 VGPRs; the
+# modules spill 98-761 VGPRs) and the tune build's barrier-free modules (47=1,
+# WRONG bytes: what the per-round barriers cost)
+if [ "$1" = occ ]; then
+TL="env RSE_LIB_PATH=reed-solomon-erasure_amd/build-tune/librse_hip.so $TU"
+bash tools/gpu_session.sh \
+ "o64:400:for i in 1 2; do $TU $W64 && $TU $W64 --set 20=4 && $TU $W64 --set 20=4 --set 13=16 && $TL $W64 --set 47=1 || exit 1; done" \
+ "o32:400:for i in 1 2; do $TU $W32 && $TU $W32 --set 20=4 --set 13=8 && $TL $W32 --set 47=1 || exit 1; done"
+fi
+if [ "$1" = nosync ]; then
+TL="env RSE_LIB_PATH=reed-solomon-erasure_amd/build-tune/librse_hip.so $TU"
+bash tools/gpu_session.sh \
+ "n64:400:for i in 1 2; do $TU $W64 && $TL $W64 --set 47=1 || exit 1; done" \
+ "n32:400:for i in 1 2; do $TU $W32 && $TL $W32 --set 47=1 || exit 1; done"
+fi
