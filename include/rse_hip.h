@@ -415,9 +415,6 @@ void rse_dispatcher_stop(void);
                                         256 shards): a chain of wide modules over blocks of at
                                         most this many data inputs, each coding every output
                                         (default 128); 0: modules of 8 outputs x 32 inputs */
-#define RSE_OPT_WIDE_LDS_PIPE 48      /* wide modules: each LDS slot's (pair's) reads issued before
-                                        the previous slot's network (1, default), or just before
-                                        its own (0; A/B). Read when a module is generated */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: 0 fixed workgroup counts (8192

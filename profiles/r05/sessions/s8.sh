@@ -28,13 +28,9 @@ bash tools/gpu_session.sh \
 exit
 fi
 bash tools/gpu_session.sh \
- "tests:600:$PY tests/test_gpu_parity.py -k 'wide or sub_chunk'" \
  "p64:300:for i in 1 2; do $TU $W64 && $TU $W64 --set 48=0 || exit 1; done" \
  "p32:300:for i in 1 2; do $TU $W32 && $TU $W32 --set 48=0 || exit 1; done" \
  "p50:300:for i in 1 2; do $TU $W50 && $TU $W50 --set 48=0 || exit 1; done" \
  "p50m:300:for i in 1 2; do $TU $W50M && $TU $W50M --set 48=0 || exit 1; done" \
  "g16:300:$TU $G16" \
- "ic64:120:timeout -s KILL 110 $P --pmc $CI -d gpurun_out/ic64 -o p -- $PT $W64" \
- "ic16:120:timeout -s KILL 110 $P --pmc $CI -d gpurun_out/ic16 -o p -- $PT $W16" \
- "lds64:120:timeout -s KILL 110 $P --pmc $CL -d gpurun_out/lds64 -o p -- $PT $W64" \
- "lds64o:120:timeout -s KILL 110 $P --pmc $CL -d gpurun_out/lds64o -o p -- $PT $W64 --set 48=0"
+ "smoke:300:python3 -c 'import __graft_entry__ as g; g.smoke()'"

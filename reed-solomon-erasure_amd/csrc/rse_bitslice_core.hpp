@@ -540,51 +540,10 @@ __device__ __forceinline__ void mac_pair(uint32_t (&acc)[C::p * 16], const uint3
   }
 }
 
-// Slot S's 16 planes of a round set.
-template <int W, int S>
-__device__ __forceinline__ void read_slot(const uint4 (&set)[W][4][64], uint32_t lane,
-                                          uint32_t (&pl)[16]) {
-#pragma unroll
-  for (int q4 = 0; q4 < 4; ++q4) {
-    const uint4 v = set[S][q4][lane];
-    pl[q4 * 4 + 0] = v.x;
-    pl[q4 * 4 + 1] = v.y;
-    pl[q4 * 4 + 2] = v.z;
-    pl[q4 * 4 + 3] = v.w;
-  }
-}
-
-// wide_code_round's single-input networks with the next slot's LDS reads
-// issued before this slot's XORs (pl: slot S, already read).  Without it each
-// slot's reads are waited for right before its network: the acc pins between
-// inputs are scheduling boundaries, so the compiler cannot overlap them, and
-// at 2 waves per SIMD of one workgroup both waves of a SIMD stall together.
 template <class C, int W, int R, int S>
-__device__ __forceinline__ void wide_code_round_pl(uint32_t (&acc)[C::p * 16],
-                                                   const uint4 (&set)[W][4][64], uint32_t lane,
-                                                   const uint32_t (&pl)[16]) {
-  constexpr bool more = S + 1 < W && R * W + S + 1 < C::k;
-  uint32_t nx[16];
-  if constexpr (more) {
-    read_slot<W, S + 1>(set, lane, nx);
-    __builtin_amdgcn_sched_barrier(0);  // the reads stay ahead of the network
-  }
-  mac_input<C, R * W + S, false>(acc, pl, make_int_seq<C::p * 16>{});
-#pragma unroll
-  for (int q = 0; q < C::p * 16; ++q) asm volatile("" : "+v"(acc[q]));
-  if constexpr (more) wide_code_round_pl<C, W, R, S + 1>(acc, set, lane, nx);
-}
-
-template <class C, int W, int R, int S, bool PL = false>
 __device__ __forceinline__ void wide_code_round(uint32_t (&acc)[C::p * 16],
                                                 const uint4 (&set)[W][4][64], uint32_t lane) {
-  if constexpr (PL && !C::kPairIn) {
-    if constexpr (S < W && R * W + S < C::k) {
-      uint32_t pl[16];
-      read_slot<W, S>(set, lane, pl);
-      wide_code_round_pl<C, W, R, S>(acc, set, lane, pl);
-    }
-  } else if constexpr (C::kPairIn) {
+  if constexpr (C::kPairIn) {
     // two inputs at a time (W even, so a round's inputs pair up)
     static_assert(W % 2 == 0, "paired inputs need an even number of waves");
     if constexpr (S < W && R * W + S < C::k) {
@@ -670,7 +629,7 @@ __device__ __forceinline__ void wide_rounds(uint32_t (&acc)[C::p * 16], u32x4 (&
 // workgroup, ~32 KiB per CU at 2 workgroups -- ~8 MiB over the chip, which at
 // ~2 us of loaded HBM latency caps the read rate near 4 TB/s whatever the
 // VALU does (Little's law); D inputs per wave raise that cap D-fold.
-template <class C, int W, int WI, int D, int R, class A, uint32_t S = 1024u, bool PL = false>
+template <class C, int W, int WI, int D, int R, class A, uint32_t S = 1024u>
 __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
                                                  u32x4 (&buf)[D + 1][4], const A& a, uint64_t off,
                                                  uint64_t next_off, WidePlanes<W>& lds, uint32_t& g,
@@ -693,9 +652,9 @@ __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
         set[WI][q4][lane] = make_uint4(pl[q4 * 4], pl[q4 * 4 + 1], pl[q4 * 4 + 2], pl[q4 * 4 + 3]);
     }
     __syncthreads();
-    wide_code_round<C, W, R, 0, PL>(acc, set, lane);
+    wide_code_round<C, W, R, 0>(acc, set, lane);
     ++g;
-    wide_rounds_deep<C, W, WI, D, R + 1, A, S, PL>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_deep<C, W, WI, D, R + 1, A, S>(acc, buf, a, off, next_off, lds, g, lane);
   }
 }
 
@@ -704,7 +663,7 @@ __device__ __forceinline__ void wide_rounds_deep(uint32_t (&acc)[C::p * 16],
 // per wave (wide_rounds_deep); 1 is wide_rounds.
 // SUB: 1 or 2 KiB shards, a chunk = 4096 / SUB consecutive stripes' shards
 // (bitslice_body's SUB).
-template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0, bool PL = false>
+template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0>
 __device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& lds) {
   const WideHdr& h = a.h;
   constexpr int K = C::k, NR = (K + W - 1) / W;
@@ -736,7 +695,7 @@ __device__ __forceinline__ void wide_body_lds_deep(const A& a, WidePlanes<W>& ld
     const uint64_t next = c + gridDim.x;
     const uint64_t next_off = next < total ? chunk_off(next) : ~0ull;
     uint32_t acc[C::p * 16];
-    wide_rounds_deep<C, W, WI, D, 0, A, S, PL>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_deep<C, W, WI, D, 0, A, S>(acc, buf, a, off, next_off, lds, g, lane);
     if constexpr (NR % (D + 1) != 0) {  // the next chunk's rounds j into slots j
       u32x4 t[D][4];
 #pragma unroll
@@ -837,64 +796,11 @@ __device__ __forceinline__ void mac_pair_half(uint32_t (&acc)[C::p * 8], const u
     ((acc[OP] = xacc<C::planes.sel[OP / 8][J][OP % 8]>(acc[OP], src)), ...);
 }
 
-// The planes of slots S and S + 1 of a half-chunk round set: network input
-// pair (R * W + S) / 2 (the second all zero past k).
 template <class C, int W, int R, int S>
-__device__ __forceinline__ void read_pair_half(const uint4 (&set)[W][2][64], uint32_t lane,
-                                               uint32_t (&pa)[8], uint32_t (&pb)[8]) {
-#pragma unroll
-  for (int q4 = 0; q4 < 2; ++q4) {
-    const uint4 v = set[S][q4][lane];
-    pa[q4 * 4 + 0] = v.x;
-    pa[q4 * 4 + 1] = v.y;
-    pa[q4 * 4 + 2] = v.z;
-    pa[q4 * 4 + 3] = v.w;
-  }
-  if constexpr (R * W + S + 1 < C::k) {
-#pragma unroll
-    for (int q4 = 0; q4 < 2; ++q4) {
-      const uint4 v = set[S + 1][q4][lane];
-      pb[q4 * 4 + 0] = v.x;
-      pb[q4 * 4 + 1] = v.y;
-      pb[q4 * 4 + 2] = v.z;
-      pb[q4 * 4 + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) pb[q] = 0u;
-  }
-}
-
-// wide_code_round_half with the next pair's LDS reads issued before this
-// pair's XORs (wide_code_round_pl: the same reason).
-template <class C, int W, int R, int S>
-__device__ __forceinline__ void wide_code_round_half_pl(uint32_t (&acc)[C::p * 8],
-                                                        const uint4 (&set)[W][2][64], uint32_t lane,
-                                                        const uint32_t (&pa)[8],
-                                                        const uint32_t (&pb)[8]) {
-  constexpr bool more = S + 2 < W && R * W + S + 2 < C::k;
-  uint32_t na[8], nb[8];
-  if constexpr (more) {
-    read_pair_half<C, W, R, S + 2>(set, lane, na, nb);
-    __builtin_amdgcn_sched_barrier(0);  // the reads stay ahead of the network
-  }
-  mac_pair_half<C, (R * W + S) / 2>(acc, pa, pb, make_int_seq<C::p * 8>{});
-#pragma unroll
-  for (int q = 0; q < C::p * 8; ++q) asm volatile("" : "+v"(acc[q]));
-  if constexpr (more) wide_code_round_half_pl<C, W, R, S + 2>(acc, set, lane, na, nb);
-}
-
-template <class C, int W, int R, int S, bool PL = false>
 __device__ __forceinline__ void wide_code_round_half(uint32_t (&acc)[C::p * 8],
                                                      const uint4 (&set)[W][2][64], uint32_t lane) {
   static_assert(C::kPairIn && W % 2 == 0, "half chunks: paired GF(2^8) networks, W even");
-  if constexpr (PL) {
-    if constexpr (S < W && R * W + S < C::k) {
-      uint32_t pa[8], pb[8];
-      read_pair_half<C, W, R, S>(set, lane, pa, pb);
-      wide_code_round_half_pl<C, W, R, S>(acc, set, lane, pa, pb);
-    }
-  } else if constexpr (S < W && R * W + S < C::k) {
+  if constexpr (S < W && R * W + S < C::k) {
     uint32_t pa[8], pb[8];
 #pragma unroll
     for (int q4 = 0; q4 < 2; ++q4) {
@@ -927,7 +833,7 @@ __device__ __forceinline__ void wide_code_round_half(uint32_t (&acc)[C::p * 8],
 // The rounds of one half chunk, D own inputs in flight per wave (as
 // wide_rounds_deep: ring of D + 1 slots; past the last round, the next
 // chunk's first rounds).
-template <class C, int W, int WI, int D, int R, class A, uint32_t S, bool PL = false>
+template <class C, int W, int WI, int D, int R, class A, uint32_t S>
 __device__ __forceinline__ void wide_rounds_half(uint32_t (&acc)[C::p * 8], u32x4 (&buf)[D + 1][2],
                                                  const A& a, uint64_t off, uint64_t next_off,
                                                  WideHalfPlanes<W>& lds, uint32_t& g, uint32_t lane) {
@@ -948,9 +854,9 @@ __device__ __forceinline__ void wide_rounds_half(uint32_t (&acc)[C::p * 8], u32x
       set[WI][1][lane] = make_uint4(pl[4], pl[5], pl[6], pl[7]);
     }
     __syncthreads();
-    wide_code_round_half<C, W, R, 0, PL>(acc, set, lane);
+    wide_code_round_half<C, W, R, 0>(acc, set, lane);
     ++g;
-    wide_rounds_half<C, W, WI, D, R + 1, A, S, PL>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_half<C, W, WI, D, R + 1, A, S>(acc, buf, a, off, next_off, lds, g, lane);
   }
 }
 
@@ -958,7 +864,7 @@ __device__ __forceinline__ void wide_rounds_half(uint32_t (&acc)[C::p * 8], u32x
 // this with the same `lds`.  The launch's chunk count is in 2 KiB units
 // (rse_jit.cpp launch_wide: twice the 4 KiB chunks, or ceil(n_stripes /
 // (2048 / SUB))).
-template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0, bool PL = false>
+template <class C, int O0, int W, int WI, int D, class A, uint32_t SUB = 0>
 __device__ __forceinline__ void wide_body_half(const A& a, WideHalfPlanes<W>& lds) {
   static_assert(SUB == 0 || SUB == 1024u || SUB == 2048u, "1 or 2 KiB shards");
   const WideHdr& h = a.h;
@@ -992,7 +898,7 @@ __device__ __forceinline__ void wide_body_half(const A& a, WideHalfPlanes<W>& ld
     const uint64_t next = c + gridDim.x;
     const uint64_t next_off = next < total ? chunk_off(next) : ~0ull;
     uint32_t acc[C::p * 8];
-    wide_rounds_half<C, W, WI, D, 0, A, S, PL>(acc, buf, a, off, next_off, lds, g, lane);
+    wide_rounds_half<C, W, WI, D, 0, A, S>(acc, buf, a, off, next_off, lds, g, lane);
     if constexpr (NR % (D + 1) != 0) {  // the next chunk's rounds j into slots j
       u32x4 t[D][2];
 #pragma unroll

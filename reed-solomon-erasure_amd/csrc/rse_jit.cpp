@@ -238,9 +238,6 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
     // accumulators; 8 outputs per wave no longer spill)
     const bool half = pairs && get_option(38) != 0;
     if (wide_half) *wide_half = half;
-    // RSE_OPT_WIDE_LDS_PIPE: the next slot's LDS reads issued before the
-    // current slot's network (rse_bitslice_core.hpp wide_code_round_pl)
-    const bool pl = get_option(48) != 0;
     for (int w = 0; w < W; ++w) {
       uint32_t o0, n;
       wide_share(p, W, w, &o0, &n);
@@ -279,13 +276,13 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
         if (half)
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body_half<rse::JitWide%d, %u, %d, %d, %d, "
-                        "WideArgs, %du, %s>(a, lds); break;\n",
-                        w, w, o0, W, w, (int)get_option(26), 1024 * q, pl ? "true" : "false");
+                        "WideArgs, %du>(a, lds); break;\n",
+                        w, w, o0, W, w, (int)get_option(26), 1024 * q);
         else if (shared)
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body_lds_deep<rse::JitWide%d, %u, %d, %d, %d, "
-                        "WideArgs, %du, %s>(a, lds); break;\n",
-                        w, w, o0, W, w, (int)get_option(26), 1024 * q, pl ? "true" : "false");
+                        "WideArgs, %du>(a, lds); break;\n",
+                        w, w, o0, W, w, (int)get_option(26), 1024 * q);
         else
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body<rse::JitWide%d, %u, WideArgs, %du>(a); "

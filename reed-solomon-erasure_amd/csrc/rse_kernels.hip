@@ -804,7 +804,6 @@ struct Options {
   int64_t wide_grid = 0;          // wide launches: 0 fixed workgroup counts, m > 0 m x resident
   int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
   int64_t wide_block_inputs = 128;  // data inputs per wide module of a chain (0: 8 x 32 blocks)
-  int64_t wide_lds_pipe = 1;  // wide modules: next slot's LDS reads before this slot's network
   int64_t tune_nosync = 0;  // RSE_TUNE_SPLITS builds: wide modules without barriers (timing)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
@@ -1352,7 +1351,6 @@ int set_option(int key, int64_t value) {
     case 44: g_opt.wide_grid = value < 0 ? 0 : value > 64 ? 64 : value; return 0;
     case 45: g_opt.dispatch_wgs = value < 1 ? 1 : value > 64 ? 64 : value; return 0;
     case 46: g_opt.wide_block_inputs = value < 0 ? 0 : value; return 0;
-    case 48: g_opt.wide_lds_pipe = value ? 1 : 0; return 0;
 #ifdef RSE_TUNE_SPLITS
     case 47: g_opt.tune_nosync = value ? 1 : 0; return 0;  // rse_jit.cpp make_source
 #endif
@@ -1412,7 +1410,6 @@ int64_t get_option(int key) {
     case 44: return g_opt.wide_grid;
     case 45: return g_opt.dispatch_wgs;
     case 46: return g_opt.wide_block_inputs;
-    case 48: return g_opt.wide_lds_pipe;
 #ifdef RSE_TUNE_SPLITS
     case 47: return g_opt.tune_nosync;
 #endif
