@@ -417,9 +417,11 @@ void rse_dispatcher_stop(void);
                                         (default 128); 0: modules of 8 outputs x 32 inputs */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
-#define RSE_OPT_WIDE_GRID 44          /* wide-module launches: 0 fixed workgroup counts (8192
+#define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192
                                         GF(2^8), 16384 GF(2^16)); m > 0: m x the workgroups the
-                                        device holds at once (occupancy of the module) */
+                                        device holds at once (occupancy of the module); 0
+                                        (default): 1 x that for 1 / 2 KiB shards of codecs with
+                                        k x p >= 1000, fixed counts otherwise */
 #define RSE_OPT_WIDE_PAIRS 29        /* wide GF(2^8) modules built after: 1 (default) XOR networks
                                         over pairs of inputs (temporaries may combine both), coded two
                                         inputs at a time; 0: one input at a time */

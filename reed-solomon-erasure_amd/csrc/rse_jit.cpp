@@ -1004,8 +1004,15 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   // tools/tune.py grid sweeps, 128 stripes x 1 MiB (profiles/r04/s2/): GF(2^16)
   // 40+12 16384 workgroups 5.29 TB/s against 5.05 at 4096; GF(2^8) 50+20 flat
   // from 2048 to 8192 (4.72), 4.68 at 16384
-  // RSE_OPT_WIDE_GRID m > 0: m x the workgroups the device holds at once
-  const int64_t mult = get_option(44);
+  // RSE_OPT_WIDE_GRID m > 0: m x the workgroups the device holds at once;
+  // 0 (auto): that once for 1 / 2 KiB shards of codecs with k x p >= 1000,
+  // whose launches are a few chunks per workgroup: each workgroup then walks
+  // its chunks with the next one's loads in flight instead of a fresh
+  // workgroup starting cold (same box, profiles/r05/s45/g*.log: 32+32 x 1 KiB
+  // 4.01 -> 4.22 TB/s, 64+64 2.49 -> 2.57, 50+20 4.53 -> 4.58; 16+16 5.78 ->
+  // 5.32 and the 1 MiB codecs 5-7 % slower, so not for those); -1 fixed counts
+  int64_t mult = get_option(44);
+  if (mult == 0) mult = (subq && (uint64_t)k * p >= 1000u) ? 1 : -1;
   uint64_t gx = grid > 0                ? (uint64_t)grid
                 : (mult > 0 && cap > 0) ? (uint64_t)mult * cap
                 : field == 16           ? 16384u

@@ -801,7 +801,7 @@ struct Options {
   int64_t dispatch = 1;           // *_now calls on the resident dispatcher (rse_dispatch.hip)
   int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
   int64_t dispatch_max_bytes = 65536;  // shard bytes up to which a *_now call is dispatched
-  int64_t wide_grid = 0;          // wide launches: 0 fixed workgroup counts, m > 0 m x resident
+  int64_t wide_grid = 0;          // wide launches: -1 fixed workgroup counts, m > 0 m x resident, 0 auto
   int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
   int64_t wide_block_inputs = 128;  // data inputs per wide module of a chain (0: 8 x 32 blocks)
   int64_t tune_nosync = 0;  // RSE_TUNE_SPLITS builds: wide modules without barriers (timing)
@@ -1348,7 +1348,7 @@ int set_option(int key, int64_t value) {
     case 39: g_opt.dispatch = value ? 1 : 0; return 0;
     case 40: g_opt.dispatch_idle_us = value < 10 ? 10 : value > 1000000 ? 1000000 : value; return 0;
     case 41: g_opt.dispatch_max_bytes = value < 0 ? 0 : value; return 0;
-    case 44: g_opt.wide_grid = value < 0 ? 0 : value > 64 ? 64 : value; return 0;
+    case 44: g_opt.wide_grid = value < -1 ? -1 : value > 64 ? 64 : value; return 0;
     case 45: g_opt.dispatch_wgs = value < 1 ? 1 : value > 64 ? 64 : value; return 0;
     case 46: g_opt.wide_block_inputs = value < 0 ? 0 : value; return 0;
 #ifdef RSE_TUNE_SPLITS
