@@ -415,6 +415,9 @@ void rse_dispatcher_stop(void);
                                         256 shards): a chain of wide modules over blocks of at
                                         most this many data inputs, each coding every output
                                         (default 128); 0: modules of 8 outputs x 32 inputs */
+#define RSE_OPT_DISPATCH_LANE_UNITS 49 /* dispatcher: a request takes ceil(units / (this x 512))
+                                        of the resident workgroups, units = 16-byte vectors x
+                                        outputs (default 1); one workgroup up to 1024 units */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192

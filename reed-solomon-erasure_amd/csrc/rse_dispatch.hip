@@ -354,15 +354,22 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
   if ((e = disp_init(d)) != hipSuccess) return e;
   const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;  // 0: the zeroed ring
   const uint32_t n_gran = 1 + n_in + n_out + (n_in * n_out + 11) / 12;
-  // workgroups that code it: ~2 (16-byte vector, output) units per lane, as
+  // workgroups that code it: ~RSE_OPT_DISPATCH_LANE_UNITS (1) (16-byte vector,
+  // output) units per lane, as
   // many as the running kernel has; outputs per work item: items (vectors x
   // output blocks) for their lanes
   const uint64_t n_vec = len_bytes / 16u;
   if (!d.running) d.n_wgs = (uint32_t)std::min<int64_t>(std::max<int64_t>(get_option(45), 1),
                                                           kMaxDispWgs);
+  // (profiles/r05/s10/latency.log, 8 resident, 10+4: 4 KiB 6.6 us on one
+  // workgroup against 7.3 on two; 8 / 16 KiB 8.0 / 8.3 us at one unit per
+  // lane against 8.4 / 9.2 at two and 8.9 / 10.6 at four)
   const uint64_t units = n_vec * n_out;
-  const uint32_t n_wg = (uint32_t)std::min<uint64_t>(
-      d.n_wgs, std::max<uint64_t>(1, (units + 2 * kDispThreads - 1) / (2 * kDispThreads)));
+  const uint64_t per_wg = (uint64_t)std::max<int64_t>(get_option(49), 1) * kDispThreads;
+  const uint32_t n_wg =
+      units <= 2u * kDispThreads
+          ? 1u  // a request within 2 units per lane of one workgroup stays on it
+          : (uint32_t)std::min<uint64_t>(d.n_wgs, (units + per_wg - 1) / per_wg);
   const uint64_t lanes = (uint64_t)n_wg * kDispThreads;
   uint32_t ob = 1;
   while (ob < 8 && n_vec * ((n_out + 2 * ob - 1) / (2 * ob)) >= lanes) ob *= 2;

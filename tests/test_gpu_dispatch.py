@@ -235,16 +235,18 @@ def test_now_c_abi_latency(R):
     assert us < 15, us
 
 
-@pytest.mark.parametrize("wgs", [1, 3, 8, 32])
-def test_now_dispatcher_workgroup_counts(R, wgs):
+@pytest.mark.parametrize("wgs,units", [(1, 1), (3, 1), (8, 1), (8, 3), (32, 1), (32, 2)])
+def test_now_dispatcher_workgroup_counts(R, wgs, units):
     """RSE_OPT_DISPATCH_WORKGROUPS: the resident kernel's workgroups split a
-    request's (vector, output block) items; every count gives the oracle's
-    bytes for encode, verify and reconstruct, at sizes that use one and all
-    of them (up to 256 KiB shards with the size limit raised)."""
+    request's (vector, output block) items, as many as RSE_OPT_DISPATCH_LANE_UNITS
+    gives the request; every count gives the oracle's bytes for encode, verify
+    and reconstruct, at sizes that use one and all of them (up to 256 KiB
+    shards with the size limit raised)."""
     lib = R._lib.load()
-    WGS = 45
-    old = [lib.rse_get_option(x) for x in (WGS, MAX_BYTES)]
+    WGS, UNITS = 45, 49
+    old = [lib.rse_get_option(x) for x in (WGS, MAX_BYTES, UNITS)]
     try:
+        lib.rse_set_option(UNITS, units)
         lib.rse_set_option(WGS, wgs)
         lib.rse_set_option(MAX_BYTES, 1 << 18)
         lib.rse_dispatcher_stop()  # the next call launches with `wgs` workgroups
@@ -255,4 +257,5 @@ def test_now_dispatcher_workgroup_counts(R, wgs):
     finally:
         lib.rse_set_option(WGS, old[0])
         lib.rse_set_option(MAX_BYTES, old[1])
+        lib.rse_set_option(UNITS, old[2])
         lib.rse_dispatcher_stop()

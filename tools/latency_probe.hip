@@ -11,6 +11,7 @@
 //   H  empty kernel + hipStreamWriteValue32, host spins
 //   I  rse_encode_now 10+4 x 1 KiB (the resident dispatcher)
 //   J  rse_encode_now by shard size: 1, 8, 32 dispatcher workgroups, and the launch path
+//   K  rse_encode_now 4-64 KiB: 8 / 16 resident workgroups, 1 / 2 / 4 units per lane
 // The resident kernel of E exits on a stop value or after a bounded number of
 // polls, so it always drains.
 //   hipcc --offload-arch=gfx950 -O2 -I include tools/latency_probe.hip \
@@ -221,6 +222,44 @@ int main() {
     rse_set_option(RSE_OPT_DISPATCH, 1);
     rse_set_option(RSE_OPT_DISPATCH_WORKGROUPS, 8);
     rse_set_option(RSE_OPT_DISPATCH_MAX_BYTES, 32768);
+    rse_dispatcher_stop();
+    rse_codec_free(c);
+    CK(hipFree(buf));
+  }
+  {  // K: workgroups per request (RSE_OPT_DISPATCH_LANE_UNITS) at 8 and 16 resident ones
+    rse_codec* c = nullptr;
+    if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
+    const size_t T = 14, Lmax = 1u << 16;
+    uint8_t* buf = nullptr;
+    CK(hipMalloc(reinterpret_cast<void**>(&buf), T * Lmax));
+    CK(hipMemset(buf, 7, T * Lmax));
+    rse_set_option(RSE_OPT_DISPATCH, 1);
+    rse_set_option(RSE_OPT_DISPATCH_MAX_BYTES, (int64_t)Lmax);
+    for (int wgs : {8, 16}) {
+      rse_set_option(RSE_OPT_DISPATCH_WORKGROUPS, wgs);
+      rse_dispatcher_stop();
+      for (size_t L : {4096u, 8192u, 16384u, 32768u, 65536u}) {
+        std::vector<void*> sh(T);
+        std::vector<size_t> lens(T, L);
+        for (size_t i = 0; i < T; ++i) sh[i] = buf + i * L;
+        for (int u : {1, 2, 4}) {
+          rse_set_option(RSE_OPT_DISPATCH_LANE_UNITS, u);
+          Stat g;
+          for (int i = 0; i < 1020; ++i) {
+            const auto t0 = clk::now();
+            if (rse_encode_now(c, sh.data(), lens.data(), T)) return 4;
+            if (i >= 20) g.v.push_back(us_since(t0));
+          }
+          char name[96];
+          std::snprintf(name, sizeof name, "K encode_now 10+4 x %zu KiB, %d resident, %d units/lane",
+                        L >> 10, wgs, u);
+          g.report(name);
+        }
+      }
+    }
+    rse_set_option(RSE_OPT_DISPATCH_LANE_UNITS, 2);
+    rse_set_option(RSE_OPT_DISPATCH_WORKGROUPS, 8);
+    rse_set_option(RSE_OPT_DISPATCH_MAX_BYTES, 65536);
     rse_dispatcher_stop();
     rse_codec_free(c);
     CK(hipFree(buf));
