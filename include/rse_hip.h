@@ -352,7 +352,8 @@ void rse_dispatcher_stop(void);
                                        mixing: 3 (default) bit-sliced Horner's rule, four steps per
                                        mask word unrolled; 2 the same one step at a time, 1 bit-sliced
                                        doubling chains above 4 rows, 0 v_perm tables (A/B) */
-#define RSE_OPT_WIDE_SPLIT 18       /* outputs per wave of the one-module kernels (2..8, default 8):
+#define RSE_OPT_WIDE_SPLIT 18       /* outputs per wave of the one-module kernels (2..8; 0, the
+                                       default: 8, and 4 for GF(2^8) codecs past 48 parity rows):
                                        a codec with more parity rows than this (but <= 8 x this)
                                        is coded by W waves sharing each input chunk */
 #define RSE_OPT_WIDE_BALANCE 19     /* 1 (default): W at least 4 (p >= 4) and a power of two, so a

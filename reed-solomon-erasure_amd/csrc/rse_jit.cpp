@@ -180,8 +180,14 @@ void emit_code(std::string& s, const char* name, int field, uint32_t k, uint32_t
 // more waves fit.  Same-box A/B (profiles/r02_wide4/): GF(2^8) 50+20 3.72 TB/s
 // in 4 waves vs 3.37 in 3; 10+16 5.07 in 4 vs 4.92 in 2; GF(2^16) 40+12 4.29
 // vs 4.18 in 2; 100+30 2.63 in 4 vs 2.54 in 8.
-int wide_waves(uint32_t p) {
-  const uint32_t per = wide_per_wave();
+// RSE_OPT_WIDE_SPLIT 0 (auto, the default): 8 outputs per wave, but 4 for
+// GF(2^8) codecs past 48 parity rows -- 64+64 in 16 waves of ~120 VGPRs, 4
+// per SIMD, against 8 of ~170 at 2 (same box, alternating processes, launches
+// in resident workgroups: 2.70-2.73 against 2.55-2.60 TB/s, profiles/r05/s45/
+// s64.log; 32+32 and 50+20 are not faster at 4, s32.log, s50.log).
+int wide_waves(uint32_t p, int field = 0) {
+  uint32_t per = wide_per_wave();
+  if (get_option(18) == 0 && field == 8 && p > 48) per = 4;
   int w = (int)((p + per - 1) / per);
   if (get_option(19) != 0 && p >= 4) {
     int b = 4;
@@ -227,7 +233,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   if (kind == kJitWide) {
     // one code struct per wave's share of the outputs, and the kernel (the
     // launch takes W from the build: the options may change meanwhile)
-    const int W = wide_waves(p);
+    const int W = wide_waves(p, field);
     if (wide_w) *wide_w = W;
     const bool shared = W > 1 && get_option(14) != 0;  // RSE_OPT_WIDE_LDS
     // GF(2^8) networks over pairs of inputs (RSE_OPT_WIDE_PAIRS): the LDS

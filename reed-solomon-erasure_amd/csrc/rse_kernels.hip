@@ -780,7 +780,7 @@ struct Options {
   int64_t wide_lds = 1;           // wide modules: slicing shared through LDS
   int64_t jit_disk_cache = 1;     // run-time specialised modules cached on disk
   int64_t recon_mix = 3;          // syndrome reconstruct mixing: 3/2 Horner (4 steps per word / 1), 1 doubling chains, 0 tables
-  int64_t wide_split = 8;         // outputs per wave of wide modules
+  int64_t wide_split = 0;         // outputs per wave of wide modules (0: auto, rse_jit.cpp wide_waves)
   int64_t wide_balance = 1;       // wide modules: waves per workgroup rounded to 2, 4, 8
   int64_t wide_occupancy = 0;     // wide modules: waves per SIMD compiled for (0 = auto)
   int64_t host_copy_2d = 1;       // host pipeline: 2D copies for runs of a flat buffer's shards
@@ -1321,7 +1321,7 @@ int set_option(int key, int64_t value) {
     case 14: g_opt.wide_lds = value ? 1 : 0; return 0;
     case 15: g_opt.jit_disk_cache = value ? 1 : 0; return 0;
     case 17: g_opt.recon_mix = value < 0 ? 0 : value > 3 ? 3 : value; return 0;
-    case 18: g_opt.wide_split = value < 2 ? 2 : value > 8 ? 8 : value; return 0;
+    case 18: g_opt.wide_split = value <= 0 ? 0 : value < 2 ? 2 : value > 8 ? 8 : value; return 0;
     case 19: g_opt.wide_balance = value ? 1 : 0; return 0;
     case 20: g_opt.wide_occupancy = value < 0 ? 0 : value > 4 ? 4 : value == 1 ? 2 : value; return 0;
     case 21: g_opt.host_copy_2d = value ? 1 : 0; return 0;

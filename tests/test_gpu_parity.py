@@ -1499,8 +1499,8 @@ def test_bench_ranks_rehearsal(ranks, extras, tmp_path):
 
 # (field, k, p, modules): one wide module (p <= 64, k + 2p <= 480), or
 # blocks of 8 outputs x 32 inputs beyond that.  Waves per workgroup
-# (rse_jit.cpp wide_waves): 1 for p < 4, else 4 (p <= 32) or 8 (10+40: shares
-# of 5; 4+17: 5/4/4/4).
+# (rse_jit.cpp wide_waves): 1 for p < 4, else 4 (p <= 32), 8 (10+40: shares
+# of 5; 4+17: 5/4/4/4), or 16 for GF(2^8) past 48 outputs (64+64: 4 each).
 WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
                (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9),
                (8, 32, 32, 1), (8, 64, 64, 1)]  # benches/bandwidth.rs:94-95's widest (half chunks)
@@ -1591,6 +1591,8 @@ def test_wide_codec_kernels(R, subfield, field, k, p, modules):
         if modules == 1:
             kf = 8 if field == 8 or subfield else 16  # every codec here has <= 256 shards
             assert last_kernel().startswith(f"bitslice-wide gf{kf} {k}+{p}"), last_kernel()
+            if kf == 8 and p > 48:  # RSE_OPT_WIDE_SPLIT auto: 4 outputs per wave
+                assert " w16 " in last_kernel(), last_kernel()
         for i in range(p):
             assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
         assert r.verify(t)
