@@ -419,6 +419,9 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_DISPATCH_LANE_UNITS 49 /* dispatcher: a request takes ceil(units / (this x 512))
                                         of the resident workgroups, units = 16-byte vectors x
                                         outputs (default 1); one workgroup up to 1024 units */
+#define RSE_OPT_WIDE_PIN_PAIRS 48     /* half-chunk GF(2^8) wide modules built after: XOR networks of
+                                        this many input pairs per scheduling region (1, default;
+                                        up to 8; rse_wide_ext.hpp) */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192
