@@ -59,6 +59,8 @@ def main():
                     help="RSE_OPT_WIDE_SPLIT: outputs per wave of one-module kernels (0: default)")
     ap.add_argument("--wide-lds", type=int, default=-1,
                     help="RSE_OPT_WIDE_LDS for wide-codec modules (-1: default)")
+    ap.add_argument("--batch-parity", action="store_true",
+                    help="batch: rebuild lost parity too (data_only=False)")
     ap.add_argument("--batch-cycle", type=int, default=0,
                     help="batch: stripes alternate between this many fixed patterns "
                          "(rotations of --erase) instead of random ones (0)")
@@ -127,13 +129,17 @@ def main():
         if args.op == "encode":
             r.encode_flat(buf, elems, S)
         elif args.op == "batch":
-            r.reconstruct_batch(buf, elems, S, batch_present, data_only=True)
+            r.reconstruct_batch(buf, elems, S, batch_present, data_only=not args.batch_parity)
         else:
             r.reconstruct_data_flat(buf, elems, S, present)
 
     if args.op == "batch":  # per stripe with missing data: k reads + the missing data written
         miss = (~batch_present[:, :k]).sum(axis=1)
-        nbytes = int((miss > 0).sum() * k + miss.sum()) * L
+        if args.batch_parity:  # k reads + every lost shard written
+            lost = (~batch_present).sum(axis=1)
+            nbytes = int((lost > 0).sum() * k + lost.sum()) * L
+        else:
+            nbytes = int((miss > 0).sum() * k + miss.sum()) * L
     else:
         nbytes = S * ((k + p) if args.op == "encode" else (k + len(erased))) * L
     shapes = [(512, 1), (1024, 1), (2048, 1), (4096, 1), (8, 0), (16, 0)]
