@@ -929,11 +929,13 @@ def other_configs(stream):
 
 
 # k, p, shard bytes, stripes per launch.  1000+24: galois_16.rs's reason to
-# exist (far past 256 shards); its modules are one per 8 x 32 block of the
-# parity rows (rse_jit.cpp jit_register_blocks), prebuilt into jitcache/ by
-# tools/prebuild_all.sh.  (A one-module GF(2^16) 256+16 did not finish
+# exist (far past 256 shards); it runs as a chain of 8 wide modules over
+# blocks of 125 data shards (rse_jit.cpp "wide modules over input blocks"),
+# prebuilt into jitcache/ by tools/prebuild_all.sh.  512 stripes (32 GiB) per
+# launch: the chain ran 2.32 TB/s there against 2.15 at 128
+# (profiles/r05/s19/).  (A one-module GF(2^16) 256+16 did not finish
 # compiling in 25 minutes of hiprtc on the build host.)
-GF16_PROPER = (1000, 24, 64 << 10, 128)
+GF16_PROPER = (1000, 24, 64 << 10, 512)
 
 
 def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROPER[2],
