@@ -422,6 +422,9 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_WIDE_PIN_PAIRS 48     /* half-chunk GF(2^8) wide modules built after: XOR networks of
                                         this many input pairs per scheduling region (1, default;
                                         up to 8; rse_wide_ext.hpp) */
+#define RSE_OPT_SUB_DEPTH 50          /* run-time modules built after: inputs in flight per wave of
+                                        their 1 / 2 KiB-shard kernels (1: bitslice_body; 2..4,
+                                        default 4: rse_sub_ext.hpp) */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192

@@ -63,6 +63,11 @@ const char kJitSource[] =
 const char kJitExtSource[] =
 #include "rse_jit_ext.inc"
     ;
+// rse_sub_ext.hpp (build/rse_jit_sub.inc): the 1 / 2 KiB-shard body with
+// several inputs in flight, for modules built under RSE_OPT_SUB_DEPTH > 1.
+const char kJitSubSource[] =
+#include "rse_jit_sub.inc"
+    ;
 
 struct Compiled {
   bool ok = false;
@@ -239,6 +244,10 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   // pairs per scheduling region (rse_wide_ext.hpp)
   const int pin_pairs = kind == kJitWide && field == 8 ? (int)get_option(48) : 1;
   if (pin_pairs > 1) s += kJitExtSource;
+  // RSE_OPT_SUB_DEPTH > 1: the narrow modules' 1 / 2 KiB-shard kernels with
+  // that many inputs in flight per wave (rse_sub_ext.hpp)
+  const int sub_depth = kind != kJitWide && stage == kEnc ? (int)get_option(50) : 1;
+  if (sub_depth > 1) s += kJitSubSource;
   if (kind == kJitWide) {
     // one code struct per wave's share of the outputs, and the kernel (the
     // launch takes W from the build: the options may change meanwhile)
@@ -346,12 +355,19 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       s += buf;
       // 1 / 2 KiB shards: 4 / 2 stripes per 4 KiB chunk (bitslice_body SUB)
       for (int q = 1; q <= 2; ++q) {
-        std::snprintf(buf, sizeof buf,
-                      "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode_s%d(\n"
-                      "    const rse::CodeArgs a, uint64_t cps) {\n"
-                      "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, true, "
-                      "false, false, %du>(a, cps);\n}\n",
-                      p > 4 ? 2 : 3, q, 1024 * q);
+        if (sub_depth > 1)
+          std::snprintf(buf, sizeof buf,
+                        "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode_s%d(\n"
+                        "    const rse::CodeArgs a, uint64_t cps) {\n"
+                        "  rse::bitslice_body_sub_deep<rse::JitCode, %d, %du>(a, cps);\n}\n",
+                        p > 4 ? 2 : 3, q, sub_depth, 1024 * q);
+        else
+          std::snprintf(buf, sizeof buf,
+                        "extern \"C\" __global__ __launch_bounds__(256, %d) void rse_jit_encode_s%d(\n"
+                        "    const rse::CodeArgs a, uint64_t cps) {\n"
+                        "  rse::bitslice_body<rse::JitCode, true, true, false, false, false, true, "
+                        "false, false, %du>(a, cps);\n}\n",
+                        p > 4 ? 2 : 3, q, 1024 * q);
         s += buf;
       }
     }

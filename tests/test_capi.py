@@ -302,7 +302,7 @@ def test_every_header_option_is_readable():
     assert L.rse_set_option(99, 1) != 0
     want = {"RSE_OPT_RECON_PAIRS": 8, "RSE_OPT_WIDE_PAIRS": 1, "RSE_OPT_SYNC_EVENT": 0,
             "RSE_OPT_SPIN_WAIT": 1, "RSE_OPT_HOST_DIRECT": 1, "RSE_OPT_WIDE_BLOCK_INPUTS": 128,
-            "RSE_OPT_DISPATCH_MAX_BYTES": 65536}
+            "RSE_OPT_DISPATCH_MAX_BYTES": 65536, "RSE_OPT_SUB_DEPTH": 4}
     for name, v in want.items():
         assert L.rse_get_option(keys[name]) == v, name
     old = L.rse_get_option(keys["RSE_OPT_SPIN_WAIT"])

@@ -1756,6 +1756,22 @@ def test_jit_verify_completion_word(R, k, p):
         lib.rse_set_option(9, old)
 
 
+@pytest.mark.parametrize("depth,field,k,p", [(1, 8, 7, 3), (2, 8, 6, 5), (3, 16, 9, 2)])
+def test_sub_chunk_depth_option(R, depth, field, k, p):
+    """RSE_OPT_SUB_DEPTH: the narrow modules' 1 / 2 KiB kernels with 1 input in
+    flight per wave (bitslice_body, round 4's kernels) or 2 / 3 (rse_sub_ext.hpp;
+    the default 4 runs in test_sub_chunk_shards): the same checks.  Codecs no
+    other test builds (modules are keyed by rows, not options)."""
+    lib = R._lib.load()
+    old = lib.rse_get_option(50)
+    try:
+        assert lib.rse_set_option(50, depth) == 0
+        for kib in (1, 2):
+            test_sub_chunk_shards(R, field, k, p, kib)
+    finally:
+        lib.rse_set_option(50, old)
+
+
 @pytest.mark.parametrize("field,k,p", [
     (8, 10, 4), (8, 10, 2), (16, 20, 8),   # compiled codecs
     (8, 4, 4), (8, 8, 8), (8, 5, 2), (16, 6, 3),  # run-time specialised
