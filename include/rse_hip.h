@@ -105,6 +105,8 @@ int rse_codec_matrix(const rse_codec *codec, uint8_t *out, size_t out_bytes);
 #define RSE_KERNELS_SPECIALISED 2       /* bit-sliced, specialised at run time, ready */
 #define RSE_KERNELS_SPECIALISING 3      /* compile in flight (wait == 0) */
 #define RSE_KERNELS_SPECIALISE_FAILED 4 /* compile failed: table kernels */
+#define RSE_KERNELS_FFT 5               /* additive-FFT kernels, compiled into the library
+                                           (GF(2^8) k = p = 16, 32, 64; RSE_OPT_FFT) */
 int rse_codec_kernel_kind(const rse_codec *codec, int wait);
 
 /* encode (core.rs:597-611): shards[0..k] data, shards[k..k+p] parity (overwritten). */
@@ -425,6 +427,11 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_SUB_DEPTH 50          /* run-time modules built after: inputs in flight per wave of
                                         their 1 / 2 KiB-shard kernels (1: bitslice_body; 2..4,
                                         default 4: rse_sub_ext.hpp) */
+#define RSE_OPT_FFT 51                /* 1 (default): GF(2^8) codecs with k = p = 16, 32 or 64
+                                        (benches/bandwidth.rs's 16+16 .. 64+64) encode, verify and
+                                        rebuild all data shards from the parity shards on additive-FFT
+                                        kernels ((k/2) log2 k butterflies per transform instead of
+                                        k x p coefficient networks; same bytes); 0: the wide modules */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192

@@ -27,6 +27,7 @@
 
 #include "../../include/rse_hip.h"
 #include "rse_dispatch.hpp"
+#include "rse_fft.hpp"
 #include "rse_wideblk.hpp"
 #include "rse_field.hpp"
 #include "rse_kernels.hpp"
@@ -269,6 +270,26 @@ int run_job(const Job& j, hipStream_t s) {
       g.field = RSE_FIELD_GF8;
       return run_job(g, s);
     }
+  }
+  // GF(2^8) k = p = 16 / 32 / 64: the codec's parity rows (encode, verify) or
+  // their inverse (all data shards rebuilt from the parity) on the additive-FFT
+  // kernels (rse_fft.hip): every whole 2 KiB column (1 KiB shards: all), the
+  // rest of every shard below
+  if (!j.accumulate && j.field == RSE_FIELD_GF8 && n_in == n_out && j.stripe_stride % 16u == 0 &&
+      rse::get_option(RSE_OPT_BITSLICE) && j.n_stripes <= 0xffffffffu &&
+      rse::fft_direction(8, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data())) {
+    bool al = true;
+    for (size_t i = 0; i < n_in; ++i) al = al && aligned16(j.in[i]);
+    for (size_t r = 0; r < n_out; ++r) {
+      if (j.mode != rse::kCheck) al = al && aligned16(j.out[r]);
+      if (j.mode != rse::kStore) al = al && aligned16(j.cmp[r]);
+    }
+    uint64_t done = 0;
+    if (al)
+      RSE_HIP(rse::launch_fft(j.field, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data(), j.in,
+                              j.out, j.cmp, j.len_bytes, j.stripe_stride, (uint32_t)j.n_stripes,
+                              j.mode, j.mismatch, j.per_stripe, s, &done));
+    if (done) return done == j.len_bytes ? RSE_OK : run_rest(j, done, s);
   }
   // a wide codec's (or pattern's) rows with their one-module kernel built:
   // every whole 4 KiB chunk in one launch (each input read once, each output
@@ -719,6 +740,8 @@ void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_
   c->jit_requested.store(true, std::memory_order_relaxed);
   if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
+  // k = p = 16 / 32 / 64: the compiled additive-FFT kernels (rse_fft.hip)
+  if (rse::fft_direction(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data())) return;
   if (wide && rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p))
     rse::jit_register_wide(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else if (wide)
@@ -1045,12 +1068,22 @@ int run_plan_tail(const rse_codec* c, const ReconPlan& plan, size_t off, uint64_
   return run_job(j, s);
 }
 
+// Every data shard of a k = p = 16 / 32 / 64 GF(2^8) codec rebuilt from its
+// parity shards: run_job codes the plan's rows on the additive-FFT kernels
+// (rse_fft.hip), so neither a pattern module nor the syndrome kernels apply.
+bool fft_plan(const rse_codec* c, const ReconPlan& plan) {
+  return plan.rows.n_in == plan.rows.n_out &&
+         rse::fft_direction(c->kfield, (uint32_t)plan.rows.n_in, (uint32_t)plan.rows.n_out,
+                            plan.rows.c.data()) < 0;
+}
+
 int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens,
                      const uint8_t* present, size_t n, bool data_only, hipStream_t s) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   ReconPlan plan;
   int rc = plan_reconstruct(c, shards, lens, present, n, data_only, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
+  if (fft_plan(c, plan)) return run_plan_tail(c, plan, 0, 0, 1, s);
   if (pattern_kernel(c, plan, plan.len * c->esize())) {
     ++g_pattern_launches;
     return run_plan_tail(c, plan, 0, 0, 1, s);  // launch_code finds the pattern's kernel
@@ -1082,6 +1115,7 @@ int flat_reconstruct(const rse_codec* c, uint8_t* base, size_t shard_len, size_t
   int rc = plan_reconstruct(c, ptrs.data(), lens.data(), present, c->total, data_only, plan);
   if (rc || plan.nothing_to_do || plan.rows.n_out == 0) return rc;
   const uint64_t stride = (uint64_t)c->total * sb;
+  if (fft_plan(c, plan)) return run_plan_tail(c, plan, 0, stride, n_stripes, s);
   if (pattern_kernel(c, plan, sb, sb * n_stripes)) {
     ++g_pattern_launches;
     return run_plan_tail(c, plan, 0, stride, n_stripes, s);
@@ -1690,8 +1724,10 @@ size_t rse_codec_total_shard_count(const rse_codec* c) { return c ? c->total : 0
 int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
-  if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const Rows rows = parity_rows(c);
+  if (rse::fft_direction(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data()))
+    return RSE_KERNELS_FFT;
+  if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||
                     rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
   const bool one = rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p);
@@ -1804,17 +1840,52 @@ namespace {
 // result in device memory, and neither is ordered after the caller's streams:
 // the caller has finished writing the inputs (the reference's synchronous
 // contract, core.rs:597-695).
+// The device that holds every shard of a *_now call (the call has no stream
+// to take it from): *dev, or RSE_ERR_INVALID_ARGUMENT for host memory or
+// shards on different devices.  One runtime query per allocation, not per
+// shard: a shard inside the allocation range found last needs none.
+int now_device(const uint8_t* const* a, size_t na, const uint8_t* const* b, size_t nb, int* dev) {
+  int d0 = -1;
+  uintptr_t lo = 0, hi = 0;
+  for (size_t i = 0; i < na + nb; ++i) {
+    const uint8_t* q = i < na ? a[i] : b[i - na];
+    const uintptr_t u = reinterpret_cast<uintptr_t>(q);
+    if (u >= lo && u < hi) continue;
+    int d = -1;
+    if (!device_memory(q, &d) || (d0 >= 0 && d != d0)) return RSE_ERR_INVALID_ARGUMENT;
+    d0 = d;
+    void* base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<uint8_t*>(q)) == hipSuccess && base) {
+      lo = reinterpret_cast<uintptr_t>(base);
+      hi = lo + size;
+    } else {
+      (void)hipGetLastError();
+      lo = hi = 0;
+    }
+  }
+  *dev = d0;
+  return RSE_OK;
+}
+
 int run_now(const rse_codec* c, const Rows& rows, const uint8_t* const* in, uint8_t* const* out,
             const uint8_t* const* cmp, size_t len_bytes, bool* mismatch) {
   const bool check = cmp != nullptr;
   uint8_t* const* tgt = check ? const_cast<uint8_t* const*>(cmp) : out;
+  // the shards' device for the whole call (not whichever is current)
+  int dev = -1;
+  if (const int rc = now_device(in, rows.n_in, tgt, rows.n_out, &dev)) return rc;
+  OnDevice on_dev(dev);
   if (rse::dispatch_applies(c->kfield, (uint32_t)rows.n_in, (uint32_t)rows.n_out, len_bytes, in,
                             tgt)) {
     bool mm = false;
-    RSE_HIP(rse::dispatch_run(rows.c.data(), (uint32_t)rows.n_in, (uint32_t)rows.n_out, in, tgt,
-                              len_bytes, check, &mm));
-    if (mismatch) *mismatch = mm;
-    return RSE_OK;
+    const hipError_t e = rse::dispatch_run(rows.c.data(), (uint32_t)rows.n_in,
+                                           (uint32_t)rows.n_out, in, tgt, len_bytes, check, &mm);
+    if (e == hipSuccess) {
+      if (mismatch) *mismatch = mm;
+      return RSE_OK;
+    }
+    if (e != hipErrorNotSupported) RSE_HIP(e);  // not usable on this device: launch instead
   }
   Lease lease;
   RSE_HIP(lease.acquire());

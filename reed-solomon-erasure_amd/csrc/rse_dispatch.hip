@@ -30,11 +30,16 @@
 //    kernel takes the pending request (it starts from the last sequence
 //    number served).
 //
-// Memory ordering.  Inputs are read with non-temporal loads (they bypass the
-// CU's L1, which would otherwise keep lines of an earlier request), outputs are
-// written with write-through (sc1) stores and drained (s_waitcnt vmcnt(0))
-// before the ack, so later kernels on any XCD read them from memory
-// (MI355X_MICROARCH.md, inter-workgroup visibility).  Only vector stores are
+// Memory ordering (MI355X_MICROARCH.md, inter-workgroup visibility).  The
+// inputs come from kernels that completed before the call (the contract of
+// the *_now entries: the caller has finished writing them), so their bytes
+// were released at the end of those kernels.  The consumer side is the
+// guide's valid form: one relaxed poll, then ONE agent-scope acquire per
+// request on every coding workgroup's CU (its L1 invalidated; the table
+// building overlaps the invalidate, which completes at an s_waitcnt vmcnt(0)
+// before the workgroup barrier), then the loads.  Outputs are written with
+// write-through (sc1) stores and drained (s_waitcnt vmcnt(0)) before the ack,
+// so later kernels on any XCD read them from memory.  Only vector stores are
 // used.
 #include <hip/hip_runtime.h>
 
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
   const bool lead = blockIdx.x == 0;
   uint64_t* ack = acks + (size_t)blockIdx.x * kAckStride;
   uint64_t last = now_ticks();
+  uint64_t last_ack = seen;  // thread 0: the last ack stored (seq | mismatch)
   for (;;) {
     if (wave == 0) {
       uint32_t state = 0;
@@ -205,6 +211,7 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
             const uint32_t n_wg = (uint32_t)(__shfl(g0.w, 0) >> 16) & 0xFFu;  // b bits 48..55
             if ((__shfl(g0.y, 0) & 0xFu) == kOpStop) state = 2;  // a stop request: end now
             else if (blockIdx.x >= n_wg) state = 3;              // not one of its workgroups
+            else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1 invalidated
           }
         }
       }
@@ -240,6 +247,8 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
       const Gf8Tab t = make_gf8_tab(coef);
       write_tab(tq, tt, (int)c, t);
     }
+    // the acquire's invalidate has completed before any wave loads an input
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint64_t n_vec = len / 16u;
     // outputs per item: enough items for the threads, at most 8
@@ -253,13 +262,15 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
     if (diff) atomicOr(&s_diff, 1u);
     __syncthreads();
     if (tid == 0) {
-      const uint64_t a = (uint64_t)seen | (s_diff ? kAckMismatch : 0ull);
-      __hip_atomic_store(ack, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      last_ack = (uint64_t)seen | (s_diff ? kAckMismatch : 0ull);
+      __hip_atomic_store(ack, last_ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     last = now_ticks();
     __syncthreads();
   }
-  if (tid == 0) __hip_atomic_store(ack, (uint64_t)seen | kAckExit, __ATOMIC_RELAXED,
+  // the exit ack keeps the last request served and its verdict: a host that
+  // reads it late still finds its request served
+  if (tid == 0) __hip_atomic_store(ack, last_ack | kAckExit, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -267,6 +278,7 @@ __global__ __launch_bounds__(kDispThreads) void rse_dispatch_kernel(const Granul
 struct Dispatcher {
   std::mutex mu;
   bool init = false, running = false;
+  bool broken = false;  // a kernel that outlived a timed-out request: not used again
   hipStream_t st = nullptr;
   Granule* req = nullptr;  // pinned, mapped: host view
   Granule* dreq = nullptr;
@@ -322,6 +334,39 @@ hipError_t disp_launch(Dispatcher& d, uint32_t at_least = 1) {
   return e;
 }
 
+// Posts a stop request (the next sequence number, one granule): workgroups
+// that had not taken the pending request never will, one that is coding it
+// ends after it.  Called with d.mu held.
+void post_stop(Dispatcher& d) {
+  const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;
+  volatile Granule* r = d.req;
+  r[0].a = kOpStop | (1u << 20);  // one granule
+  r[0].b = 0;
+  std::atomic_thread_fence(std::memory_order_release);
+  r[0].tag = seq;
+  d.seq = seq;
+}
+
+// A request that timed out is taken back before the call fails: a stop is
+// posted and the kernel is waited for (up to 2 s), so it cannot write the
+// caller's outputs after the call has returned.  A kernel that does not end
+// marks the dispatcher broken: later calls on the device take the launch
+// path.  Called with d.mu held.
+void retract(Dispatcher& d) {
+  post_stop(d);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+    const hipError_t q = hipStreamQuery(d.st);
+    if (q != hipErrorNotReady) {
+      d.running = false;
+      d.served = d.seq;
+      return;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  d.broken = true;
+}
+
 }  // namespace
 
 bool dispatch_applies(int field, uint32_t n_in, uint32_t n_out, uint64_t len_bytes,
@@ -351,6 +396,7 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
   if (dev < 0 || dev >= kDispDevs) return hipErrorInvalidDevice;
   Dispatcher& d = dispatcher(dev);
   std::lock_guard<std::mutex> g(d.mu);
+  if (d.broken) return hipErrorNotSupported;  // the caller takes the launch path
   if ((e = disp_init(d)) != hipSuccess) return e;
   const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;  // 0: the zeroed ring
   const uint32_t n_gran = 1 + n_in + n_out + (n_in * n_out + 11) / 12;
@@ -412,7 +458,7 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
   for (uint32_t w = 0; w < n_wg;) {
     for (uint64_t n = 1;; ++n) {
       const uint64_t a = ack[w * kAckStride];
-      if ((uint32_t)a == seq && !(a & kAckExit)) {
+      if ((uint32_t)a == seq) {  // served (an exit ack keeps the last request served)
         mm = mm || (a & kAckMismatch) != 0;
         ++w;
         break;
@@ -425,8 +471,10 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
         const hipError_t q = hipStreamQuery(d.st);
         if (q != hipErrorNotReady && q != hipSuccess) return q;
         again = q == hipSuccess && ack[w * kAckStride] == a;  // ended without our ack
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+          retract(d);
           return hipErrorLaunchTimeOut;
+        }
         if (!again) continue;
       }
       if ((e = hipStreamSynchronize(d.st)) != hipSuccess) return e;
@@ -449,19 +497,13 @@ void dispatch_stop_all() {
   for (int dev = 0; dev < kDispDevs; ++dev) {
     Dispatcher& d = dispatcher(dev);
     std::lock_guard<std::mutex> g(d.mu);
-    if (!d.init || !d.running) continue;
+    if (!d.init || !d.running || d.broken) continue;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) continue;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) continue;
-    const uint32_t seq = d.seq + 1 == 0 ? 1 : d.seq + 1;
-    volatile Granule* r = d.req;
-    r[0].a = kOpStop | (1u << 20);  // one granule
-    r[0].b = 0;
-    std::atomic_thread_fence(std::memory_order_release);
-    r[0].tag = seq;
-    d.seq = seq;
+    post_stop(d);
     (void)hipStreamSynchronize(d.st);  // it takes the stop (or has idled out)
-    d.served = seq;
+    d.served = d.seq;
     d.running = false;
     if (cur != dev) (void)hipSetDevice(cur);
   }

@@ -154,7 +154,7 @@ class ReedSolomon:
 
     # rse_codec_kernel_kind values (include/rse_hip.h); no reference counterpart
     KERNELS = {0: "table", 1: "bitslice-compiled", 2: "bitslice-specialised",
-               3: "specialising", 4: "specialise-failed"}
+               3: "specialising", 4: "specialise-failed", 5: "fft-compiled"}
 
     def kernel_kind(self, wait: bool = False) -> str:
         """Which kernels code this codec (results are identical either way):

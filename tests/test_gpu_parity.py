@@ -1576,9 +1576,12 @@ def test_wide_codec_kernels(R, subfield, field, k, p, modules):
     full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
     oc.encode(full)
     blocks = modules
-    old = lib.rse_get_option(9)
+    old, old51 = lib.rse_get_option(9), lib.rse_get_option(51)
     try:
         assert lib.rse_set_option(9, 2) == 0
+        # k = p = 16 / 32 / 64 default to the FFT kernels (tests/test_gpu_fft.py):
+        # the wide modules here are their RSE_OPT_FFT 0 path
+        assert lib.rse_set_option(51, 0) == 0
         r = R.core.ReedSolomon(k, p, field)
         assert r.kernel_kind(wait=True) == "bitslice-specialised"
         t = [dev(x).reshape(shape) for x in full[:k]] + \
@@ -1618,6 +1621,7 @@ def test_wide_codec_kernels(R, subfield, field, k, p, modules):
                 assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
     finally:
         lib.rse_set_option(9, old)
+        lib.rse_set_option(51, old51)
 
 
 def test_wide_block_chain_gf16_past_256(R):
@@ -1795,9 +1799,10 @@ def test_sub_chunk_shards(R, field, k, p, kib):
     n = nb // es
     T = k + p
     oc = O.Codec(field, k, p)
-    old9, old33 = lib.rse_get_option(9), lib.rse_get_option(33)
+    old9, old33, old51 = lib.rse_get_option(9), lib.rse_get_option(33), lib.rse_get_option(51)
     try:
         lib.rse_set_option(9, 2)  # run-time builds waited for
+        lib.rse_set_option(51, 0)  # 16+16 .. 64+64: the wide modules, not the FFT kernels
         r = R.core.ReedSolomon(k, p, field)
         assert r.kernel_kind(wait=True).startswith("bitslice")
         for stripes in (1, 3, 6, 1001):
@@ -1844,6 +1849,7 @@ def test_sub_chunk_shards(R, field, k, p, kib):
     finally:
         lib.rse_set_option(9, old9)
         lib.rse_set_option(33, old33)
+        lib.rse_set_option(51, old51)
 
 
 def test_wide_launch_follows_the_module_not_the_options(R):

@@ -12,6 +12,9 @@
 //   I  rse_encode_now 10+4 x 1 KiB (the resident dispatcher)
 //   J  rse_encode_now by shard size: 1, 8, 32 dispatcher workgroups, and the launch path
 //   K  rse_encode_now 4-64 KiB: 8 / 16 resident workgroups, 1 / 2 / 4 units per lane
+//   L  rse_encode_now back to back, and each followed by hipDeviceSynchronize, by idle time
+//   M  a kernel on another stream + its synchronisation between rse_encode_now calls
+// argv[1] (optional): the letters of the cases to run.
 // The resident kernel of E exits on a stop value or after a bounded number of
 // polls, so it always drains.
 //   hipcc --offload-arch=gfx950 -O2 -I include tools/latency_probe.hip \
@@ -23,6 +26,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "rse_hip.h"
@@ -85,7 +89,11 @@ struct Stat {
   }
 };
 
-int main() {
+static const char* g_cases = nullptr;  // argv[1]: the case letters to run (all when absent)
+bool want(char c) { return !g_cases || std::strchr(g_cases, c); }
+
+int main(int argc, char** argv) {
+  if (argc > 1) g_cases = argv[1];
   const int reps = 2000;
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -96,7 +104,7 @@ int main() {
   uint32_t* dw = nullptr;
   CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dw), hw, 0));
 
-  {  // A
+  if (want('A')) {  // A
     Stat s;
     for (int i = 0; i < reps + 50; ++i) {
       const auto t0 = clk::now();
@@ -106,7 +114,7 @@ int main() {
     }
     s.report("A empty kernel + hipStreamSynchronize");
   }
-  {  // B
+  if (want('B')) {  // B
     Stat s;
     for (int i = 0; i < reps + 50; ++i) {
       const uint32_t want = (uint32_t)i + 1;
@@ -118,7 +126,7 @@ int main() {
     CK(hipStreamSynchronize(st));
     s.report("B empty kernel, host spins on a pinned word");
   }
-  {  // H: empty kernel + stream memory write, host spins
+  if (want('H')) {  // H: empty kernel + stream memory write, host spins
     Stat s;
     for (int i = 0; i < reps + 50; ++i) {
       const uint32_t want = 0x20000u + (uint32_t)i;
@@ -131,7 +139,7 @@ int main() {
     CK(hipStreamSynchronize(st));
     s.report("H empty kernel + hipStreamWriteValue32, host spins");
   }
-  {  // C, D
+  if (want('C')) {  // C, D
     rse_codec* c = nullptr;
     if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
     const size_t L = 1024, T = 14;
@@ -186,7 +194,7 @@ int main() {
     rse_codec_free(c);
     CK(hipFree(buf));
   }
-  {  // J: rse_encode_now by shard size and dispatcher workgroups, against the launch path
+  if (want('J')) {  // J: rse_encode_now by shard size and dispatcher workgroups, against the launch path
     rse_codec* c = nullptr;
     if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
     const size_t T = 14, Lmax = 1u << 20;
@@ -226,7 +234,7 @@ int main() {
     rse_codec_free(c);
     CK(hipFree(buf));
   }
-  {  // K: workgroups per request (RSE_OPT_DISPATCH_LANE_UNITS) at 8 and 16 resident ones
+  if (want('K')) {  // K: workgroups per request (RSE_OPT_DISPATCH_LANE_UNITS) at 8 and 16 resident ones
     rse_codec* c = nullptr;
     if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
     const size_t T = 14, Lmax = 1u << 16;
@@ -264,7 +272,7 @@ int main() {
     rse_codec_free(c);
     CK(hipFree(buf));
   }
-  {  // E
+  if (want('E')) {  // E
     hipStream_t rs;
     CK(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
     volatile uint32_t* db = vw + 16;
@@ -292,7 +300,7 @@ int main() {
     if (!ok) std::printf("E: responder did not answer\n");
     CK(hipStreamDestroy(rs));
   }
-  {  // F
+  if (want('F')) {  // F
     Stat s;
     for (int i = 0; i < reps; ++i) {
       const auto t0 = clk::now();
@@ -301,6 +309,55 @@ int main() {
       if (q != hipSuccess) return 5;
     }
     s.report("F hipStreamQuery, idle stream");
+  }
+  if (want('L')) {  // L: encode_now then a device-wide synchronisation (torch.cuda.synchronize),
+                    // by the dispatcher's idle time; M: a kernel on another stream between calls
+    rse_codec* c = nullptr;
+    if (rse_codec_new(RSE_FIELD_GF8, 10, 4, &c)) return 3;
+    const size_t T = 14, L = 1024;
+    uint8_t* buf = nullptr;
+    CK(hipMalloc(reinterpret_cast<void**>(&buf), T * L));
+    CK(hipMemset(buf, 7, T * L));
+    std::vector<void*> sh(T);
+    std::vector<size_t> lens(T, L);
+    for (size_t i = 0; i < T; ++i) sh[i] = buf + i * L;
+    hipStream_t other;
+    CK(hipStreamCreateWithFlags(&other, hipStreamNonBlocking));
+    for (int idle : {2000, 200, 50}) {
+      rse_set_option(RSE_OPT_DISPATCH_IDLE_US, idle);
+      rse_dispatcher_stop();
+      char name[96];
+      Stat a, b, m;
+      for (int i = 0; i < 520; ++i) {
+        const auto t0 = clk::now();
+        if (rse_encode_now(c, sh.data(), lens.data(), T)) return 4;
+        if (i >= 20) a.v.push_back(us_since(t0));
+      }
+      std::snprintf(name, sizeof name, "L encode_now 10+4 x 1 KiB back to back, idle %d us", idle);
+      a.report(name);
+      for (int i = 0; i < 220; ++i) {
+        const auto t0 = clk::now();
+        if (rse_encode_now(c, sh.data(), lens.data(), T)) return 4;
+        CK(hipDeviceSynchronize());
+        if (i >= 20) b.v.push_back(us_since(t0));
+      }
+      std::snprintf(name, sizeof name, "L encode_now + hipDeviceSynchronize, idle %d us", idle);
+      b.report(name);
+      for (int i = 0; i < 520; ++i) {
+        if (rse_encode_now(c, sh.data(), lens.data(), T)) return 4;
+        const auto t0 = clk::now();
+        hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, other, nullptr, 0u);
+        CK(hipStreamSynchronize(other));
+        if (i >= 20) m.v.push_back(us_since(t0));
+      }
+      std::snprintf(name, sizeof name, "M other stream's kernel + sync after encode_now, idle %d", idle);
+      m.report(name);
+    }
+    rse_set_option(RSE_OPT_DISPATCH_IDLE_US, 2000);
+    rse_dispatcher_stop();
+    CK(hipStreamDestroy(other));
+    rse_codec_free(c);
+    CK(hipFree(buf));
   }
   CK(hipHostFree(hw));
   CK(hipStreamDestroy(st));
