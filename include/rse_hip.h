@@ -432,6 +432,11 @@ void rse_dispatcher_stop(void);
                                         rebuild all data shards from the parity shards on additive-FFT
                                         kernels ((k/2) log2 k butterflies per transform instead of
                                         k x p coefficient networks; same bytes); 0: the wide modules */
+#define RSE_OPT_HOST_QUEUES 52        /* host pipeline (*_host, *_host_flat) streams: 1 (default) each
+                                         on a hardware queue of its own, so the H2D and D2H copies
+                                         never queue behind each other whatever other streams the
+                                         process holds; 2 the D2H stream at high priority; 0 plain
+                                         streams (A/B) */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192

@@ -271,13 +271,13 @@ int run_job(const Job& j, hipStream_t s) {
       return run_job(g, s);
     }
   }
-  // GF(2^8) k = p = 16 / 32 / 64: the codec's parity rows (encode, verify) or
-  // their inverse (all data shards rebuilt from the parity) on the additive-FFT
-  // kernels (rse_fft.hip): every whole 2 KiB column (1 KiB shards: all), the
+  // GF(2^8) k = p = 16 / 32 / 64: the codec's parity rows (encode, verify; also
+  // their own inverse, so all data shards rebuilt from the parity) on the
+  // additive-FFT kernels (rse_fft.hip): every whole 2 KiB column (1 KiB shards: all), the
   // rest of every shard below
   if (!j.accumulate && j.field == RSE_FIELD_GF8 && n_in == n_out && j.stripe_stride % 16u == 0 &&
       rse::get_option(RSE_OPT_BITSLICE) && j.n_stripes <= 0xffffffffu &&
-      rse::fft_direction(8, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data())) {
+      rse::fft_applies(8, (uint32_t)n_in, (uint32_t)n_out, j.rows->c.data())) {
     bool al = true;
     for (size_t i = 0; i < n_in; ++i) al = al && aligned16(j.in[i]);
     for (size_t r = 0; r < n_out; ++r) {
@@ -424,6 +424,7 @@ struct Scratch {
   size_t words = 0;
   hipStream_t own = nullptr;
   int nh = 0, ring = 0;  // host pipeline: nh H2D streams + kernel + D2H
+  int qmode = -1;        // ... created under this RSE_OPT_HOST_QUEUES
   std::vector<hipStream_t> st;
   std::vector<hipEvent_t> h2d, coded, d2h;
   hipEvent_t start = nullptr;
@@ -587,15 +588,47 @@ hipError_t lease_ring(Scratch* r, size_t dbytes) {
   return hipSuccess;
 }
 
+// One stream of the host pipeline.  HIP maps streams onto at most
+// GPU_MAX_HW_QUEUES (4) hardware queues per priority, least-used first, so
+// once the process holds a few streams (torch's, the caller's, other leases')
+// the pipeline's H2D and D2H streams can share one queue.  Commands of one
+// queue start in order, so the D2H copy that waits for a chunk's kernel then
+// holds up the next chunks' H2D copies behind it: the duplex halves (the
+// bench's pinned-host leg read 41.6 against 76.1 GB/s for the same call,
+// VERDICT r05).  RSE_OPT_HOST_QUEUES 1 (default) gives every pipeline stream
+// a hardware queue of its own: a stream with a CU mask (all CUs) is never
+// mapped onto a shared queue.  2: the D2H stream at high priority instead (a
+// queue pool of its own), the other streams plain.  0: plain streams.
+hipError_t pipe_stream(int qmode, bool d2h, hipStream_t* q) {
+  if (qmode == 1) {
+    int dev = 0, n_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask(((size_t)std::max(n_cu, 1) + 31) / 32, 0u);
+    for (int i = 0; i < n_cu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+    e = hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data());
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();  // no dedicated queue: a plain stream
+  }
+  if (qmode == 2 && d2h) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+      return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
+  }
+  return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
+}
+
 // The host pipeline's streams and events for (nh, ring), and a kept ring of
 // dbytes if that is at most kPipeRingKeep.
 hipError_t lease_pipe(Scratch* r, int nh, int ring, size_t dbytes) {
   hipError_t e = hipSuccess;
-  if (r->nh != nh || r->ring != ring) {
+  const int qmode = (int)rse::get_option(RSE_OPT_HOST_QUEUES);
+  if (r->nh != nh || r->ring != ring || r->qmode != qmode) {
     drop_pipe_streams(*r);
     for (int i = 0; i < nh + 2 && e == hipSuccess; ++i) {
       hipStream_t q = nullptr;
-      e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+      e = pipe_stream(qmode, i == nh + 1, &q);
       if (e == hipSuccess) r->st.push_back(q);
     }
     for (auto* ev : {&r->h2d, &r->coded, &r->d2h})
@@ -610,6 +643,7 @@ hipError_t lease_pipe(Scratch* r, int nh, int ring, size_t dbytes) {
     }
     r->nh = nh;
     r->ring = ring;
+    r->qmode = qmode;
   }
   if (!r->start) {
     e = hipEventCreateWithFlags(&r->start, hipEventDisableTiming);
@@ -741,7 +775,7 @@ void want_bitslice(const rse_codec* c, size_t len_bytes, bool now = false, size_
   if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return;
   const Rows rows = parity_rows(c);
   // k = p = 16 / 32 / 64: the compiled additive-FFT kernels (rse_fft.hip)
-  if (rse::fft_direction(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data())) return;
+  if (rse::fft_applies(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data())) return;
   if (wide && rse::wide_eligible((uint32_t)c->k, (uint32_t)c->p))
     rse::jit_register_wide(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data(), false);
   else if (wide)
@@ -1073,8 +1107,8 @@ int run_plan_tail(const rse_codec* c, const ReconPlan& plan, size_t off, uint64_
 // (rse_fft.hip), so neither a pattern module nor the syndrome kernels apply.
 bool fft_plan(const rse_codec* c, const ReconPlan& plan) {
   return plan.rows.n_in == plan.rows.n_out &&
-         rse::fft_direction(c->kfield, (uint32_t)plan.rows.n_in, (uint32_t)plan.rows.n_out,
-                            plan.rows.c.data()) < 0;
+         rse::fft_applies(c->kfield, (uint32_t)plan.rows.n_in, (uint32_t)plan.rows.n_out,
+                          plan.rows.c.data());
 }
 
 int reconstruct_impl(const rse_codec* c, void* const* shards, const size_t* lens,
@@ -1725,7 +1759,7 @@ int rse_codec_kernel_kind(const rse_codec* c, int wait) {
   if (!c) return RSE_ERR_INVALID_ARGUMENT;
   if (rse::bitslice_compiled(c->kfield, (uint32_t)c->k, (uint32_t)c->p)) return RSE_KERNELS_COMPILED;
   const Rows rows = parity_rows(c);
-  if (rse::fft_direction(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data()))
+  if (rse::fft_applies(c->kfield, (uint32_t)c->k, (uint32_t)c->p, rows.c.data()))
     return RSE_KERNELS_FFT;
   if (wait) want_bitslice(c, rse::bitslice_chunk_bytes(), true);
   const bool wide = c->k > (size_t)kMaxIn || c->p > rse::kJitMaxOut ||

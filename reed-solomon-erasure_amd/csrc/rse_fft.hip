@@ -16,11 +16,14 @@
 //     a ^= s^_i(beta ^ j) . b;   b ^= a
 // (level i, block offset j), and its inverse interpolates.  Encode is the
 // inverse transform on U (the data values -> P in the novel basis) followed
-// by the forward transform on k ^ U (-> the parity values); rebuilding every
-// data shard from the parity shards is the same pair with the cosets swapped.
-// The polynomial is unique, so the bytes are the reference's exactly
-// (tests/test_oracle_golden.py checks the transform against the oracle's
-// encode and reconstruct; tests/test_gpu_parity.py the kernels).
+// by the forward transform on k ^ U (-> the parity values).  Rebuilding every
+// data shard from the parity shards is the same map: Q(x) = P(x ^ k) has
+// degree < k too and swaps the two cosets (i <-> k ^ i = k + i for i < k), so
+// the k x k parity block is its own inverse and one kernel serves encode,
+// verify and the rebuild (tests/test_fft_math.py checks the involution on the
+// oracle's matrices).  The polynomial is unique, so the bytes are the
+// reference's exactly (tests/test_fft_math.py checks the transform against the
+// oracle's encode and reconstruct; tests/test_gpu_fft.py the kernels).
 //
 // Cost.  (k/2) log2 k butterflies per transform, each one constant multiply
 // (an 8 x 8 bit matrix: a v_bitop3 XOR network over the bit-sliced planes)
@@ -203,9 +206,9 @@ __device__ __forceinline__ void fft_get(const uint4 (&slot)[2][64], uint32_t (&x
   x[7] = b.w;
 }
 
-// The kernel: K = k = p, B0 / B1 the cosets of the inputs / outputs (encode:
-// 0 / K; rebuilding the data from the parity: K / 0), SUB 1024 for 1 KiB
-// shards (two stripes per 2 KiB column), else 0 (whole 2 KiB columns).
+// The kernel: K = k = p, B0 / B1 the cosets of the inputs / outputs (0 / K:
+// the parity rows, which are also their inverse), SUB 1024 for 1 KiB shards
+// (two stripes per 2 KiB column), else 0 (whole 2 KiB columns).
 template <int K, uint32_t B0, uint32_t B1, uint32_t SUB>
 __global__ __launch_bounds__(K * 8) void fft_kernel(const FftArgs a) {
   static_assert(K == 16 || K == 32 || K == 64, "k = p = 16, 32 or 64");
@@ -291,11 +294,11 @@ __global__ __launch_bounds__(K * 8) void fft_kernel(const FftArgs a) {
 }
 
 // ------------------------------------------------------------------- host
-// The rows the kernels replace: the K+K codec's parity rows (encode, verify)
-// and their inverse (every data shard rebuilt from the parity shards, in
-// parity order: reconstruct with shards 0 .. K-1 missing, core.rs:801-923).
+// The rows the kernels replace: the K+K codec's parity rows (encode, verify;
+// their own inverse, so also every data shard rebuilt from the parity shards
+// in parity order: reconstruct with shards 0 .. K-1 missing, core.rs:801-923).
 struct FftRows {
-  std::vector<uint16_t> enc[3], dec[3];  // K = 16, 32, 64
+  std::vector<uint16_t> par[3];  // K = 16, 32, 64
 };
 const FftRows& fft_rows() {
   static const FftRows r = [] {
@@ -308,34 +311,25 @@ const FftRows& fft_rows() {
         for (size_t j = 0; j < K; ++j) top.at(i, j) = v.at(i, j);
       top.invert(inv);
       const Matrix<Gf8Field> m = v.multiply(inv);  // core.rs:430-436
-      Matrix<Gf8Field> par(K, K), pinv;
-      for (size_t i = 0; i < K; ++i)
-        for (size_t j = 0; j < K; ++j) par.at(i, j) = m.at(K + i, j);
-      par.invert(pinv);
-      f.enc[q] = par.d;
-      f.dec[q] = pinv.d;
+      f.par[q].assign(m.d.begin() + K * K, m.d.begin() + 2 * K * K);
     }
     return f;
   }();
   return r;
 }
 
-template <int K, uint32_t B0, uint32_t B1>
+template <int K>
 const void* fft_fn(uint32_t sub) {
-  return sub ? reinterpret_cast<const void*>(&fft_kernel<K, B0, B1, 1024u>)
-             : reinterpret_cast<const void*>(&fft_kernel<K, B0, B1, 0u>);
+  return sub ? reinterpret_cast<const void*>(&fft_kernel<K, 0u, K, 1024u>)
+             : reinterpret_cast<const void*>(&fft_kernel<K, 0u, K, 0u>);
 }
 
 }  // namespace
 
-int fft_direction(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
-  if (field != 8 || k != p || (k != 16 && k != 32 && k != 64) || !get_option(51)) return 0;
-  const FftRows& f = fft_rows();
+bool fft_applies(int field, uint32_t k, uint32_t p, const uint16_t* rows) {
+  if (field != 8 || k != p || (k != 16 && k != 32 && k != 64) || !get_option(51)) return false;
   const int q = k == 16 ? 0 : k == 32 ? 1 : 2;
-  const size_t bytes = (size_t)k * k * sizeof(uint16_t);
-  if (std::memcmp(rows, f.enc[q].data(), bytes) == 0) return 1;
-  if (std::memcmp(rows, f.dec[q].data(), bytes) == 0) return -1;
-  return 0;
+  return std::memcmp(rows, fft_rows().par[q].data(), (size_t)k * k * sizeof(uint16_t)) == 0;
 }
 
 hipError_t launch_fft(int field, uint32_t k, uint32_t p, const uint16_t* rows,
@@ -343,9 +337,7 @@ hipError_t launch_fft(int field, uint32_t k, uint32_t p, const uint16_t* rows,
                       uint64_t len, uint64_t stripe_stride, uint32_t n_stripes, uint32_t mode,
                       uint32_t* mismatch, bool per_stripe, hipStream_t stream, uint64_t* done) {
   *done = 0;
-  const int dir = fft_direction(field, k, p, rows);
-  if (!dir || n_stripes == 0) return hipSuccess;
-  if (dir < 0 && mode != kStore) return hipSuccess;  // rebuilds are stores
+  if (!fft_applies(field, k, p, rows) || n_stripes == 0) return hipSuccess;
   // 1 KiB shards: two stripes per 2 KiB column; otherwise whole 2 KiB columns
   const uint32_t sub = len == 1024u && get_option(33) != 0 ? 1024u : 0u;
   const uint64_t cols = len / 2048u;
@@ -364,13 +356,10 @@ hipError_t launch_fft(int field, uint32_t k, uint32_t p, const uint16_t* rows,
     a.cmp[i] = cmp ? cmp[i] : nullptr;
   }
   const void* fn = nullptr;
-  switch ((int)k * (dir > 0 ? 1 : -1)) {
-    case 16: fn = fft_fn<16, 0u, 16u>(sub); break;
-    case 32: fn = fft_fn<32, 0u, 32u>(sub); break;
-    case 64: fn = fft_fn<64, 0u, 64u>(sub); break;
-    case -16: fn = fft_fn<16, 16u, 0u>(sub); break;
-    case -32: fn = fft_fn<32, 32u, 0u>(sub); break;
-    case -64: fn = fft_fn<64, 64u, 0u>(sub); break;
+  switch (k) {
+    case 16: fn = fft_fn<16>(sub); break;
+    case 32: fn = fft_fn<32>(sub); break;
+    case 64: fn = fft_fn<64>(sub); break;
     default: return hipSuccess;
   }
   const uint64_t total = sub ? ((uint64_t)n_stripes + 1) / 2 : cols * n_stripes;
@@ -387,8 +376,7 @@ hipError_t launch_fft(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   void* args[] = {&a};
   e = hipLaunchKernel(fn, dim3((uint32_t)gx), dim3(k * 8), args, 0, stream);
   if (e != hipSuccess) return e;
-  note_kernel("fft gf8 %u+%u %s%s", k, p, dir > 0 ? (mode == kStore ? "encode" : "check") : "rebuild",
-              sub ? " sub1" : "");
+  note_kernel("fft gf8 %u+%u %s%s", k, p, mode == kStore ? "code" : "check", sub ? " sub1" : "");
   count_bitslice_launch();
   *done = sub ? len : cols * 2048u;
   return hipSuccess;

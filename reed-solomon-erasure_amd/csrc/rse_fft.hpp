@@ -1,7 +1,7 @@
 // rse_fft.hpp -- the additive-FFT kernels of GF(2^8) codecs with k = p = 16,
 // 32 or 64 (rse_fft.hip): encode / verify (the codec's parity rows) and every
-// data shard rebuilt from the parity shards (their inverse), bit-exact with
-// the coefficient networks.
+// data shard rebuilt from the parity shards (the same rows: the parity block
+// is its own inverse), bit-exact with the coefficient networks.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -26,12 +26,11 @@ struct FftArgs {
   const uint8_t* cmp[kFftMax];
 };
 
-// 1: rows[p x k] are the parity rows of the GF(2^8) k+k codec (k = p = 16, 32,
-// 64); -1: their inverse (rebuild the data from the parity); 0: neither, or
-// RSE_OPT_FFT is 0.
-int fft_direction(int field, uint32_t k, uint32_t p, const uint16_t* rows);
+// rows[p x k] are the parity rows of the GF(2^8) k+k codec (k = p = 16, 32,
+// 64) -- which are also their own inverse -- and RSE_OPT_FFT is on.
+bool fft_applies(int field, uint32_t k, uint32_t p, const uint16_t* rows);
 // Codes the whole 2 KiB columns of every shard (1 KiB shards: all of them) of
-// n_stripes stripes when fft_direction applies; *done = bytes per shard
+// n_stripes stripes when fft_applies; *done = bytes per shard
 // coded, 0 if nothing was launched.
 hipError_t launch_fft(int field, uint32_t k, uint32_t p, const uint16_t* rows,
                       const uint8_t* const* in, uint8_t* const* out, const uint8_t* const* cmp,

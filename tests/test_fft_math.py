@@ -103,3 +103,14 @@ def test_fft_twiddles_of_the_transform_on_the_subspace():
             for j in range(0, k, 2 << i):
                 assert (skew(i, j) == 0) == (j == 0)
                 assert skew(i, k ^ j) != 0
+
+
+@pytest.mark.parametrize("k", [2, 4, 8, 16, 32, 64, 128])
+def test_parity_block_is_its_own_inverse(k):
+    """The k x k parity block of the k+k codec (core.rs:430-436) equals its
+    inverse -- the decode rows of every data shard from the parity shards
+    (core.rs:697-731) -- so rse_fft.hip's one kernel serves encode and the
+    rebuild: Q(x) = P(x ^ k) swaps the cosets {0..k-1} and {k..2k-1}."""
+    m = np.asarray(O.Codec(8, k, k).matrix(), np.uint8)
+    par = m[k:]
+    assert (np.asarray(O.matrix_invert(8, par), np.uint8) == par).all()

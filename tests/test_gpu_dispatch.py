@@ -109,19 +109,40 @@ def test_now_launch_path_when_dispatch_is_off(R):
         lib.rse_set_option(DISPATCH, old)
 
 
-def test_now_fresh_inputs_and_outputs_across_kernels(R):
-    """The same device buffers, rewritten by torch kernels (on any XCD)
-    between calls: every call must read the new inputs and leave its outputs
-    where the next torch kernel reads them -- 200 calls, every word checked."""
+@pytest.mark.parametrize("n,wgs,calls", [(8192, 0, 200), (65536, 8, 100)])
+def test_now_fresh_inputs_and_outputs_across_kernels(R, n, wgs, calls):
+    """The same device buffers, rewritten by torch kernels (whose workgroups
+    land on every XCD) between calls: every call must read the new inputs and
+    leave its outputs where the next torch kernel reads them -- every word
+    checked.  The 64 KiB case spreads each request over all 8 resident
+    dispatcher workgroups (RSE_OPT_DISPATCH_WORKGROUPS 8, shards up to the
+    size limit), so the hand-off is exercised on several XCDs' L2s at sizes
+    where an L1-cold test alone could not see a stale line
+    (MI355X_MICROARCH.md, the agent-scope acquire each request takes)."""
     lib = R._lib.load()
-    k, p, n = 10, 4, 8192
+    WGS = 45
+    old = [lib.rse_get_option(x) for x in (WGS, MAX_BYTES)]
+    if wgs:
+        lib.rse_set_option(WGS, wgs)
+        lib.rse_set_option(MAX_BYTES, max(n, old[1]))
+        lib.rse_dispatcher_stop()  # relaunched with `wgs` workgroups
+    try:
+        _fresh_inputs(R, lib, n, calls)
+    finally:
+        lib.rse_set_option(WGS, old[0])
+        lib.rse_set_option(MAX_BYTES, old[1])
+        lib.rse_dispatcher_stop()
+
+
+def _fresh_inputs(R, lib, n, calls):
+    k, p = 10, 4
     r = R.galois_8.ReedSolomon(k, p)
     oc = O.Codec(8, k, p)
     t = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(k + p)]
     d0 = lib.rse_get_option(DISPATCHED)
     g = torch.Generator(device="cuda")
     g.manual_seed(11)
-    for it in range(200):
+    for it in range(calls):
         for x in t[:k]:  # new inputs, written by a kernel
             x.copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g))
         if it % 2:
@@ -136,7 +157,7 @@ def test_now_fresh_inputs_and_outputs_across_kernels(R):
             assert (host[k + i] == want[k + i]).all(), (it, i)
         # a torch kernel reads the parity the dispatcher wrote
         assert int(torch.bitwise_xor(t[k], torch.from_numpy(want[k]).cuda()).sum()) == 0, it
-    assert lib.rse_get_option(DISPATCHED) - d0 == 200
+    assert lib.rse_get_option(DISPATCHED) - d0 == calls
 
 
 def test_dispatcher_idles_out_and_comes_back(R):

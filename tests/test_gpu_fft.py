@@ -53,7 +53,7 @@ def test_fft_encode_verify_rebuild(R, k, nb):
         d = dev(buf)
         r.encode_flat(d, nb, stripes)
         kern = last_kernel()
-        assert kern.startswith(f"fft gf8 {k}+{k} encode"), kern
+        assert kern.startswith(f"fft gf8 {k}+{k} code"), kern
         got = host(d).reshape(stripes + 1, T, nb)
         ref = buf.reshape(stripes + 1, T, nb)
         assert (got[stripes] == ref[stripes]).all()  # guard stripe untouched
@@ -92,7 +92,7 @@ def test_fft_encode_verify_rebuild(R, k, nb):
         dd = d.view(stripes + 1, T, nb)
         dd[:stripes, :k].fill_(0xA5)
         r.reconstruct_data_flat(d, nb, stripes, [i >= k for i in range(T)])
-        assert last_kernel().startswith(f"fft gf8 {k}+{k} rebuild"), last_kernel()
+        assert last_kernel().startswith(f"fft gf8 {k}+{k} code"), last_kernel()
         assert (host(d) == good).all()
 
 
