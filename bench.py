@@ -380,6 +380,8 @@ def leg_summary(full):
         "verify_10_4_c_abi_us_per_call": _get(full, "verify", "c_abi", "us_per_call"),
         "verify_flat_10_4_GBps": _get(full, "verify_flat", "algorithmic_GB_per_s"),
         "e2e_pinned_host_flat_MBps": _get(full, "end_to_end_pinned_host_flat", "MB_per_s"),
+        "e2e_pinned_host_flat_vs_raw_duplex": _get(full, "end_to_end_pinned_host_flat",
+                                                   "vs_raw_duplex"),
         "e2e_pinned_host_reconstruct_MBps": _get(full, "end_to_end_pinned_host_reconstruct",
                                                  "MB_per_s"),
         "e2e_host_all_ranks_MBps": _get(full, "end_to_end_host_all_ranks", "MB_per_s_all_ranks"),
@@ -642,6 +644,7 @@ def main(argv=None):
             extras["reference_bench_matrix"] = reference_bench_matrix(stream)
         else:
             extras.update(extra_legs(r, v, k, p, L, min(pool, 256), stream))
+        host_agreement(extras)
 
     if rank == 0:
         per_launch_bytes = n_local * stripe_bytes / launches
@@ -682,6 +685,26 @@ def main(argv=None):
             ROOT, "gpurun_out", f"bench_full_n{world}.json"))
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_agreement(extras):
+    """The two pinned-host rse_encode_host_flat legs (host_leg, made first,
+    and extra_legs', made after every other leg) time the same call on the
+    same 8 stripes: flag whether they agree within 10 %, and whether the
+    pipeline reaches 0.9 of plain duplex copies of the same bytes (VERDICT
+    r05 §4: they read 76.1 and 41.6 GB/s in one process while the pipeline's
+    H2D and D2H streams could share a hardware queue)."""
+    a = _get(extras, "end_to_end_host_all_ranks", "MB_per_s_all_ranks")
+    flat = extras.get("end_to_end_pinned_host_flat")
+    if a is None or not flat or _get(extras, "end_to_end_host_all_ranks", "ranks") != 1:
+        return
+    b = flat["MB_per_s"]
+    flat["vs_host_leg"] = round(b / a, 3)
+    flat["host_flat_legs_agree_within_10pct"] = abs(b - a) <= 0.1 * max(a, b)
+    raw = flat.get("raw_pinned_duplex_MB_per_s")
+    if raw:
+        flat["vs_raw_duplex"] = round(b / raw, 3)
+        flat["at_least_0_9_of_raw_duplex"] = b >= 0.9 * raw
 
 
 def _sync():

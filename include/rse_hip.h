@@ -408,7 +408,13 @@ void rse_dispatcher_stop(void);
 #define RSE_OPT_DISPATCH 39           /* 1 (default): small *_now calls run on the resident dispatcher;
                                         0: always the launch path (A/B) */
 #define RSE_OPT_DISPATCH_IDLE_US 40   /* the resident dispatcher ends after this many microseconds
-                                        without a call (default 2000) */
+                                        without a call (default 200).  It runs on a low-priority
+                                        stream, so other streams' kernels never queue behind it,
+                                        but a device-wide synchronisation (hipDeviceSynchronize,
+                                        torch.cuda.synchronize()) right after a *_now call waits
+                                        until it has idled out: ~230 us per call+sync at 200,
+                                        ~2 ms at 2000 (tools/dispatch_sync_probe.py);
+                                        rse_dispatcher_stop() ends it at once */
 #define RSE_OPT_DISPATCH_MAX_BYTES 41 /* shard bytes up to which a *_now call is dispatched
                                         (default 65536) */
 #define RSE_OPT_DISPATCH_WORKGROUPS 45 /* workgroups of the resident dispatcher (1..64, default 8):
@@ -432,11 +438,11 @@ void rse_dispatcher_stop(void);
                                         rebuild all data shards from the parity shards on additive-FFT
                                         kernels ((k/2) log2 k butterflies per transform instead of
                                         k x p coefficient networks; same bytes); 0: the wide modules */
-#define RSE_OPT_HOST_QUEUES 52        /* host pipeline (*_host, *_host_flat) streams: 1 (default) each
-                                         on a hardware queue of its own, so the H2D and D2H copies
-                                         never queue behind each other whatever other streams the
-                                         process holds; 2 the D2H stream at high priority; 0 plain
-                                         streams (A/B) */
+#define RSE_OPT_HOST_QUEUES 52        /* host pipeline (*_host_flat) streams: 1 (default) the D2H
+                                         stream at high priority, on hardware queues no default-
+                                         priority stream shares, so the D2H copies never hold up
+                                         the H2D copies whatever other streams the process holds;
+                                         0 plain streams (A/B) */
 #define RSE_OPT_DISPATCHED 42         /* read-only: *_now calls the dispatcher served */
 #define RSE_OPT_DISPATCH_LAUNCHES 43  /* read-only: launches of the resident dispatcher */
 #define RSE_OPT_WIDE_GRID 44          /* wide-module launches: -1 fixed workgroup counts (8192

@@ -593,29 +593,14 @@ hipError_t lease_ring(Scratch* r, size_t dbytes) {
 // once the process holds a few streams (torch's, the caller's, other leases')
 // the pipeline's H2D and D2H streams can share one queue.  Commands of one
 // queue start in order, so the D2H copy that waits for a chunk's kernel then
-// holds up the next chunks' H2D copies behind it: the duplex halves (the
+// holds up the next chunks' H2D copies behind it and the duplex is lost (the
 // bench's pinned-host leg read 41.6 against 76.1 GB/s for the same call,
-// VERDICT r05).  RSE_OPT_HOST_QUEUES 1 (default) gives every pipeline stream
-// a hardware queue of its own: a stream with a CU mask (all CUs) is never
-// mapped onto a shared queue.  2: the D2H stream at high priority instead (a
-// queue pool of its own), the other streams plain.  0: plain streams.
+// VERDICT r05; tools/queue_probe.py: 63 against 73-76 GB/s by where the
+// streams land).  RSE_OPT_HOST_QUEUES 1 (default): the D2H stream at high
+// priority, a queue pool of its own (rse::side_priority_stream); 0: plain
+// streams.
 hipError_t pipe_stream(int qmode, bool d2h, hipStream_t* q) {
-  if (qmode == 1) {
-    int dev = 0, n_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    std::vector<uint32_t> mask(((size_t)std::max(n_cu, 1) + 31) / 32, 0u);
-    for (int i = 0; i < n_cu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-    e = hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data());
-    if (e == hipSuccess) return e;
-    (void)hipGetLastError();  // no dedicated queue: a plain stream
-  }
-  if (qmode == 2 && d2h) {
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-      return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
-  }
+  if (qmode && d2h) return rse::side_priority_stream(true, q);
   return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
 }
 

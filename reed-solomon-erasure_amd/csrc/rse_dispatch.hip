@@ -295,9 +295,24 @@ Dispatcher& dispatcher(int dev) {
 }
 std::atomic<int64_t> g_dispatched{0}, g_dispatch_launches{0};
 
+}  // namespace
+
+hipError_t side_priority_stream(bool high, hipStream_t* q) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest)
+    return hipStreamCreateWithPriority(q, hipStreamNonBlocking, high ? greatest : least);
+  (void)hipGetLastError();
+  return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
+}
+
+namespace {
+
 hipError_t disp_init(Dispatcher& d) {
   if (d.init) return hipSuccess;
-  hipError_t e = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking);
+  // low priority: not on the hardware queues of the default-priority streams,
+  // whose commands the resident kernel would otherwise hold up until it idles
+  // out
+  hipError_t e = side_priority_stream(false, &d.st);
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&d.req), sizeof(Granule) * kMaxGranules + 64,
                       hipHostMallocMapped | hipHostMallocCoherent);

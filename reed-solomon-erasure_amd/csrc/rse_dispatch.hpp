@@ -20,6 +20,16 @@ hipError_t dispatch_run(const uint16_t* rows, uint32_t n_in, uint32_t n_out,
                         const uint8_t* const* in, uint8_t* const* out, uint64_t len_bytes,
                         bool check, bool* mismatch);
 void dispatch_stop_all();
+// A non-blocking stream at the highest (high) or lowest stream priority of the
+// current device, or a plain one where the device has a single priority.  HIP
+// maps streams onto at most GPU_MAX_HW_QUEUES hardware queues per priority,
+// least-used first, and a queue starts its commands in order; torch's and
+// most callers' streams are at the default priority, so a stream at another
+// one does not share their queues.  The resident dispatcher runs on a
+// low-priority stream (its kernel would hold up, until it idles out, every
+// command queued behind it on a shared queue), the host pipeline's D2H copies
+// on a high-priority one (rse_codec.cpp pipe_stream).
+hipError_t side_priority_stream(bool high, hipStream_t* q);
 int64_t dispatch_count();         // RSE_OPT_DISPATCHED
 int64_t dispatch_launch_count();  // RSE_OPT_DISPATCH_LAUNCHES
 

@@ -799,7 +799,7 @@ struct Options {
   int64_t recon_w4_min = 64;      // 4 KiB syndrome chunks from this many coefficients
   int64_t wide_half = 1;          // GF(2^8) paired wide modules on 2 KiB chunks (one plane group)
   int64_t dispatch = 1;           // *_now calls on the resident dispatcher (rse_dispatch.hip)
-  int64_t dispatch_idle_us = 2000;  // the resident kernel ends after this long without a call
+  int64_t dispatch_idle_us = 200;  // the resident kernel ends after this long without a call
   int64_t dispatch_max_bytes = 65536;  // shard bytes up to which a *_now call is dispatched
   int64_t wide_grid = 0;          // wide launches: -1 fixed workgroup counts, m > 0 m x resident, 0 auto
   int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
@@ -809,7 +809,7 @@ struct Options {
   int64_t sub_depth = 4;  // narrow modules' 1 / 2 KiB-shard kernels: inputs in flight per wave
   int64_t tune_nosync = 0;  // RSE_TUNE_SPLITS builds: wide modules without barriers (timing)
   int64_t fft = 1;  // GF(2^8) k = p = 16 / 32 / 64 codecs on the additive-FFT kernels (rse_fft.hip)
-  int64_t host_queues = 1;  // host pipeline streams: 1 own hardware queues, 0 shared (A/B)
+  int64_t host_queues = 1;  // host pipeline: 1 the D2H stream at high priority, 0 plain (A/B)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1360,7 +1360,7 @@ int set_option(int key, int64_t value) {
     case 48: g_opt.wide_pin_pairs = value < 1 ? 1 : value > 8 ? 8 : value; return 0;
     case 50: g_opt.sub_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 51: g_opt.fft = value ? 1 : 0; return 0;
-    case 52: g_opt.host_queues = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
+    case 52: g_opt.host_queues = value ? 1 : 0; return 0;
 #ifdef RSE_TUNE_SPLITS
     case 47: g_opt.tune_nosync = value ? 1 : 0; return 0;  // rse_jit.cpp make_source
 #endif

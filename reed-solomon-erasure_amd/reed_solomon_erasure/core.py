@@ -300,7 +300,13 @@ class ReedSolomon:
     # the *_now entry codes the stripe -- small stripes on the resident
     # dispatcher, no kernel launch -- and returns with the result in place.
     def encode_now(self, shards: ShardList) -> None:
-        """encode() (core.rs:597-611), returning when the parity is written."""
+        """encode() (core.rs:597-611), returning when the parity is written.
+
+        The *_now calls on small shards run on a resident kernel that stays
+        up RSE_OPT_DISPATCH_IDLE_US (200 us) after the last call: streams are
+        not held up by it, but a device-wide synchronisation right after a
+        call (torch.cuda.synchronize()) waits until it idles out; call
+        ``reed_solomon_erasure.core.dispatcher_stop()`` first to end it at once."""
         ptrs, lens = _arrays(shards, self.field)
         _settle(_first(shards))
         _raise(_lib.rse_encode_now(self._h, ptrs, lens, len(shards)))
@@ -690,6 +696,14 @@ def code_shards_host(field: int, rows, inputs: Sequence, outputs: Sequence,
     n = _same_len([_host_elems(t, field) for t in list(inputs) + list(outputs)])
     _raise(_lib.rse_code_shards_host(field, rb, n_out, n_in, ip, op, n, 1 if accumulate else 0,
                                      _stream()))
+
+
+def dispatcher_stop() -> None:
+    """End the resident dispatcher of the *_now calls now (it ends by itself
+    RSE_OPT_DISPATCH_IDLE_US after the last call): a device-wide
+    synchronisation after it does not wait for the idle time.  The next
+    *_now call starts it again.  No reference counterpart."""
+    _lib.rse_dispatcher_stop()
 
 
 def last_kernel() -> str:

@@ -3,8 +3,9 @@
 against the hardware queues its streams land on: with 0..6
 other streams in the process (each used once, so it holds a queue), the same
 call under RSE_OPT_HOST_QUEUES 0 (plain streams: HIP maps them least-used onto
-GPU_MAX_HW_QUEUES queues), 1 (each pipeline stream on a queue of its own) and
-2 (the D2H stream at high priority).  Every mode change re-creates the
+GPU_MAX_HW_QUEUES queues per priority) and 1 (the D2H stream at high
+priority; session r06/s4 also had a CU-masked stream per pipeline stream,
+a queue each, which measured the same).  Every mode change re-creates the
 pipeline's streams.  GPU box only."""
 import os
 import sys
@@ -44,7 +45,7 @@ def main():
     h = v.reshape(-1).cpu().pin_memory()
     h.view(ns, k + p, L)[:, k:].zero_()
     others = []
-    print("other streams | GB/s data+parity by RSE_OPT_HOST_QUEUES (0 / 1 / 2), twice", flush=True)
+    print("other streams | GB/s data+parity by RSE_OPT_HOST_QUEUES (0 / 1), twice", flush=True)
     for n_other in (0, 1, 2, 3, 4, 6):
         while len(others) < n_other:
             s_ = torch.cuda.Stream()
@@ -53,7 +54,7 @@ def main():
             others.append(s_)
         torch.cuda.synchronize()
         row = []
-        for mode in (0, 1, 2, 0, 1, 2):
+        for mode in (0, 1, 0, 1):
             assert lib.rse_set_option(QUEUES, mode) == 0
             row.append(f"{rate(r, h):6.1f}")
         print(f"{n_other:13d} | " + " ".join(row), flush=True)
