@@ -1680,6 +1680,52 @@ def test_wide_block_chain_gf16_past_256(R):
         lib.rse_set_option(9, old)
 
 
+@pytest.mark.parametrize("nbytes,stripes", [(1024, 5), (1024, 8), (2048, 3)])
+def test_wide_block_chain_gf16_short_shards(R, nbytes, stripes):
+    """The 1000+24 chain on 1 and 2 KiB shards: a wave's chunk
+    then takes 4 (2) consecutive stripes, and the blocks after the first read
+    and rewrite the running sums of every stripe of the chunk in place -- over
+    stripe counts that are (not) a multiple of the stripes per chunk, every
+    stripe against the oracle, and a guard stripe after the batch untouched."""
+    lib = R._lib.load()
+    k, p = 1000, 24
+    n_elems = nbytes // 2
+    T = k + p
+    rng = np.random.default_rng(nbytes + stripes)
+    oc = O.Codec.shared(16, k, p)
+    old = lib.rse_get_option(9)
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        r = R.core.ReedSolomon(k, p, 16)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        buf = rng.integers(0, 256, (stripes + 1) * T * nbytes, dtype=np.uint8)
+        d = dev(buf)
+        n0 = lib.rse_get_option(6)
+        r.encode_flat(d, n_elems, stripes)
+        torch.cuda.synchronize()
+        from reed_solomon_erasure.core import last_kernel
+        assert lib.rse_get_option(6) - n0 == 8, last_kernel()
+        assert last_kernel().startswith("bitslice-wide-blocks gf16 1000+24 x8"), last_kernel()
+        got = host(d).reshape(stripes + 1, T, nbytes)
+        ref = buf.reshape(stripes + 1, T, nbytes)
+        assert (got[stripes] == ref[stripes]).all()  # guard stripe
+        assert (got[:stripes, :k] == ref[:stripes, :k]).all()
+        for s_ in range(stripes):
+            sh = [ref[s_, i].copy() for i in range(k)] + [np.zeros(nbytes, np.uint8)
+                                                          for _ in range(p)]
+            oc.encode(sh)
+            for i in range(p):
+                assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
+        ok = r.verify_flat(d, n_elems, stripes)
+        assert ok.all()
+        v = got.copy()
+        v[stripes - 1, k + 3, nbytes // 2] ^= 0x10
+        want = np.arange(stripes) != stripes - 1
+        assert (r.verify_flat(dev(v.reshape(-1)), n_elems, stripes) == want).all()
+    finally:
+        lib.rse_set_option(9, old)
+
+
 @pytest.mark.parametrize("field,k,p,erased", [(8, 40, 2, [3, 39]), (8, 6, 10, [0, 1, 2, 5, 6, 8, 9, 12, 15]),
                                               (16, 36, 3, [0, 35, 37])])
 def test_wide_reconstruct_pattern_blocks(R, field, k, p, erased):
