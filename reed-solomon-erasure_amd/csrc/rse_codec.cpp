@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <list>
 #include <map>
@@ -26,6 +27,7 @@
 #include <vector>
 
 #include "../../include/rse_hip.h"
+#include "../../include/rse_hip_tune.h"
 #include "rse_dispatch.hpp"
 #include "rse_fft.hpp"
 #include "rse_wideblk.hpp"
@@ -2574,7 +2576,26 @@ int rse_reconstruct_host_batch(const rse_codec* c, void* stripes, size_t shard_l
                        (hipStream_t)stream, nullptr);
 }
 
+// The keys include/rse_hip.h gives callers; every other settable key is a
+// tuning / A-B switch (include/rse_hip_tune.h), refused unless the process
+// environment has RSE_TUNE=1.
+bool caller_option(int key) {
+  switch (key) {
+    case RSE_OPT_HOST_CHUNK_KIB: case RSE_OPT_HOST_H2D_STREAMS: case RSE_OPT_JIT:
+    case RSE_OPT_JIT_PATTERNS: case RSE_OPT_JIT_DISK_CACHE: case RSE_OPT_JIT_MAX_PATTERNS:
+    case RSE_OPT_JIT_MAX_PATTERN_BLOCKS: case RSE_OPT_DISPATCH: case RSE_OPT_DISPATCH_IDLE_US:
+    case RSE_OPT_DISPATCH_MAX_BYTES: case RSE_OPT_DISPATCH_WORKGROUPS:
+      return true;
+    default:
+      return false;
+  }
+}
+
 int rse_set_option(int key, int64_t value) {
+  if (!caller_option(key)) {
+    const char* t = std::getenv("RSE_TUNE");
+    if (!t || std::strcmp(t, "1") != 0) return RSE_ERR_INVALID_ARGUMENT;
+  }
   return rse::set_option(key, value) == 0 ? RSE_OK : RSE_ERR_INVALID_ARGUMENT;
 }
 

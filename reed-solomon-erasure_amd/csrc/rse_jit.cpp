@@ -58,11 +58,6 @@ namespace {
 const char kJitSource[] =
 #include "rse_jit_src.inc"
     ;
-// rse_wide_ext.hpp (build/rse_jit_ext.inc): wide-body variants appended only
-// to the modules whose options ask for them, so the others keep their keys.
-const char kJitExtSource[] =
-#include "rse_jit_ext.inc"
-    ;
 // rse_sub_ext.hpp (build/rse_jit_sub.inc): the 1 / 2 KiB-shard body with
 // several inputs in flight, for modules built under RSE_OPT_SUB_DEPTH > 1.
 const char kJitSubSource[] =
@@ -240,10 +235,6 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
   if (kind == kJitWide && get_option(47) == 1) s += "#define __syncthreads() ((void)0)\n";
 #endif
   s += kJitSource;
-  // RSE_OPT_WIDE_PIN_PAIRS > 1: half-chunk wide bodies with that many input
-  // pairs per scheduling region (rse_wide_ext.hpp)
-  const int pin_pairs = kind == kJitWide && field == 8 ? (int)get_option(48) : 1;
-  if (pin_pairs > 1) s += kJitExtSource;
   // RSE_OPT_SUB_DEPTH > 1: the narrow modules' 1 / 2 KiB-shard kernels with
   // that many inputs in flight per wave (rse_sub_ext.hpp)
   const int sub_depth = kind != kJitWide && stage == kEnc ? (int)get_option(50) : 1;
@@ -297,12 +288,7 @@ std::string make_source(int field, uint32_t k, uint32_t p, const std::vector<uin
       for (int w = 0; w < W; ++w) {
         uint32_t o0, n;
         wide_share(p, W, w, &o0, &n);
-        if (half && pin_pairs > 1)
-          std::snprintf(buf, sizeof buf,
-                        "    case %d: rse::wide_body_half_pp<rse::JitWide%d, %u, %d, %d, %d, "
-                        "WideArgs, %du, %d>(a, lds); break;\n",
-                        w, w, o0, W, w, (int)get_option(26), 1024 * q, pin_pairs);
-        else if (half)
+        if (half)
           std::snprintf(buf, sizeof buf,
                         "    case %d: rse::wide_body_half<rse::JitWide%d, %u, %d, %d, %d, "
                         "WideArgs, %du>(a, lds); break;\n",

@@ -805,7 +805,6 @@ struct Options {
   int64_t dispatch_wgs = 8;       // workgroups of the resident dispatcher
   int64_t wide_block_inputs = 128;  // data inputs per wide module of a chain (0: 8 x 32 blocks)
   int64_t dispatch_lane_units = 1;  // dispatcher: (vector, output) units per lane per workgroup
-  int64_t wide_pin_pairs = 1;  // half-chunk wide modules: input pairs per scheduling region
   int64_t sub_depth = 4;  // narrow modules' 1 / 2 KiB-shard kernels: inputs in flight per wave
   int64_t tune_nosync = 0;  // RSE_TUNE_SPLITS builds: wide modules without barriers (timing)
   int64_t fft = 1;  // GF(2^8) k = p = 16 / 32 / 64 codecs on the additive-FFT kernels (rse_fft.hip)
@@ -1357,7 +1356,6 @@ int set_option(int key, int64_t value) {
     case 45: g_opt.dispatch_wgs = value < 1 ? 1 : value > 64 ? 64 : value; return 0;
     case 46: g_opt.wide_block_inputs = value < 0 ? 0 : value; return 0;
     case 49: g_opt.dispatch_lane_units = value < 1 ? 1 : value > 64 ? 64 : value; return 0;
-    case 48: g_opt.wide_pin_pairs = value < 1 ? 1 : value > 8 ? 8 : value; return 0;
     case 50: g_opt.sub_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 51: g_opt.fft = value ? 1 : 0; return 0;
     case 52: g_opt.host_queues = value ? 1 : 0; return 0;
@@ -1421,7 +1419,6 @@ int64_t get_option(int key) {
     case 45: return g_opt.dispatch_wgs;
     case 46: return g_opt.wide_block_inputs;
     case 49: return g_opt.dispatch_lane_units;
-    case 48: return g_opt.wide_pin_pairs;
     case 50: return g_opt.sub_depth;
     case 51: return g_opt.fft;
     case 52: return g_opt.host_queues;

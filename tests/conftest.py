@@ -13,6 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # keyed by a hash of the whole module source, so a stale one is never hit),
 # which spares the GPU box minutes of hiprtc; build counters in the tests
 # count built + cached modules where a codec may be among them.
+# The suite A/Bs the library's tuning switches against the oracle
+# (include/rse_hip_tune.h): rse_set_option takes them only under RSE_TUNE=1.
+os.environ.setdefault("RSE_TUNE", "1")
+
 if "RSE_JIT_CACHE_DIR" not in os.environ:
     import shutil
     _cache = tempfile.mkdtemp(prefix="rse_jit_cache_")

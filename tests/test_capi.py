@@ -286,15 +286,39 @@ def test_code_shards_refuses_unequal_lengths():
         assert ei.value.error == Error.IncorrectShardSize
 
 
+def header_options(name):
+    import re
+    hdr = open(os.path.join(ROOT, "include", name)).read()
+    return {m.group(1): int(m.group(2))
+            for m in re.finditer(r"#define (RSE_OPT_[A-Z0-9_]+) (\d+)", hdr)}
+
+
+def test_tuning_switches_need_rse_tune():
+    """include/rse_hip.h holds only the options a caller of the drop-in needs;
+    the tuning / A-B switches (include/rse_hip_tune.h) are refused unless the
+    environment has RSE_TUNE=1, and the two headers share no key.  Without
+    it, a caller option is still taken and the tuning value stays put."""
+    caller, tune = header_options("rse_hip.h"), header_options("rse_hip_tune.h")
+    assert not set(caller.values()) & set(tune.values())
+    assert len(caller) <= 20 and "RSE_OPT_FFT" in tune and "RSE_OPT_JIT" in caller
+    env = {k_: v for k_, v in os.environ.items() if k_ != "RSE_TUNE"}
+    code = PRELUDE + ("print(L.rse_set_option(51, 0), L.rse_get_option(51), "
+                      "L.rse_set_option(9, 2), L.rse_get_option(9), L.rse_set_option(2, 64))")
+    out = _py(code, env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    bad = str(L.rse_set_option(99, 1))
+    assert out.stdout.split() == [bad, "1", "0", "2", bad]
+    out = _py(code, dict(env, RSE_TUNE="1"))
+    assert out.stdout.split() == ["0", "0", "0", "2", "0"]
+
+
 def test_every_header_option_is_readable():
-    """Every RSE_OPT_* key include/rse_hip.h declares answers rse_get_option
+    """Every RSE_OPT_* key include/rse_hip.h and rse_hip_tune.h declare answers rse_get_option
     (-1 is the answer for an unknown key), and the round-3 switches start at
     their documented defaults: wave-pair reconstruct and paired wide networks
     on, the event wait off, the verify completion word on."""
-    import re
-    hdr = open(os.path.join(ROOT, "include", "rse_hip.h")).read()
-    keys = {m.group(1): int(m.group(2))
-            for m in re.finditer(r"#define (RSE_OPT_[A-Z0-9_]+) (\d+)", hdr)}
+    keys = header_options("rse_hip.h")
+    keys.update(header_options("rse_hip_tune.h"))
     assert len(keys) >= 30
     for name, key in keys.items():  # KERNEL_VARIANT's default is -1 ("the default variant")
         assert L.rse_get_option(key) != -1 or name == "RSE_OPT_KERNEL_VARIANT", name

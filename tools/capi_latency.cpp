@@ -11,8 +11,10 @@
 #include <vector>
 
 #include "rse_hip.h"
+#include "rse_hip_tune.h"
 
 int main(int argc, char** argv) {
+  setenv("RSE_TUNE", "1", 0);  // the tuning switches below (include/rse_hip_tune.h)
   const size_t k = 10, p = 4, L = 16u << 20, S = 8;
   if (argc > 1) {  // workgroups of the bit-sliced launches (RSE_OPT_GRID_X; 0 = default)
     const long g = std::atol(argv[1]);

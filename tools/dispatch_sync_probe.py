@@ -12,6 +12,7 @@ microseconds per iteration of
 GPU box only."""
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -6,6 +6,7 @@ a bench-like process, with the library's per-call resource sets counted, and
 variants at the point where it is slow (debugging aid, GPU box only)."""
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -3,6 +3,7 @@
 oracle, per erasure pattern and RSE_OPT_RECON_MIX (debugging aid)."""
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 
 import numpy as np
 import torch

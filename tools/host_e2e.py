@@ -10,6 +10,7 @@ pinned H2D copy, one big D2H copy, both at once), then the pipeline for every
 import argparse
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

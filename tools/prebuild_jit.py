@@ -16,6 +16,7 @@ here."""
 import argparse
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                 "reed-solomon-erasure_amd"))

@@ -9,6 +9,7 @@ a queue each, which measured the same).  Every mode change re-creates the
 pipeline's streams.  GPU box only."""
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

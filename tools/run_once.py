@@ -6,6 +6,7 @@
 import argparse
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-erasure_amd"))

@@ -5,6 +5,7 @@ batches, and reconstruct of one lost shard of 16+16 x 1 KiB (its pattern
 kernel), every stripe checked.  Test infrastructure (imports the oracle)."""
 import os
 import sys
+os.environ.setdefault("RSE_TUNE", "1")  # tuning switches (include/rse_hip_tune.h)
 
 import numpy as np
 import torch
