@@ -959,6 +959,21 @@ def other_configs(stream):
 # (profiles/r05/s19/).  (A one-module GF(2^16) 256+16 did not finish
 # compiling in 25 minutes of hiprtc on the build host.)
 GF16_PROPER = (1000, 24, 64 << 10, 512)
+# how long a leg waits for its run-time modules before it reports itself
+# skipped (RSE_BENCH_JIT_BUDGET_S): with the tree's jitcache/ they load in
+# milliseconds; a cold build of the largest would hold the bench for minutes
+JIT_BUDGET_S = float(os.environ.get("RSE_BENCH_JIT_BUDGET_S", "180"))
+
+
+def kernels_within(r, budget_s):
+    """r.kernel_kind(wait=True) if it returns within budget_s, else None (the
+    build goes on in the background; its helpers stop at exit)."""
+    import threading
+    out = []
+    th = threading.Thread(target=lambda: out.append(r.kernel_kind(wait=True)), daemon=True)
+    th.start()
+    th.join(budget_s)
+    return out[0] if out else None
 
 
 def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROPER[2],
@@ -983,8 +998,14 @@ def gf16_proper_leg(stream, k=GF16_PROPER[0], p=GF16_PROPER[1], nbytes=GF16_PROP
     fill_splitmix(buf, SEED, 0x16 << 40)  # one stream over everything; encode overwrites parity
     r = R.core.ReedSolomon(k, p, 16)
     t0 = time.perf_counter()
-    kind = r.kernel_kind(wait=True)
+    kind = kernels_within(r, JIT_BUDGET_S)
     build_s = time.perf_counter() - t0
+    if kind is None:  # cold JIT cache: do not hold the bench for the build
+        del buf, v
+        torch.cuda.empty_cache()
+        return {"skipped": f"the {k}+{p} chain modules were not built within {JIT_BUDGET_S:.0f} s "
+                           "(a cold JIT cache: ~20-45 min of hiprtc; tools/prebuild_all.sh "
+                           "builds them into jitcache/)"}
     elems = nbytes // 2
     enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream,
                      reps=10, warm_s=0.25)
@@ -1097,8 +1118,12 @@ def wide_config(stream, g, field, k, p):
             fill_splitmix(v[s_, i], SEED, shard_id(s_, i))
     r = R.core.ReedSolomon(k, p, field)
     t0 = time.perf_counter()
-    kind = r.kernel_kind(wait=True)
+    kind = kernels_within(r, JIT_BUDGET_S)
     build_s = time.perf_counter() - t0
+    if kind is None:
+        del buf, v
+        torch.cuda.empty_cache()
+        return {"skipped": f"modules not built within {JIT_BUDGET_S:.0f} s (cold JIT cache)"}
     elems = nbytes // (field // 8)
     enc = timed_gbps(lambda: r.encode_flat(buf, elems, stripes), stripes * T * nbytes, stream,
                      reps=20, warm_s=0.25)
@@ -1243,8 +1268,12 @@ def _matrix_rows(lib, stream, st, sh, out, one_stripe, shapes):
     for block, k, p in (shapes or REF_BENCH_SHAPES):
         T = k + p
         r = R.core.ReedSolomon(k, p, 8)
-        r.kernel_kind(wait=True)  # time the codec's bit-sliced kernels, not the
-        # table kernels while they build (1 and 2 KiB shards: RSE_OPT_SUB_CHUNKS)
+        # time the codec's bit-sliced kernels, not the table kernels while they
+        # build (1 and 2 KiB shards: RSE_OPT_SUB_CHUNKS)
+        if kernels_within(r, JIT_BUDGET_S) is None:
+            out["entries"].append({"shape": f"{k}+{p} x {block // 1024} KiB",
+                                   "skipped": "modules not built in time (cold JIT cache)"})
+            continue
         n = max(1, min(32768, (256 << 20) // (T * block)))
         buf = torch.empty(n * T * block, dtype=torch.uint8, device="cuda")
         fill_splitmix(buf, SEED, 0x7E57)

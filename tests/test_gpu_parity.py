@@ -16,6 +16,7 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
+from conftest import kernels_or_skip  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -1645,7 +1646,7 @@ def test_wide_block_chain_gf16_past_256(R):
     try:
         assert lib.rse_set_option(9, 2) == 0
         r = R.core.ReedSolomon(k, p, 16)
-        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        assert kernels_or_skip(r, "GF(2^16) 1000+24") == "bitslice-specialised"
         t = [dev(x).reshape(n_elems, 2) for x in full[:k]] + \
             [torch.full((n_elems, 2), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
         n0 = lib.rse_get_option(6)
@@ -1697,7 +1698,7 @@ def test_wide_block_chain_gf16_short_shards(R, nbytes, stripes):
     try:
         assert lib.rse_set_option(9, 2) == 0
         r = R.core.ReedSolomon(k, p, 16)
-        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        assert kernels_or_skip(r, "GF(2^16) 1000+24") == "bitslice-specialised"
         buf = rng.integers(0, 256, (stripes + 1) * T * nbytes, dtype=np.uint8)
         d = dev(buf)
         n0 = lib.rse_get_option(6)

@@ -12,15 +12,21 @@ pat=()
 seq_csv() { python3 -c "print(','.join(str(i) for i in range($1)))"; }
 # benches/bandwidth.rs:88-190 shapes (bench.py REF_BENCH_SHAPES): erase shard 0,
 # and data shards 0..p-1
+# (16+16, 32+32, 64+64 rebuild all data from the parity on the additive-FFT
+# kernels, rse_fft.hip: no pattern module)
 for kp in 4:4 8:8 16:16 32:32 64:64 5:2 10:4 50:20; do
   k=${kp%:*}; p=${kp#*:}
-  pat+=(--pattern "8:$k:$p:1024:0" --pattern "8:$k:$p:1024:$(seq_csv "$p")")
+  pat+=(--pattern "8:$k:$p:1024:0")
+  case $k in 16|32|64) ;; *) pat+=(--pattern "8:$k:$p:1024:$(seq_csv "$p")") ;; esac
 done
 pat+=(--pattern "8:4:4:2048:0" --pattern "8:4:4:2048:0,1,2,3")
 pat+=(--pattern "16:20:8:4194304:0,1,2,3")  # other_configs gf16_20_8 cached pattern
 # tests/test_gpu_parity.py test_wide_full_chunks_option: one codec on full
 # (4 KiB) chunks, RSE_OPT_WIDE_HALF 0, in a process of its own
 python3 tools/prebuild_jit.py --set 38=0 --codec 8:34:10 || exit 1
+# 16+16 .. 64+64's wide modules (RSE_OPT_FFT 0: tests/test_gpu_parity.py
+# test_wide_codec_kernels, test_sub_chunk_shards; the default is the FFT kernels)
+python3 tools/prebuild_jit.py --set 51=0 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 || exit 1
 # test_wide_sixteen_waves: 4 outputs per wave (a 16-wave module)
 python3 tools/prebuild_jit.py --set 18=4 --codec 8:60:60 || exit 1
 exec python3 tools/prebuild_jit.py --codec 8:35:10 \
