@@ -114,5 +114,9 @@
                                          priority stream shares, so the D2H copies never hold up
                                          the H2D copies whatever other streams the process holds;
                                          0 plain streams (A/B) */
+#define RSE_OPT_HOST_ZC_OUT 53        /* host pipeline (*_host_flat, reconstruct_host*): 1 (default)
+                                         the shards an encode or reconstruct writes, when they are
+                                         pinned device-mapped host memory, are stored in place by
+                                         the kernel (no D2H copies); 0 D2H copies from the ring */
 
 #endif /* RSE_HIP_TUNE_H */

@@ -5,5 +5,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 1
 export TMPDIR=/tmp
 bash tools/gpu_session.sh \
+ "zerocopy:300:python3 -u tools/zerocopy_probe.py" \
  "probe:400:python3 -u tools/e2e_bench_probe.py" \
  "probe_trace:500:rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d gpurun_out/e2e_trace -o e2e -- python3 -u tools/e2e_bench_probe.py"

@@ -809,6 +809,7 @@ struct Options {
   int64_t tune_nosync = 0;  // RSE_TUNE_SPLITS builds: wide modules without barriers (timing)
   int64_t fft = 1;  // GF(2^8) k = p = 16 / 32 / 64 codecs on the additive-FFT kernels (rse_fft.hip)
   int64_t host_queues = 1;  // host pipeline: 1 the D2H stream at high priority, 0 plain (A/B)
+  int64_t host_zc_out = 1;  // host pipeline: outputs stored in place in mapped pinned memory
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1359,6 +1360,7 @@ int set_option(int key, int64_t value) {
     case 50: g_opt.sub_depth = value < 1 ? 1 : value > 4 ? 4 : value; return 0;
     case 51: g_opt.fft = value ? 1 : 0; return 0;
     case 52: g_opt.host_queues = value ? 1 : 0; return 0;
+    case 53: g_opt.host_zc_out = value ? 1 : 0; return 0;
 #ifdef RSE_TUNE_SPLITS
     case 47: g_opt.tune_nosync = value ? 1 : 0; return 0;  // rse_jit.cpp make_source
 #endif
@@ -1422,6 +1424,7 @@ int64_t get_option(int key) {
     case 50: return g_opt.sub_depth;
     case 51: return g_opt.fft;
     case 52: return g_opt.host_queues;
+    case 53: return g_opt.host_zc_out;
 #ifdef RSE_TUNE_SPLITS
     case 47: return g_opt.tune_nosync;
 #endif

@@ -740,3 +740,60 @@ def test_device_flags_must_sit_with_the_stripes(R):
                                    ctypes.cast(other.data_ptr(), ctypes.POINTER(ctypes.c_uint8)),
                                    0, torch.cuda.current_stream().cuda_stream)
     assert rc == 100 and bool((buf == 0x33).all())
+
+
+@pytest.mark.parametrize("zc", [1, 0])
+@pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 20, 8)])
+def test_pipeline_outputs_in_place(R, small_chunks, field, k, p, zc):
+    """RSE_OPT_HOST_ZC_OUT: the shards an encode or reconstruct writes, when
+    they are pinned device-mapped host memory, are stored by the kernel in
+    place (no D2H copies); 0 keeps the D2H copies.  Both give the oracle's
+    bytes for encode_host_flat, reconstruct_host_batch (every stripe its own
+    pattern, data only and with parity), per-shard encode_host with one
+    pageable parity shard among pinned ones (that stripe falls back to the
+    copies), and a verify of the result."""
+    lib = R._lib.load()
+    old = lib.rse_get_option(53)
+    lib.rse_set_option(53, zc)
+    try:
+        es = field // 8
+        n = 3 * 65536 + 4096 + 16  # several 64 KiB chunks and a ragged one
+        stripes, T = 3, k + p
+        rng = np.random.default_rng(31 * k + zc)
+        oc = O.Codec(field, k, p)
+        full = np.zeros((stripes, T, n * es), np.uint8)
+        for s_ in range(stripes):
+            sh = rand_shards(rng, k, n * es) + [np.zeros(n * es, np.uint8) for _ in range(p)]
+            oc.encode(sh)
+            full[s_] = np.stack(sh)
+        r = R.core.ReedSolomon(k, p, field)
+        h = torch.from_numpy(full.reshape(-1).copy()).pin_memory()
+        hv = h.view(stripes, T, n * es)
+        hv[:, k:].fill_(0xC3)
+        r.encode_host_flat(h, n, stripes)
+        assert (hv.numpy() == full).all()
+        assert r.verify_host_flat(h, n, stripes).all()
+        pres = np.ones((stripes, T), bool)
+        for s_ in range(stripes):
+            pres[s_, rng.choice(T, p, replace=False)] = False
+        for data_only in (True, False):
+            w = hv.numpy()
+            w[~pres] = 0x3C
+            r.reconstruct_host_batch(h, n, stripes, pres, data_only=data_only)
+            got = hv.numpy()
+            for s_ in range(stripes):
+                for i in range(T):
+                    if pres[s_, i] or not data_only or i < k:
+                        assert (got[s_, i] == full[s_, i]).all(), (data_only, s_, i)
+                    else:
+                        assert (got[s_, i] == 0x3C).all(), (data_only, s_, i)  # not rebuilt
+            hv.copy_(torch.from_numpy(full))
+        # per-shard host stripe: pinned shards, one pageable parity shard
+        hs = [torch.from_numpy(full[0, i].copy()).pin_memory() for i in range(k)] + \
+             [torch.full((n * es,), 0x77, dtype=torch.uint8).pin_memory() for _ in range(p - 1)] + \
+             [torch.full((n * es,), 0x77, dtype=torch.uint8)]
+        r.encode_host([x.view(n, 2) if field == 16 else x for x in hs])
+        for i in range(T):
+            assert (hs[i].numpy() == full[0, i]).all(), i
+    finally:
+        lib.rse_set_option(53, old)

@@ -34,12 +34,14 @@ def probed_extra_legs(r, v, k_, p_, L_, n_stripes, stream, stripe0=0):
     import torch
     out = orig_extra(r, v, k_, p_, L_, n_stripes, stream, stripe0)
     lib = bench.R_lib()
-    print("bench flat leg:", out["end_to_end_pinned_host_flat"]["MB_per_s"], "MB/s", flush=True)
+    f = out["end_to_end_pinned_host_flat"]
+    print("bench flat leg:", f["MB_per_s"], "MB/s, first call", f["first_call_MB_per_s"],
+          "outputs in place", f["outputs_in_place"], flush=True)
     h = v[:ns].reshape(-1).cpu().pin_memory()
     print(f"{'same call, new pinned buffer':44s}", rate(r, h), flush=True)
     print(f"{'again':44s}", rate(r, h), flush=True)
-    for key, vals, dflt in ((52, (0, 1), 1), (21, (0,), 1), (8, (1, 3, 4), 2),
-                            (7, (1024, 8192), 4096)):
+    for key, vals, dflt in ((53, (0, 1, 0, 1), 1), (52, (0, 1), 1), (21, (0,), 1),
+                            (8, (1, 3, 4), 2), (7, (1024, 8192), 4096), (53, (0, 1), 1)):
         for val in vals:
             lib.rse_set_option(key, val)
             print(f"{f'  option {key} = {val}':44s}", rate(r, h), flush=True)
