@@ -1510,7 +1510,7 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
   const bool zc = rse::get_option(RSE_OPT_HOST_ZC_OUT) &&
                   (op == HostOp::kEncode || op == HostOp::kRecon || op == HostOp::kReconData ||
                    (low && !code->accumulate && !any_mem));
-  std::vector<uint8_t*> zmap(T, nullptr);  // the stripe's written shards' device mappings
+  std::vector<uint8_t*> zmap(nbuf, nullptr);  // the stripe's written shards' device mappings
   bool zc_stripe = false;
   for (size_t ci = 0; e == hipSuccess && rc == RSE_OK && ci < nchunks; ++ci) {
     const size_t si = ci / per_stripe;
@@ -1523,9 +1523,10 @@ int host_pipeline(const rse_codec* c, HostOp op, const std::vector<HostStripe>& 
                 up, down);
       set_for = si;
       zc_stripe = zc && !down.empty();
-      for (uint32_t i : down) {
-        zmap[i] = zc_stripe ? mapped_host(host(i)) : nullptr;
-        zc_stripe = zc_stripe && zmap[i] && aligned16(zmap[i]);
+      for (size_t d = 0; zc_stripe && d < down.size(); ++d) {
+        const uint32_t i = down[d];
+        zmap[i] = i < nbuf ? mapped_host(host(i)) : nullptr;
+        zc_stripe = zmap[i] && aligned16(zmap[i]);
       }
     }
     if (down.empty() && !verify) continue;  // nothing to rebuild in this stripe
