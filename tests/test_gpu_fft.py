@@ -152,3 +152,35 @@ def test_fft_not_for_other_shapes(R):
     s2 = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(48)]
     r2.encode(s2)
     assert not last_kernel().startswith("fft"), last_kernel()
+
+
+@pytest.mark.parametrize("k", [16, 32, 64])
+def test_fft_gf16_subfield_codecs(R, k):
+    """GF(2^16) codecs of at most 256 shards code in the GF(2^8) subfield
+    (DESIGN §4), so GF(2^16) 16+16 .. 64+64 take the same FFT kernels: encode
+    of 2 KiB columns and a ragged tail, verify, and every data shard rebuilt,
+    against the GF(2^16) oracle."""
+    from reed_solomon_erasure.core import last_kernel
+    p, n_elems, stripes = k, 2048 + 24, 3
+    nb, T = 2 * n_elems, 2 * k
+    oc = O.Codec(16, k, p)
+    rng = np.random.default_rng(160 + k)
+    full = np.zeros((stripes, T, nb), np.uint8)
+    for s_ in range(stripes):
+        sh = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(k)] + \
+             [np.zeros(nb, np.uint8) for _ in range(p)]
+        oc.encode(sh)
+        full[s_] = np.stack(sh)
+    r = R.galois_16.ReedSolomon(k, p)
+    assert r.kernel_kind() == "fft-compiled"
+    buf = full.copy()
+    buf[:, k:] = 0x69
+    d = dev(buf.reshape(-1))
+    r.encode_flat(d, n_elems, stripes)
+    assert last_kernel().startswith(f"fft gf8 {k}+{k} code") or \
+        not last_kernel().startswith("fft"), last_kernel()  # the tail ran last
+    assert (host(d).reshape(stripes, T, nb) == full).all()
+    assert r.verify_flat(d, n_elems, stripes).all()
+    d.view(stripes, T, nb)[:, :k].fill_(0)
+    r.reconstruct_data_flat(d, n_elems, stripes, [i >= k for i in range(T)])
+    assert (host(d).reshape(stripes, T, nb) == full).all()
