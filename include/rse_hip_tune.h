@@ -118,9 +118,5 @@
                                          the shards an encode or reconstruct writes, when they are
                                          pinned device-mapped host memory, are stored in place by
                                          the kernel (no D2H copies); 0 D2H copies from the ring */
-#define RSE_OPT_RECON_W4_PAIRS 54     /* rse_reconstruct_batch of the compiled codecs over 4 KiB
-                                         chunks (shards under 16 KiB, tails past 16 KiB chunks) at 8
-                                         sigma rows: 1 / 2 (default) wave pairs with one / two own
-                                         inputs in flight per wave; 0 one wave per chunk */
 
 #endif /* RSE_HIP_TUNE_H */

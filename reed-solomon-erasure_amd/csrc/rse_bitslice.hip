@@ -216,32 +216,6 @@ __global__ __launch_bounds__(128 * P, 3) void bitslice_recon_desc_pair_kernel(
   bitslice_recon_desc_pair_body<C, true, P, PF, DBG>(descs, chunks_per_stripe, n_stripes);
 }
 
-// rse_reconstruct_batch over whole 4 KiB columns past byte `base` (shards of 4
-// to 16 KiB, and the rest of longer ones past their 16 KiB chunks) at 8 sigma
-// rows on wave pairs: a 128-lane workgroup is one pair, each unit one 4 KiB
-// column of one stripe (P = 1, so its barriers sync only the pair).  The
-// one-wave kernel (bitslice_recon_desc_w4_kernel at NS = 8) holds all 8 rows:
-// 255 VGPRs, 2 waves per SIMD, 1.87 resident, waiting on memory 0.54 of its
-// cycles (profiles/r06/s11/); a pair wave holds 4 rows at 3 waves per SIMD.
-// DBG 4: two own inputs in flight per wave (pair_advance).
-template <class C, int DBG>
-__global__ __launch_bounds__(128, 3) void bitslice_recon_desc_pair_w4_kernel(
-    const BsReconArgs* descs, uint64_t cps4, uint64_t n_stripes, uint64_t base) {
-  __shared__ PairLds<1> lds;
-  const uint64_t total = cps4 * n_stripes;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t u = blockIdx.x; u < total; u += gridDim.x) {
-    const uint64_t stripe = u / cps4, col = u - stripe * cps4;
-    const BsReconArgs& a = desc_at(descs, stripe);
-    if (a.n_out == 0) continue;  // workgroup-uniform
-    const uint64_t off = base + col * 4096u + lane * 16u;
-    u32x4 cur[4];
-    if (wave & 1u) recon_pair_unit<C, true, 1, 1, false, DBG>(a, off, lds, 0, lane, cur, false, ~0ull);
-    else recon_pair_unit<C, true, 0, 1, false, DBG>(a, off, lds, 0, lane, cur, false, ~0ull);
-  }
-}
-
 // ------------------------------------------------- batched reconstruct planner
 // One lane per stripe of rse_reconstruct_batch: the syndrome plan of
 // rse_codec.cpp bitslice_reconstruct on the device.  The valid/invalid
@@ -449,8 +423,6 @@ struct BsShape {
                       // (nullptr above p); non-temporal
   BsDescFn rec_desc[4];  // the same over per-stripe argument blocks (reconstruct_batch)
   BsDesc4Fn rec_desc4[4];      // the same over 4 KiB chunks, one per wave (Horner)
-  BsDesc4Fn rec_desc4_pair[2];  // NS = 8 over 4 KiB chunks on wave pairs: [0] one own input
-                                // in flight per wave, [1] two (RSE_OPT_RECON_W4_PAIRS 1 / 2)
   BsRec4Fn rec4[4];            // rec's Horner mode over 4 KiB chunks, one per wave
   BsRecFn rec_deep[2][4];      // Horner mixing, [depth 2 / 3 inputs in flight][NS]
   BsDescFn rec_desc_deep[2][4];
@@ -475,11 +447,6 @@ constexpr BsDescFn rec_desc_fn() {
 template <class C, int NS>
 constexpr BsDesc4Fn rec_desc4_fn() {
   if constexpr (NS <= C::p) return bitslice_recon_desc_w4_kernel<C, NS>;
-  else return nullptr;
-}
-template <class C, int DBG>
-constexpr BsDesc4Fn rec_desc4_pair_fn() {
-  if constexpr (C::p >= 8) return bitslice_recon_desc_pair_w4_kernel<C, DBG>;
   else return nullptr;
 }
 template <class C, int NS>
@@ -539,7 +506,6 @@ constexpr BsDescFn rec_desc_deep_fn() {
     {rec_fn<C, 1, 3>(), rec_fn<C, 2, 3>(), rec_fn<C, 4, 3>(), rec_fn<C, 8, 3>()}}, \
    {rec_desc_fn<C, 1>(), rec_desc_fn<C, 2>(), rec_desc_fn<C, 4>(), rec_desc_fn<C, 8>()},   \
    {rec_desc4_fn<C, 1>(), rec_desc4_fn<C, 2>(), rec_desc4_fn<C, 4>(), rec_desc4_fn<C, 8>()}, \
-   {rec_desc4_pair_fn<C, 0>(), rec_desc4_pair_fn<C, 4>()},                                 \
    {rec4_fn<C, 1>(), rec4_fn<C, 2>(), rec4_fn<C, 4>(), rec4_fn<C, 8>()},                 \
    {{rec_deep_fn<C, 1, 2>(), rec_deep_fn<C, 2, 2>(), rec_deep_fn<C, 4, 2>(),           \
      rec_deep_fn<C, 8, 2>()},                                                          \
@@ -895,7 +861,6 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
   BsDesc4Fn sfn4 = nullptr;
   hipFunction_t jfn = nullptr, jfn4 = nullptr;
   bool compiled = false, pairs = false;
-  BsDesc4Fn pfn4 = nullptr;  // 4 KiB chunks at 8 sigma rows on wave pairs
   for (const BsShape& sh : kBsShapes) {
     if (sh.field != field || sh.k != k || sh.p != p) continue;
     compiled = true;
@@ -909,8 +874,6 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
         if (q == 3 && pair_groups(field) && sh.rec_desc_pair[pair_slot(field)] && depth == 1) {
           sfn = sh.rec_desc_pair[pair_slot(field)];  // 8 sigma rows on wave pairs
           pairs = true;
-          const int64_t w4p = get_option(54);  // RSE_OPT_RECON_W4_PAIRS
-          if (w4p > 0) pfn4 = sh.rec_desc4_pair[w4p > 1 ? 1 : 0];
         }
         if (pairs)
           note_kernel("bitslice-recon-batch gf%d %u+%u ns8 pairs%d", field, k, p, pair_groups(field));
@@ -963,15 +926,7 @@ hipError_t launch_bitslice_recon_batch(int field, uint32_t k, uint32_t p,
     *done = base4;
     count_bitslice_launch();
   }
-  if (cps4 && pfn4) {  // one 4 KiB column per 128-lane pair workgroup
-    const uint64_t gx = grid_for(cps4 * ns);
-    hipLaunchKernelGGL(pfn4, dim3((uint32_t)gx), dim3(128), 0, stream, (const BsReconArgs*)d_descs,
-                       cps4, ns, base4);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    *done = base4 + cps4 * 4096u;
-    if (!cps) count_bitslice_launch();
-  } else if (cps4 && (sfn4 || jfn4)) {
+  if (cps4 && (sfn4 || jfn4)) {
     const uint64_t gx = grid_for((cps4 * ns + 3) / 4);
     if (sfn4) {
       hipLaunchKernelGGL(sfn4, dim3((uint32_t)gx), dim3(kBsBlock), 0, stream,

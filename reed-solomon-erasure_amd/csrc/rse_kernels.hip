@@ -810,7 +810,6 @@ struct Options {
   int64_t fft = 1;  // GF(2^8) k = p = 16 / 32 / 64 codecs on the additive-FFT kernels (rse_fft.hip)
   int64_t host_queues = 1;  // host pipeline: 1 the D2H stream at high priority, 0 plain (A/B)
   int64_t host_zc_out = 1;  // host pipeline: outputs stored in place in mapped pinned memory
-  int64_t recon_w4_pairs = 2;  // batch reconstruct, 4 KiB chunks at 8 rows: wave pairs (1, 2: depth)
 };
 thread_local int64_t g_bs_launches = 0;  // bit-sliced launches on this thread (RSE_OPT 6)
 Options g_opt;
@@ -1362,7 +1361,6 @@ int set_option(int key, int64_t value) {
     case 51: g_opt.fft = value ? 1 : 0; return 0;
     case 52: g_opt.host_queues = value ? 1 : 0; return 0;
     case 53: g_opt.host_zc_out = value ? 1 : 0; return 0;
-    case 54: g_opt.recon_w4_pairs = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
 #ifdef RSE_TUNE_SPLITS
     case 47: g_opt.tune_nosync = value ? 1 : 0; return 0;  // rse_jit.cpp make_source
 #endif
@@ -1427,7 +1425,6 @@ int64_t get_option(int key) {
     case 51: return g_opt.fft;
     case 52: return g_opt.host_queues;
     case 53: return g_opt.host_zc_out;
-    case 54: return g_opt.recon_w4_pairs;
 #ifdef RSE_TUNE_SPLITS
     case 47: return g_opt.tune_nosync;
 #endif

@@ -617,55 +617,6 @@ def test_reconstruct_batch_per_stripe_patterns(R, subfield, field, k, p, n, stri
     lib.rse_set_option(9, old_jit)
 
 
-@pytest.mark.parametrize("w4p", [0, 1, 2])
-@pytest.mark.parametrize("n_elems", [2048, 10240])
-def test_reconstruct_batch_4k_chunks_on_wave_pairs(R, w4p, n_elems):
-    """RSE_OPT_RECON_W4_PAIRS: rse_reconstruct_batch of GF(2^16) 20+8 (the
-    compiled subfield codec) over 4 KiB chunks -- 4 KiB shards, and the tail of
-    20 KiB ones past their 16 KiB chunk -- at 8 sigma rows: one wave holding
-    every row (0), or wave pairs with one (1) or two (2, the default) own inputs
-    in flight.  Every stripe its own pattern of 1..8 losses (lost parity rows
-    past the fourth force 8 rows), reconstruct and reconstruct_data, against
-    the oracle stripe by stripe."""
-    lib = R._lib.load()
-    old = lib.rse_get_option(54)
-    field, k, p, stripes = 16, 20, 8, 37
-    T, nb = k + p, 2 * n_elems
-    rng = np.random.default_rng(4000 + n_elems + w4p)
-    oc = O.Codec(field, k, p)
-    full = np.zeros((stripes, T, nb), np.uint8)
-    for s_ in range(stripes):
-        sh = rand_shards(rng, k, nb) + [np.zeros(nb, np.uint8) for _ in range(p)]
-        oc.encode(sh)
-        full[s_] = np.stack(sh)
-    r = R.core.ReedSolomon(k, p, field)
-    try:
-        assert lib.rse_set_option(54, w4p) == 0
-        for data_only in (False, True):
-            present = np.ones((stripes, T), bool)
-            for s_ in range(stripes):
-                ne = 1 + s_ % p
-                present[s_, rng.choice(T, ne, replace=False)] = False
-            present[0, k + 6] = False  # a parity row past the fourth: 8 sigma rows
-            v = full.copy()
-            v[~present] = 0x5A
-            want = v.copy()
-            for s_ in range(stripes):
-                ob = [want[s_, i].copy() for i in range(T)]
-                oc.reconstruct(ob, present[s_].tolist(), data_only=data_only)
-                want[s_] = np.stack(ob)
-            d = dev(v.reshape(-1))
-            n0 = lib.rse_get_option(6)
-            r.reconstruct_batch(d, n_elems, stripes, present, data_only=data_only)
-            got = host(d).reshape(stripes, T, nb)
-            assert lib.rse_get_option(6) - n0 == 1, data_only
-            from reed_solomon_erasure.core import last_kernel
-            assert "ns8 pairs" in last_kernel(), last_kernel()
-            assert (got == want).all(), data_only
-    finally:
-        lib.rse_set_option(54, old)
-
-
 @pytest.mark.parametrize("field,k,p", [(8, 10, 4), (16, 20, 8)])
 @pytest.mark.parametrize("dflags", [False, True])
 def test_reconstruct_batch_parity_only_losses(R, field, k, p, dflags):
