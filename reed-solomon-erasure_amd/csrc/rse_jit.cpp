@@ -23,6 +23,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -801,10 +802,35 @@ int status_of(Entry* e, bool wait) {
 // for the kJitBlock modules (~4.5x the algorithmic bytes at 1000+24).
 // RSE_OPT_WIDE_BLOCK_INPUTS caps the data inputs per block (hiprtc time grows
 // with the module); blocks are balanced.
+//
+// Past one module's 64 outputs (round 6): the outputs split into balanced
+// groups of at most 64, each coded on its own over every input -- one wide
+// module when the group fits one (k + 2 np <= 480 and k within
+// RSE_OPT_WIDE_BLOCK_INPUTS: GF(2^8) 128+128 is two modules of 128 inputs x 64
+// outputs), else a chain as above.  Every input is read once per group and
+// every output written once (plus the chain's re-reads), against once per 8
+// outputs for the 8 x 32 block modules.
 struct WideBlock {
-  uint32_t i0, ni, kk;          // data inputs i0..i0+ni, module inputs kk (ni, or ni + p)
-  std::vector<uint16_t> rows;   // p x kk
+  uint32_t o0, np;              // the output group: outputs o0..o0+np of the codec
+  uint32_t i0, ni, kk;          // data inputs i0..i0+ni, module inputs kk (ni, or ni + np)
+  bool first;                   // the group's first block (it stores; later ones add)
+  std::vector<uint16_t> rows;   // np x kk
 };
+
+// A chain's length over k inputs for p outputs, or 0; fits: also when one
+// module would hold them (an output group with k past the block limit).
+uint32_t chain_len(uint32_t k, uint32_t p, bool fits) {
+  const int64_t lim = get_option(46);
+  if (lim <= 0 || k == 0 || p == 0 || (!fits && wide_eligible(k, p)) || 3u * p >= kWideMaxPtrs)
+    return 0;
+  const uint32_t kmax = (uint32_t)std::min<int64_t>(lim, (int64_t)(kWideMaxPtrs - 3u * p));
+  const uint32_t n = (k + kmax - 1) / kmax;
+  if (n < 2) return 0;
+  const uint32_t base = k / n;  // blocks of base or base + 1 inputs
+  if (!wide_eligible(base, p) || !wide_eligible(base + p, p) || !wide_eligible(base + 1 + p, p))
+    return 0;
+  return n;
+}
 
 bool wide_blocks_plan_impl(uint32_t k, uint32_t p, uint32_t* nb) {
   const int64_t lim = get_option(46);
@@ -819,12 +845,16 @@ bool wide_blocks_plan_impl(uint32_t k, uint32_t p, uint32_t* nb) {
   return true;
 }
 
-std::vector<WideBlock> wide_blocks_of(uint32_t k, uint32_t p, const uint16_t* rows, uint32_t n) {
+std::vector<WideBlock> wide_blocks_of(uint32_t k, uint32_t p, const uint16_t* rows, uint32_t n,
+                                      uint32_t o0 = 0) {
   std::vector<WideBlock> v(n);
   const uint32_t base = k / n, extra = k % n;
   uint32_t i0 = 0;
   for (uint32_t b = 0; b < n; ++b) {
     WideBlock& w = v[b];
+    w.o0 = o0;
+    w.np = p;
+    w.first = b == 0;
     w.i0 = i0;
     w.ni = base + (b < extra ? 1u : 0u);
     w.kk = w.ni + (b ? p : 0u);
@@ -834,6 +864,55 @@ std::vector<WideBlock> wide_blocks_of(uint32_t k, uint32_t p, const uint16_t* ro
       if (b) w.rows[(size_t)o * w.kk + w.ni + o] = 1;  // the output's sum so far
     }
     i0 += w.ni;
+  }
+  return v;
+}
+
+// The output groups of a p x k matrix: {o0, np, modules}; false when neither
+// the chain of every output nor groups of <= 64 outputs apply.
+bool wide_groups_of(uint32_t k, uint32_t p, std::vector<std::array<uint32_t, 3>>* g) {
+  g->clear();
+  uint32_t nb = 0;
+  if (wide_blocks_plan_impl(k, p, &nb)) {  // p <= 64: one chain (round 5, unchanged)
+    g->push_back({0u, p, nb});
+    return true;
+  }
+  const int64_t lim = get_option(46);
+  if (lim <= 0 || k == 0 || p <= kJitMaxOut * 8u || wide_eligible(k, p)) return false;
+  const uint32_t G = (p + kJitMaxOut * 8u - 1) / (kJitMaxOut * 8u), base = p / G, extra = p % G;
+  uint32_t o0 = 0;
+  for (uint32_t i = 0; i < G; ++i) {
+    const uint32_t np = base + (i < extra ? 1u : 0u);
+    const uint32_t n = (int64_t)k <= lim && wide_eligible(k, np) ? 1u : chain_len(k, np, true);
+    if (n == 0) return false;
+    g->push_back({o0, np, n});
+    o0 += np;
+  }
+  return true;
+}
+
+// Every module of the plan, group by group.
+std::vector<WideBlock> wide_plan_blocks(uint32_t k, uint32_t p, const uint16_t* rows,
+                                        const std::vector<std::array<uint32_t, 3>>& g) {
+  std::vector<WideBlock> v;
+  std::vector<uint16_t> gr;
+  for (const auto& x : g) {
+    const uint32_t o0 = x[0], np = x[1], n = x[2];
+    gr.assign(rows + (size_t)o0 * k, rows + (size_t)(o0 + np) * k);
+    if (n == 1) {  // one module over every input
+      WideBlock w;
+      w.o0 = o0;
+      w.np = np;
+      w.first = true;
+      w.i0 = 0;
+      w.ni = k;
+      w.kk = k;
+      w.rows = gr;
+      v.push_back(std::move(w));
+    } else {
+      std::vector<WideBlock> c = wide_blocks_of(k, np, gr.data(), n, o0);
+      for (auto& w : c) v.push_back(std::move(w));
+    }
   }
   return v;
 }
@@ -865,14 +944,14 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
   if (get_option(9) == 0 || (field != 8 && field != 16) || k == 0 || p == 0) return 0;
   registry();
   Worker& w = worker();
-  uint32_t nb = 0;
-  if (wide_blocks_plan_impl(k, p, &nb)) {
-    const std::vector<WideBlock> bl = wide_blocks_of(k, p, rows, nb);
+  std::vector<std::array<uint32_t, 3>> groups;
+  if (wide_groups_of(k, p, &groups)) {
+    const std::vector<WideBlock> bl = wide_plan_blocks(k, p, rows, groups);
     std::lock_guard<std::mutex> g(g_mu);
     int need = 0, pending = 0;
     for (const WideBlock& b : bl)
-      if (!find_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide)) {
-        need += (int)(((b.kk + kMaxIn - 1) / kMaxIn) * ((p + kJitMaxOut - 1) / kJitMaxOut));
+      if (!find_locked(field, b.kk, b.np, b.rows.data(), b.kk, kJitWide)) {
+        need += (int)(((b.kk + kMaxIn - 1) / kMaxIn) * ((b.np + kJitMaxOut - 1) / kJitMaxOut));
         ++pending;
       }
     if (need == 0) return 1;
@@ -881,8 +960,8 @@ int jit_register_blocks(int field, uint32_t k, uint32_t p, const uint16_t* rows,
                 : g_blocks + need > kMaxBlocks)
       return 0;
     for (const WideBlock& b : bl)
-      if (!find_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide))
-        add_locked(field, b.kk, p, b.rows.data(), b.kk, kJitWide, pattern);
+      if (!find_locked(field, b.kk, b.np, b.rows.data(), b.kk, kJitWide))
+        add_locked(field, b.kk, b.np, b.rows.data(), b.kk, kJitWide, pattern);
     w.start();
     g_cv.notify_all();
     return 1;
@@ -1057,10 +1136,10 @@ hipError_t launch_wide(int field, uint32_t k, uint32_t p, const uint16_t* rows,
 
 int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, bool wait) {
   int worst = 2;
-  uint32_t nb = 0;
-  if (wide_blocks_plan_impl(k, p, &nb)) {
-    for (const WideBlock& b : wide_blocks_of(k, p, rows, nb)) {
-      const int s = status_of(find_entry(field, b.kk, p, b.rows.data(), b.kk, kJitWide), wait);
+  std::vector<std::array<uint32_t, 3>> groups;
+  if (wide_groups_of(k, p, &groups)) {
+    for (const WideBlock& b : wide_plan_blocks(k, p, rows, groups)) {
+      const int s = status_of(find_entry(field, b.kk, b.np, b.rows.data(), b.kk, kJitWide), wait);
       if (s < worst) worst = s;
       if (worst <= 0) break;
     }
@@ -1075,8 +1154,10 @@ int jit_blocks_status(int field, uint32_t k, uint32_t p, const uint16_t* rows, b
 }
 
 bool wide_blocks_plan(uint32_t k, uint32_t p, uint32_t* n_blocks) {
+  std::vector<std::array<uint32_t, 3>> groups;
+  const bool ok = wide_groups_of(k, p, &groups);
   uint32_t nb = 0;
-  const bool ok = wide_blocks_plan_impl(k, p, &nb);
+  for (const auto& x : groups) nb += x[2];
   if (n_blocks) *n_blocks = ok ? nb : 0;
   return ok;
 }
@@ -1086,30 +1167,35 @@ hipError_t launch_wide_blocks(int field, uint32_t k, uint32_t p, const uint16_t*
                               uint64_t stripe_stride, uint32_t n_stripes, hipStream_t stream,
                               uint64_t* done) {
   *done = 0;
-  uint32_t nb = 0;
-  if (!wide_blocks_plan_impl(k, p, &nb) || n_stripes == 0) return hipSuccess;
-  const std::vector<WideBlock> bl = wide_blocks_of(k, p, rows, nb);
+  std::vector<std::array<uint32_t, 3>> groups;
+  if (!wide_groups_of(k, p, &groups) || n_stripes == 0) return hipSuccess;
+  const std::vector<WideBlock> bl = wide_plan_blocks(k, p, rows, groups);
   const bool wait = get_option(9) >= 2;
   for (const WideBlock& b : bl)  // every module built, or none is launched
-    if (status_of(find_entry(field, b.kk, p, b.rows.data(), b.kk, kJitWide), wait) != 2)
+    if (status_of(find_entry(field, b.kk, b.np, b.rows.data(), b.kk, kJitWide), wait) != 2)
       return hipSuccess;
   std::vector<const uint8_t*> ins;
   uint64_t d0 = 0;
   for (size_t bi = 0; bi < bl.size(); ++bi) {
     const WideBlock& b = bl[bi];
     ins.assign(in + b.i0, in + b.i0 + b.ni);
-    if (bi) ins.insert(ins.end(), out, out + p);
+    if (!b.first) ins.insert(ins.end(), out + b.o0, out + b.o0 + b.np);  // the group's sums so far
     uint64_t d = 0;
-    const hipError_t he = launch_wide(field, b.kk, p, b.rows.data(), ins.data(), out, nullptr, len,
-                                      stripe_stride, n_stripes, kStore, nullptr, false, stream, &d);
+    const hipError_t he = launch_wide(field, b.kk, b.np, b.rows.data(), ins.data(), out + b.o0,
+                                      nullptr, len, stripe_stride, n_stripes, kStore, nullptr,
+                                      false, stream, &d);
     if (he != hipSuccess) return he;
     // every block codes the same whole chunks (same length, every module built)
     if (bi == 0) d0 = d;
     else if (d != d0) return hipErrorInvalidValue;
     if (d0 == 0) return hipSuccess;
   }
-  note_kernel("bitslice-wide-blocks gf%d %u+%u x%u (%u+%u w%d)", field, k, p, nb, bl[0].ni, p,
-              wide_waves(p));
+  if (groups.size() == 1)
+    note_kernel("bitslice-wide-blocks gf%d %u+%u x%u (%u+%u w%d)", field, k, p, groups[0][2],
+                bl[0].ni, p, wide_waves(p));
+  else
+    note_kernel("bitslice-wide-groups gf%d %u+%u g%u x%u (%u+%u w%d)", field, k, p,
+                (uint32_t)groups.size(), groups[0][2], bl[0].ni, bl[0].np, wide_waves(bl[0].np));
   *done = d0;
   return hipSuccess;
 }

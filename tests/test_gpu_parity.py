@@ -1498,12 +1498,13 @@ def test_bench_ranks_rehearsal(ranks, extras, tmp_path):
         assert h["ranks"] == ranks and h["parity_matches_device_all_ranks"] is True
 
 
-# (field, k, p, modules): one wide module (p <= 64, k + 2p <= 480), or
-# blocks of 8 outputs x 32 inputs beyond that.  Waves per workgroup
+# (field, k, p, modules): one wide module (p <= 64, k + 2p <= 480), or past
+# 64 outputs one module per output group of <= 64 (round 6; 8 x 32 blocks
+# before).  Waves per workgroup
 # (rse_jit.cpp wide_waves): 1 for p < 4, else 4 (p <= 32), 8 (10+40: shares
 # of 5; 4+17: 5/4/4/4), or 16 for GF(2^8) past 48 outputs (64+64: 4 each).
 WIDE_CODECS = [(8, 40, 2, 1), (8, 6, 10, 1), (16, 36, 3, 1), (8, 33, 9, 1), (16, 20, 12, 1),
-               (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 9),
+               (8, 10, 40, 1), (16, 4, 17, 1), (8, 4, 66, 2),  # 66 outputs: two groups of 33
                (8, 32, 32, 1), (8, 64, 64, 1)]  # benches/bandwidth.rs:94-95's widest (half chunks)
 
 
@@ -1623,6 +1624,69 @@ def test_wide_codec_kernels(R, subfield, field, k, p, modules):
     finally:
         lib.rse_set_option(9, old)
         lib.rse_set_option(51, old51)
+
+
+@pytest.mark.parametrize("k,p,lim,modules", [(20, 70, 128, 2), (40, 70, 16, 6), (128, 128, 128, 2)])
+def test_wide_output_groups(R, k, p, lim, modules):
+    """Past one wide module's 64 outputs (round 6): the outputs split into
+    balanced groups of <= 64, each coded over every input by one wide module
+    (20+70: two of 20 x 35; GF(2^8)'s widest, 128+128: two of 128 x 64), or --
+    past RSE_OPT_WIDE_BLOCK_INPUTS inputs (here 16) -- by a chain over input
+    blocks writing the group's outputs at their offset (40+70: two chains of
+    three).  Encode (one launch per module), verify, a 3-stripe encode_flat,
+    and a first-use reconstruct of more than 64 lost shards, against the
+    oracle."""
+    lib = R._lib.load()
+    field, nbytes = 8, 16384 + 4096 + 48
+    rng = np.random.default_rng(k * 1000 + p)
+    oc = O.Codec(field, k, p)
+    full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
+    oc.encode(full)
+    old = [lib.rse_get_option(x) for x in (9, 46)]
+    try:
+        assert lib.rse_set_option(9, 2) == 0
+        assert lib.rse_set_option(46, lim) == 0
+        r = R.core.ReedSolomon(k, p, field)
+        assert r.kernel_kind(wait=True) == "bitslice-specialised"
+        t = [dev(x) for x in full[:k]] + [torch.full((nbytes,), 0x5A, dtype=torch.uint8,
+                                                     device="cuda") for _ in range(p)]
+        n0 = lib.rse_get_option(6)
+        r.encode(t)
+        torch.cuda.synchronize()
+        from reed_solomon_erasure.core import last_kernel
+        assert lib.rse_get_option(6) - n0 == modules, last_kernel()
+        assert last_kernel().startswith(f"bitslice-wide-groups gf8 {k}+{p} g2"), last_kernel()
+        for i in range(p):
+            assert (host(t[k + i]) == full[k + i]).all(), i
+        assert r.verify(t)
+        t[k + p - 1][9000] ^= 1
+        assert not r.verify(t)
+        t[k + p - 1][9000] ^= 1
+        stripes = 3
+        flat = torch.full((stripes, k + p, nbytes), 0xA5, dtype=torch.uint8, device="cuda")
+        for s_ in range(stripes):
+            for i in range(k):
+                flat[s_, i] = dev(np.roll(full[i], s_))
+        r.encode_flat(flat, nbytes, stripes)
+        got = host(flat)
+        for s_ in range(stripes):
+            sh = [np.roll(full[i], s_) for i in range(k)] + [np.zeros(nbytes, np.uint8)
+                                                              for _ in range(p)]
+            oc.encode(sh)
+            for i in range(p):
+                assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
+        # more than 64 shards lost, first use of the pattern (RSE_OPT_JIT 1:
+        # syndrome / table kernels, no decode-pattern build)
+        assert lib.rse_set_option(9, 1) == 0
+        lost = sorted(rng.choice(k + p, p, replace=False).tolist())
+        for i in lost:
+            t[i].fill_(0)
+        r.reconstruct([(x, i not in lost) for i, x in enumerate(t)])
+        for i in range(k + p):
+            assert (host(t[i]) == full[i]).all(), (i, i in lost)
+    finally:
+        lib.rse_set_option(9, old[0])
+        lib.rse_set_option(46, old[1])
 
 
 def test_wide_block_chain_gf16_past_256(R):

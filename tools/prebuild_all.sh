@@ -27,9 +27,12 @@ python3 tools/prebuild_jit.py --set 38=0 --codec 8:34:10 || exit 1
 # 16+16 .. 64+64's wide modules (RSE_OPT_FFT 0: tests/test_gpu_parity.py
 # test_wide_codec_kernels, test_sub_chunk_shards; the default is the FFT kernels)
 python3 tools/prebuild_jit.py --set 51=0 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 || exit 1
+# tests/test_gpu_parity.py test_wide_output_groups: past 64 outputs, groups
+# of <= 64 (one module each; 40+70 with 16-input blocks: chains of three)
+python3 tools/prebuild_jit.py --set 46=16 --codec 8:40:70 || exit 1
 # test_wide_sixteen_waves: 4 outputs per wave (a 16-wave module)
 python3 tools/prebuild_jit.py --set 18=4 --codec 8:60:60 || exit 1
-exec python3 tools/prebuild_jit.py --codec 8:35:10 \
+exec python3 tools/prebuild_jit.py --codec 8:35:10 --codec 8:20:70 --codec 8:128:128 --codec 8:4:66 \
   --codec 8:50:20 --codec 16:40:12 --codec 16:100:30 \
   --codec 8:4:4 --codec 8:8:8 --codec 8:16:16 --codec 8:32:32 --codec 8:64:64 --codec 8:5:2 \
   --codec 8:12:4 --codec 16:6:3 --codec 8:6:3 --codec 8:32:8 --codec 8:17:5 --codec 16:1000:24 \
