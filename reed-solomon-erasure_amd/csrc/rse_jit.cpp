@@ -118,7 +118,7 @@ int g_patterns = 0;  // decode-pattern entries (capped: max_patterns)
 int max_patterns() { return (int)std::min<int64_t>(get_option(35), 1 << 30); }
 int max_pattern_blocks() { return (int)std::min<int64_t>(get_option(36), 1 << 30); }
 int g_blocks = 0;  // wide-codec block entries (capped: kMaxBlocks)
-constexpr int kMaxBlocks = 256;
+constexpr int kMaxBlocks = 1024;  // 128+128: 64, GF(2^16) 1000+24: 120
 // blocks of wide decode patterns: a separate budget, so patterns can never
 // use up the codecs' own (and never queue more than a few patterns' builds)
 int g_pattern_blocks = 0;
