@@ -214,7 +214,9 @@ def test_run_time_specialisation_builds_on_cpu():
 def test_wide_codec_modules_build_on_cpu():
     """Wide codecs (k > 32 or p > 8) get one module each (every wave of a
     workgroup codes its share of <= 8 outputs over all inputs); past 64
-    outputs, one module per 8 x 32 block of the parity rows."""
+    outputs, one module per balanced group of <= 64 outputs (round 6; one
+    per 8 x 32 block of the parity rows before), and with
+    RSE_OPT_WIDE_BLOCK_INPUTS 0 the 8 x 32 blocks again."""
     built = L.rse_get_option(10)
     assert R.galois_8.ReedSolomon(6, 10).kernel_kind(wait=True) == "bitslice-specialised"
     assert L.rse_get_option(10) == built + 1
@@ -223,7 +225,15 @@ def test_wide_codec_modules_build_on_cpu():
     assert L.rse_get_option(10) == built + 1
     built = L.rse_get_option(10)
     assert R.galois_8.ReedSolomon(2, 65).kernel_kind(wait=True) == "bitslice-specialised"
-    assert L.rse_get_option(10) == built + 9  # 9 output blocks of <= 8
+    assert L.rse_get_option(10) == built + 2  # output groups of 33 and 32
+    built = L.rse_get_option(10)
+    old = L.rse_get_option(46)
+    try:
+        assert L.rse_set_option(46, 0) == 0
+        assert R.galois_8.ReedSolomon(3, 65).kernel_kind(wait=True) == "bitslice-specialised"
+        assert L.rse_get_option(10) == built + 9  # 9 output blocks of <= 8
+    finally:
+        L.rse_set_option(46, old)
 
 
 def _py(code, env, timeout=600):
