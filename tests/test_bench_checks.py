@@ -275,3 +275,39 @@ def test_printed_line_reports_a_false_flag_and_still_fits(tmp_path, capsys):
     assert len(last.encode()) < 4096 and json.loads(last) == got
     assert got["checks"]["all_true"] is False
     assert got["checks"]["false"][0].startswith("reference_bench_matrix.entries[3]")
+
+
+def test_host_agreement_flag():
+    """The two pinned-host flat encode legs must agree within 10 % (VERDICT r05
+    §4): the flag is true for 66.0 k / 65.7 k MB/s, false for round 5's
+    39.6 k / 72.6 k, and the ratio to plain duplex copies is a number, not a
+    correctness flag.  Nothing is added when a leg did not run or the job had
+    several ranks."""
+    def extras(flat, ranks_mb, ranks=1):
+        return {"end_to_end_host_all_ranks": {"MB_per_s_all_ranks": ranks_mb, "ranks": ranks},
+                "end_to_end_pinned_host_flat": {"MB_per_s": flat,
+                                                "raw_pinned_duplex_MB_per_s": 76000.0}}
+    e = extras(66000.0, 65700.0)
+    bench.host_agreement(e)
+    f = e["end_to_end_pinned_host_flat"]
+    assert f["host_flat_legs_agree_within_10pct"] is True
+    assert f["vs_raw_duplex"] == round(66000.0 / 76000.0, 3)
+    assert ("end_to_end_pinned_host_flat.host_flat_legs_agree_within_10pct", True) in \
+        bench.correctness_flags(e)
+    assert not [x for x in bench.correctness_flags(e) if "duplex" in x[0]]
+    e = extras(39600.0, 72600.0)
+    bench.host_agreement(e)
+    assert e["end_to_end_pinned_host_flat"]["host_flat_legs_agree_within_10pct"] is False
+    e = extras(39600.0, 72600.0, ranks=2)
+    bench.host_agreement(e)
+    assert "host_flat_legs_agree_within_10pct" not in e["end_to_end_pinned_host_flat"]
+    e = {"end_to_end_pinned_host_flat": {"MB_per_s": 1.0}}
+    bench.host_agreement(e)
+    assert e == {"end_to_end_pinned_host_flat": {"MB_per_s": 1.0}}
+
+
+def test_warm_calls_runs_for_the_time_given():
+    n = []
+    t0 = time.perf_counter()
+    bench.warm_calls(lambda: n.append(1), seconds=0.05)
+    assert time.perf_counter() - t0 >= 0.05 and len(n) >= 2
