@@ -1689,7 +1689,8 @@ def test_wide_output_groups(R, k, p, lim, modules):
         lib.rse_set_option(46, old[1])
 
 
-def test_wide_block_chain_gf16_past_256(R):
+@pytest.mark.parametrize("lim,label", [(128, "x8 (125+24"), (400, "x3 (333+24")])
+def test_wide_block_chain_gf16_past_256(R, lim, label):
     """GF(2^16) 1000+24 (k + 2p > 480: too wide for one wide module's pointer
     block) on a chain of wide modules over input blocks (rse_jit.cpp;
     RSE_OPT_WIDE_BLOCK_INPUTS 128: 8 blocks of 125 data shards), each coding
@@ -1707,18 +1708,21 @@ def test_wide_block_chain_gf16_past_256(R):
     full = rand_shards(rng, k, nbytes) + [np.zeros(nbytes, np.uint8) for _ in range(p)]
     oc.encode(full)
     old = lib.rse_get_option(9)
+    old46 = lib.rse_get_option(46)
     try:
         assert lib.rse_set_option(9, 2) == 0
+        assert lib.rse_set_option(46, lim) == 0  # data inputs per chain block
         r = R.core.ReedSolomon(k, p, 16)
-        assert kernels_or_skip(r, "GF(2^16) 1000+24") == "bitslice-specialised"
+        assert kernels_or_skip(r, f"GF(2^16) 1000+24, blocks of <= {lim}") == \
+            "bitslice-specialised"
         t = [dev(x).reshape(n_elems, 2) for x in full[:k]] + \
             [torch.full((n_elems, 2), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(p)]
         n0 = lib.rse_get_option(6)
         r.encode(t)
         torch.cuda.synchronize()
-        assert lib.rse_get_option(6) - n0 == 8
+        assert lib.rse_get_option(6) - n0 == int(label[1])
         from reed_solomon_erasure.core import last_kernel
-        assert last_kernel().startswith("bitslice-wide-blocks gf16 1000+24 x8 (125+24"), last_kernel()
+        assert last_kernel().startswith(f"bitslice-wide-blocks gf16 1000+24 {label}"), last_kernel()
         for i in range(p):
             assert (host(t[k + i]).reshape(-1) == full[k + i]).all(), i
         assert r.verify(t)
@@ -1743,6 +1747,7 @@ def test_wide_block_chain_gf16_past_256(R):
                 assert (got[s_, k + i] == sh[k + i]).all(), (s_, i)
     finally:
         lib.rse_set_option(9, old)
+        lib.rse_set_option(46, old46)
 
 
 @pytest.mark.parametrize("nbytes,stripes", [(1024, 5), (1024, 8), (2048, 3)])
@@ -1762,7 +1767,8 @@ def test_wide_block_chain_gf16_short_shards(R, nbytes, stripes):
     try:
         assert lib.rse_set_option(9, 2) == 0
         r = R.core.ReedSolomon(k, p, 16)
-        assert kernels_or_skip(r, "GF(2^16) 1000+24") == "bitslice-specialised"
+        assert kernels_or_skip(r, "GF(2^16) 1000+24, blocks of <= 128") == \
+            "bitslice-specialised"
         buf = rng.integers(0, 256, (stripes + 1) * T * nbytes, dtype=np.uint8)
         d = dev(buf)
         n0 = lib.rse_get_option(6)
