@@ -1689,7 +1689,7 @@ def test_wide_output_groups(R, k, p, lim, modules):
         lib.rse_set_option(46, old[1])
 
 
-@pytest.mark.parametrize("lim,label", [(128, "x8 (125+24"), (400, "x3 (333+24")])
+@pytest.mark.parametrize("lim,label", [(128, "x8 (125+24"), (400, "x3 (334+24")])
 def test_wide_block_chain_gf16_past_256(R, lim, label):
     """GF(2^16) 1000+24 (k + 2p > 480: too wide for one wide module's pointer
     block) on a chain of wide modules over input blocks (rse_jit.cpp;
