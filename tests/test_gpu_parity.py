@@ -1697,8 +1697,11 @@ def test_wide_block_chain_gf16_past_256(R, lim, label):
     all 24 outputs, the blocks after the first reading the sums so far as 24
     more inputs.  Encode (whole 4 KiB chunks on the chain, a table-coded tail),
     verify (sums materialised through the chain, then compared) and a
-    2-stripe encode_flat against the oracle.  The modules come from the
-    tree's jitcache (tools/prebuild_all.sh)."""
+    2-stripe encode_flat against the oracle; also on 3 blocks of 333-334
+    inputs (RSE_OPT_WIDE_BLOCK_INPUTS 400).  The modules come from the tree's
+    jitcache (tools/prebuild_all.sh builds the default chain's; the 400-input
+    ones, ~145 minutes of hiprtc, were built by hand: without them that case
+    skips)."""
     lib = R._lib.load()
     k, p = 1000, 24
     nbytes = 2 * 4096 + 96
